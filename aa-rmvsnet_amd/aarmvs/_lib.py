@@ -1,0 +1,82 @@
+"""ctypes binding of libaarmvs.so (the C ABI declared in include/aarmvs.h).
+
+The library is built in-tree by ``make -C aa-rmvsnet_amd/csrc`` (or
+``__graft_entry__.build()``).  There is no fallback: if the shared object is
+missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+MAX_SRC = 16
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libaarmvs.so")
+
+c_int, c_size_t, c_void_p, c_char_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
+
+
+class SweepArgs(ctypes.Structure):
+    """Mirror of ``aarmvs_sweep_args``."""
+    _fields_ = [
+        ("B", c_int), ("C", c_int), ("H", c_int), ("W", c_int),
+        ("nsrc", c_int), ("D", c_int), ("d_begin", c_int), ("d_end", c_int),
+        ("ref_fea", c_void_p),
+        ("src_fea", c_void_p * MAX_SRC),
+        ("rel_proj", c_void_p),
+        ("depth_values", c_void_p),
+        ("packed_params", c_void_p),
+        ("workspace", c_void_p),
+        ("depth_out", c_void_p),
+        ("conf_out", c_void_p),
+        ("cost_out", c_void_p),
+        ("slice_out", c_void_p),
+        ("omega_out", c_void_p),
+    ]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "aarmvs_last_error": (c_char_p, []),
+    "aarmvs_version": (c_char_p, []),
+    "aarmvs_param_count": (c_size_t, []),
+    "aarmvs_packed_param_bytes": (c_size_t, []),
+    "aarmvs_pack_params": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "aarmvs_homo_warp": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                 c_void_p, c_void_p]),
+    "aarmvs_sweep_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "aarmvs_sweep": (c_int, [ctypes.POINTER(SweepArgs), c_void_p]),
+    "aarmvs_state_ptr": (c_void_p, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    "aarmvs_unet_step": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p, c_void_p]),
+    "aarmvs_softmax_depth": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+}
+
+_LIB = None
+
+
+class AarmvsError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the configured CDLL.  Raises if it is not built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise AarmvsError(
+                f"libaarmvs.so not found at {LIB_PATH}: build it with "
+                "`make -C aa-rmvsnet_amd/csrc` (hipcc, gfx950). There is no CPU fallback.")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = handle
+    return _LIB
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().aarmvs_last_error().decode(errors="replace")
+        raise AarmvsError(f"{what} failed (status {rc}): {msg}")

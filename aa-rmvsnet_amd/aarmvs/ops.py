@@ -1,0 +1,178 @@
+"""Torch-facing wrappers of the HIP depth-sweep library.
+
+Tensors stay on the device (PyTorch's caching allocator owns every buffer);
+launches go to ``torch.cuda.current_stream()``.  All functions raise
+``AarmvsError`` for CPU tensors or when libaarmvs.so is missing: the product
+path has no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import AarmvsError, check, lib
+from .synthetic import SWEEP_SHAPES
+
+SWEEP_KEYS = tuple(SWEEP_SHAPES.keys())  # raw-blob order (include/aarmvs.h)
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _require_device(*ts: torch.Tensor) -> None:
+    for t in ts:
+        if not t.is_cuda:
+            raise AarmvsError("aarmvs: the HIP sweep needs ROCm device tensors (got a CPU tensor); "
+                              "there is no CPU fallback")
+        if t.dtype != torch.float32:
+            raise AarmvsError(f"aarmvs: expected float32 tensors, got {t.dtype}")
+
+
+def relative_projection(src_proj: torch.Tensor, ref_proj: torch.Tensor) -> torch.Tensor:
+    """rows 0..2 of src_proj @ inverse(ref_proj) (module.py:16-18), [B,3,4] fp32.
+
+    Computed on the host in fp32, exactly as the reference's CPU path does; the
+    4x4 matrices are tiny and this keeps the sampling grid bit-compatible.
+    """
+    s = src_proj.detach().float().cpu()
+    r = ref_proj.detach().float().cpu()
+    return torch.matmul(s, torch.inverse(r))[:, :3, :4].contiguous()
+
+
+def pack_params(params: dict, device) -> torch.Tensor:
+    """Flatten the 48 sweep tensors (checkpoint keys) and pack them on the device."""
+    missing = [k for k in SWEEP_KEYS if k not in params]
+    if missing:
+        raise KeyError(f"aarmvs.pack_params: missing parameters {missing[:3]}...")
+    raw = torch.cat([params[k].detach().reshape(-1).float() for k in SWEEP_KEYS]).to(device)
+    if raw.numel() != lib().aarmvs_param_count():
+        raise AarmvsError("aarmvs.pack_params: parameter count mismatch with libaarmvs")
+    nbytes = lib().aarmvs_packed_param_bytes()
+    packed = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
+    check(lib().aarmvs_pack_params(raw.data_ptr(), packed.data_ptr(), _stream()), "pack_params")
+    packed._aarmvs_raw = raw  # keep the source alive until the async pack has run
+    return packed
+
+
+def homo_warp(src_fea: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor) -> torch.Tensor:
+    """homo_warping_depthwise on the GPU for precomputed rel [B,3,4] and depth [B]."""
+    _require_device(src_fea)
+    src = src_fea.contiguous()
+    B, C, H, W = src.shape
+    rel_d = rel.reshape(B, 12).to(src.device, torch.float32).contiguous()
+    dep = depth.reshape(B).to(src.device, torch.float32).contiguous()
+    out = torch.empty_like(src)
+    check(lib().aarmvs_homo_warp(src.data_ptr(), rel_d.data_ptr(), dep.data_ptr(), B, C, H, W,
+                                 out.data_ptr(), _stream()), "homo_warp")
+    return out
+
+
+def softmax_depth(cost: torch.Tensor) -> torch.Tensor:
+    _require_device(cost)
+    c = cost.contiguous()
+    B, D = c.shape[:2]
+    out = torch.empty_like(c)
+    check(lib().aarmvs_softmax_depth(c.data_ptr(), out.data_ptr(), B, D, c[0, 0].numel(),
+                                     _stream()), "softmax_depth")
+    return out
+
+
+class DepthSweep:
+    """Runs EMVSNet's depth loop (drmvsnet.py:273-291 / :306-342) on the HIP library.
+
+    Holds the packed parameters and a workspace per (B, H, W, nsrc) geometry.
+    """
+
+    def __init__(self, params: dict, device):
+        self.device = torch.device(device)
+        self.packed = pack_params(params, self.device)
+        self._ws = {}
+
+    def workspace(self, B, H, W, nsrc) -> torch.Tensor:
+        key = (B, H, W, nsrc)
+        ws = self._ws.get(key)
+        if ws is None:
+            n = lib().aarmvs_sweep_workspace_bytes(B, H, W, nsrc)
+            if n == 0:
+                raise AarmvsError(f"aarmvs: invalid sweep geometry B={B} H={H} W={W} nsrc={nsrc} "
+                                  "(H and W must be multiples of 4, 1 <= nsrc <= 16)")
+            self._ws.clear()   # one live geometry at a time keeps HBM use bounded
+            ws = torch.empty(n, dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
+
+    def __call__(self, ref_fea, src_feas, ref_proj, src_projs, depth_values, *,
+                 want_depth=True, want_cost=False, d_range=None, debug=False):
+        """Returns dict(depth, conf, cost, slice, omega) (entries None when not requested)."""
+        ref = ref_fea.contiguous()
+        srcs = [s.contiguous() for s in src_feas]
+        _require_device(ref, *srcs)
+        B, C, H, W = ref.shape
+        nsrc = len(srcs)
+        if nsrc < 1 or nsrc > _lib.MAX_SRC:
+            raise AarmvsError(f"aarmvs: need 1..{_lib.MAX_SRC} source views, got {nsrc}")
+        for s in srcs:
+            if s.shape != ref.shape:
+                raise AarmvsError("aarmvs: source features must match the reference feature shape")
+        dv = depth_values.to(ref.device, torch.float32).contiguous()
+        D = dv.shape[1]
+        rel = torch.stack([relative_projection(sp, ref_proj) for sp in src_projs])  # [nsrc,B,3,4]
+        rel = rel.reshape(nsrc, B, 12).to(ref.device).contiguous()
+        ws = self.workspace(B, H, W, nsrc)
+        out = {"depth": None, "conf": None, "cost": None, "slice": None, "omega": None}
+        if want_depth:
+            out["depth"] = torch.empty(B, H, W, device=ref.device)
+            out["conf"] = torch.empty(B, H, W, device=ref.device)
+        if want_cost:
+            out["cost"] = torch.empty(B, D, H, W, device=ref.device)
+        if debug:
+            out["slice"] = torch.empty(B, C, H, W, device=ref.device)
+            out["omega"] = torch.empty(nsrc, B, H, W, device=ref.device)
+        a = _lib.SweepArgs()
+        a.B, a.C, a.H, a.W, a.nsrc, a.D = B, C, H, W, nsrc, D
+        d0, d1 = (0, D) if d_range is None else d_range
+        a.d_begin, a.d_end = d0, d1
+        a.ref_fea = ref.data_ptr()
+        for i, s in enumerate(srcs):
+            a.src_fea[i] = s.data_ptr()
+        a.rel_proj = rel.data_ptr()
+        a.depth_values = dv.data_ptr()
+        a.packed_params = self.packed.data_ptr()
+        a.workspace = ws.data_ptr()
+        a.depth_out = _ptr(out["depth"])
+        a.conf_out = _ptr(out["conf"])
+        a.cost_out = _ptr(out["cost"])
+        a.slice_out = _ptr(out["slice"])
+        a.omega_out = _ptr(out["omega"])
+        check(lib().aarmvs_sweep(ctypes.byref(a), _stream()), "sweep")
+        out["_keepalive"] = (rel, dv, srcs, ref)
+        return out
+
+    def state(self, B, H, W, nsrc, parity, cell, which) -> torch.Tensor:
+        """View of a hidden/cell state inside the workspace (after a sweep call)."""
+        ws = self.workspace(B, H, W, nsrc)
+        ptr = lib().aarmvs_state_ptr(ws.data_ptr(), B, H, W, nsrc, parity, cell, which)
+        if not ptr:
+            raise AarmvsError("aarmvs: bad state query")
+        hid = (16, 16, 16, 16, 8)[cell]
+        sc = (1, 2, 4, 2, 1)[cell]
+        off = ptr - ws.data_ptr()
+        return ws[off: off + B * hid * (H // sc) * (W // sc) * 4].view(torch.float32).view(
+            B, hid, H // sc, W // sc)
+
+    def unet_step(self, x: torch.Tensor, step: int, nsrc: int = 1) -> torch.Tensor:
+        _require_device(x)
+        x = x.contiguous()
+        B, C, H, W = x.shape
+        ws = self.workspace(B, H, W, nsrc)
+        cost = torch.empty(B, 1, H, W, device=x.device)
+        check(lib().aarmvs_unet_step(x.data_ptr(), B, H, W, nsrc, step, self.packed.data_ptr(),
+                                     ws.data_ptr(), cost.data_ptr(), _stream()), "unet_step")
+        return cost

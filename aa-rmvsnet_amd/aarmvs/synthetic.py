@@ -1,0 +1,163 @@
+"""Deterministic synthetic inputs and random-init weights (numpy only).
+
+Used by the benchmark, the tests and the golden-fixture generator so that the
+reference (run in the build container) and this build (run on the GPU box) see
+bit-identical inputs.  Recipe follows SURVEY.md §8(d):
+
+* features ~ N(0,1) ``[B,32,H,W]`` per view, images ~ N(0,1) ``[B,N,3,H,W]``;
+* K = [[f,0,W/2],[0,f,H/2],[0,0,1]] with f = W; reference extrinsic = I;
+  source view v translated along x by -20*v mm with a small alternating yaw;
+  projection = [K @ E[:3,:4]; E[3]] as built by datasets/dtu_yao.py:144-146;
+* depth hypotheses linspace(425, 935, D) mm (optionally descending, the
+  ``flip_flag`` case of dtu_yao.py:172-173);
+* weights: per-tensor ``default_rng([seed, crc32(name)])``, conv weights/biases
+  U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (torch's default bound), norm affines near
+  (1, 0) so that gamma/beta are exercised.
+"""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+
+
+def camera_projections(N: int, H: int, W: int, baseline: float = 20.0,
+                       yaw: float = 0.02) -> np.ndarray:
+    """[N,4,4] float32 projection matrices (view 0 = reference)."""
+    f = float(W)
+    K = np.array([[f, 0, W / 2.0], [0, f, H / 2.0], [0, 0, 1]], dtype=np.float64)
+    out = []
+    for v in range(N):
+        th = yaw * v * (1 if v % 2 else -1)
+        R = np.array([[np.cos(th), 0, np.sin(th)], [0, 1, 0], [-np.sin(th), 0, np.cos(th)]])
+        E = np.eye(4)
+        E[:3, :3] = R
+        E[:3, 3] = [-baseline * v, 0.3 * v, 0.0]
+        P = E.copy()
+        P[:3, :4] = K @ E[:3, :4]
+        out.append(P)
+    return np.stack(out).astype(np.float32)
+
+
+def depth_hypotheses(D: int, lo: float = 425.0, hi: float = 935.0,
+                     descending: bool = False, inverse: bool = False) -> np.ndarray:
+    if inverse:  # data_eval_transform.py:119-124
+        d = 1.0 / np.linspace(1.0 / lo, 1.0 / hi, D)
+    else:
+        d = np.linspace(lo, hi, D)
+    d = d.astype(np.float32)
+    return d[::-1].copy() if descending else d
+
+
+def scene(B: int, N: int, H: int, W: int, D: int, seed: int = 0, C: int = 32,
+          descending: bool = False, images: bool = False):
+    """Synthetic multi-view sample.  Returns dict of numpy arrays.
+
+    ``features``: [N,B,C,H,W] (view-major; view 0 is the reference) unless
+    ``images`` is set, in which case ``imgs`` [B,N,3,H,W] is produced instead.
+    """
+    rng = np.random.default_rng(seed)
+    out = {}
+    if images:
+        out["imgs"] = rng.standard_normal((B, N, 3, H, W), dtype=np.float32)
+    else:
+        out["features"] = rng.standard_normal((N, B, C, H, W), dtype=np.float32)
+    proj = camera_projections(N, H, W)
+    out["proj_matrices"] = np.broadcast_to(proj, (B, N, 4, 4)).copy()
+    dv = depth_hypotheses(D, descending=descending)
+    out["depth_values"] = np.broadcast_to(dv, (B, D)).copy()
+    return out
+
+
+def _fan_in(shape, name: str) -> int:
+    if len(shape) <= 1:
+        return 1
+    if "deconv" in name and name.endswith("conv.weight"):   # ConvTranspose2d: [Cin,Cout,k,k]
+        return int(shape[1] * np.prod(shape[2:]))
+    return int(np.prod(shape[1:]))
+
+
+def init_weights(shapes: dict, seed: int = 1) -> dict:
+    """Random-init parameters for a state_dict layout ``{name: shape}``."""
+    out = {}
+    weight_shapes = {n: s for n, s in shapes.items()}
+    for name in sorted(shapes):
+        shape = tuple(shapes[name])
+        rng = np.random.default_rng([seed, zlib.crc32(name.encode())])
+        leaf = name.rsplit(".", 1)[-1]
+        if leaf in ("running_mean",):
+            arr = np.zeros(shape, np.float32)
+        elif leaf in ("running_var",):
+            arr = np.ones(shape, np.float32)
+        elif leaf == "num_batches_tracked":
+            arr = np.zeros(shape, np.int64)
+        elif len(shape) >= 2:            # conv / deconv weight
+            b = 1.0 / np.sqrt(_fan_in(shape, name))
+            arr = rng.uniform(-b, b, shape).astype(np.float32)
+        else:                            # bias or norm affine
+            wname = name[: -len(leaf)] + "weight"
+            wshape = weight_shapes.get(wname)
+            is_norm = wshape is not None and len(wshape) == 1
+            if is_norm and leaf == "weight":
+                arr = (1.0 + 0.1 * rng.standard_normal(shape)).astype(np.float32)
+            elif is_norm:
+                arr = (0.1 * rng.standard_normal(shape)).astype(np.float32)
+            else:
+                fi = _fan_in(wshape, wname) if wshape is not None else 1
+                b = 1.0 / np.sqrt(fi)
+                arr = rng.uniform(-b, b, shape).astype(np.float32)
+        out[name] = arr
+    return out
+
+
+def array_digest(*arrays) -> str:
+    """Stable digest of arrays (detects RNG drift between hosts)."""
+    h = zlib.crc32(b"")
+    for a in arrays:
+        h = zlib.crc32(np.ascontiguousarray(a).tobytes(), h)
+    return f"{h:08x}"
+
+
+# state_dict layout of the sweep's parameters (checkpoint keys):
+# omega.* (drmvsnet.py:27-38) and cost_regularization.* (drmvsnet.py:66-117).
+SWEEP_SHAPES = {
+    "omega.reweight_network.0.0.weight": (4, 32, 3, 3),
+    "omega.reweight_network.0.0.bias": (4,),
+    "omega.reweight_network.0.1.weight": (4,),
+    "omega.reweight_network.0.1.bias": (4,),
+    "omega.reweight_network.1.stem.0.0.weight": (4, 4, 1, 1),
+    "omega.reweight_network.1.stem.0.0.bias": (4,),
+    "omega.reweight_network.1.stem.0.1.weight": (4,),
+    "omega.reweight_network.1.stem.0.1.bias": (4,),
+    "omega.reweight_network.1.stem.1.weight": (4, 4, 1, 1),
+    "omega.reweight_network.1.stem.1.bias": (4,),
+    "omega.reweight_network.1.stem.2.weight": (4,),
+    "omega.reweight_network.1.stem.2.bias": (4,),
+    "omega.reweight_network.2.weight": (1, 4, 1, 1),
+    "omega.reweight_network.2.bias": (1,),
+    "cost_regularization.cell_list.0.conv.weight": (64, 48, 3, 3),
+    "cost_regularization.cell_list.0.conv.bias": (64,),
+    "cost_regularization.cell_list.1.conv.weight": (64, 32, 3, 3),
+    "cost_regularization.cell_list.1.conv.bias": (64,),
+    "cost_regularization.cell_list.2.conv.weight": (64, 32, 3, 3),
+    "cost_regularization.cell_list.2.conv.bias": (64,),
+    "cost_regularization.cell_list.3.conv.weight": (64, 48, 3, 3),
+    "cost_regularization.cell_list.3.conv.bias": (64,),
+    "cost_regularization.cell_list.4.conv.weight": (32, 40, 3, 3),
+    "cost_regularization.cell_list.4.conv.bias": (32,),
+    "cost_regularization.deconv_0.conv.weight": (16, 16, 3, 3),
+    "cost_regularization.deconv_0.conv.bias": (16,),
+    "cost_regularization.deconv_0.gn.weight": (16,),
+    "cost_regularization.deconv_0.gn.bias": (16,),
+    "cost_regularization.deconv_1.conv.weight": (16, 16, 3, 3),
+    "cost_regularization.deconv_1.conv.bias": (16,),
+    "cost_regularization.deconv_1.gn.weight": (16,),
+    "cost_regularization.deconv_1.gn.bias": (16,),
+    "cost_regularization.conv_0.weight": (1, 8, 3, 3),
+    "cost_regularization.conv_0.bias": (1,),
+}
+
+
+def sweep_weights(seed: int = 1) -> dict:
+    """Random-init sweep parameters (same values init_weights gives the full model)."""
+    return init_weights(SWEEP_SHAPES, seed=seed)

@@ -1,0 +1,109 @@
+// Internal declarations shared by the HIP translation units of libaarmvs.
+// Layouts of the packed parameter buffer and of the sweep workspace live here.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/aarmvs.h"
+
+namespace aarmvs {
+
+constexpr int kC = 32;          // feature channels (FeatNet output)
+constexpr int kSlots = 32;      // fp64 atomic slots per GroupNorm statistic
+constexpr float kGnEps = 1e-5f; // nn.GroupNorm default eps
+
+// ---------------------------------------------------------------------------
+// Parameter tensors, in raw-blob order (aarmvs.h).
+// ---------------------------------------------------------------------------
+enum ParamId : int {
+  P_OW0, P_OB0, P_OG0W, P_OG0B, P_OW1, P_OB1, P_OG1W, P_OG1B, P_OW2, P_OB2, P_OG2W, P_OG2B,
+  P_OWO, P_OBO,
+  P_C0W, P_C0B, P_C1W, P_C1B, P_C2W, P_C2B, P_C3W, P_C3B, P_C4W, P_C4B,
+  P_D0W, P_D0B, P_D0GW, P_D0GB, P_D1W, P_D1B, P_D1GW, P_D1GB,
+  P_HW, P_HB,
+  P_COUNT
+};
+
+constexpr int kParamSize[P_COUNT] = {
+    4 * 32 * 9, 4, 4, 4, 16, 4, 4, 4, 16, 4, 4, 4, 4, 1,
+    64 * 48 * 9, 64, 64 * 32 * 9, 64, 64 * 32 * 9, 64, 64 * 48 * 9, 64, 32 * 40 * 9, 32,
+    16 * 16 * 9, 16, 16, 16, 16 * 16 * 9, 16, 16, 16,
+    8 * 9, 1};
+
+struct ParamLayout {
+  size_t raw_off[P_COUNT];
+  size_t pk_off[P_COUNT];   // packed offsets (floats), 64-float aligned
+  size_t raw_total;
+  size_t pk_total;
+};
+const ParamLayout& param_layout();
+
+// LSTM cell geometry (drmvsnet.py:241-244): input x-channels, hidden channels, scale.
+constexpr int kCellCX[5] = {32, 16, 16, 32, 32};
+constexpr int kCellHid[5] = {16, 16, 16, 16, 8};
+constexpr int kCellScale[5] = {1, 2, 4, 2, 1};
+
+// ---------------------------------------------------------------------------
+// Workspace layout.
+// ---------------------------------------------------------------------------
+struct Workspace {
+  double* stats;        // [B][nstat][kSlots][2]
+  float* max_prob;      // [B,HW]
+  float* exp_sum;       // [B,HW]
+  float* depth;         // [B,HW]
+  float* x;             // [B,32,H,W] cost slice
+  float* t1;            // [B][nsrc][HW][4] omega conv3x3 output
+  float* u0;            // [B,16,H/2,W/2] deconv_0 output (pre-GN)
+  float* u1;            // [B,16,H,W]     deconv_1 output (pre-GN)
+  float* h[5][2];       // ping-pong hidden states
+  float* c[5];          // cell states (updated in place)
+  size_t bytes;
+  size_t stats_bytes;
+  size_t state_bytes;   // h[*][*], c[*] region (contiguous) for zero-init
+  void* state_begin;
+  size_t wta_bytes;     // max_prob/exp_sum/depth region
+};
+Workspace carve_workspace(void* base, int B, int H, int W, int nsrc);
+__host__ __device__ inline int nstat(int nsrc) { return 3 * nsrc + 4; }
+// statistic ids within a batch element
+__host__ __device__ inline int stat_omega(int v, int k) { return 3 * v + k; }
+__host__ __device__ inline int stat_deconv(int nsrc, int j, int g) { return 3 * nsrc + 2 * j + g; }
+
+// ---------------------------------------------------------------------------
+// Kernel launchers (defined in the .hip units).
+// ---------------------------------------------------------------------------
+struct SweepGeom {
+  int B, H, W, nsrc, D;
+  int cu_count;
+};
+
+hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s);
+hipError_t launch_homo_warp(const float* src, const float* rel, const float* depth, int B, int C,
+                            int H, int W, float* out, hipStream_t s);
+
+struct CostArgs {
+  const float* ref;
+  const float* src[AARMVS_MAX_SRC];
+  const float* rel;       // [nsrc][B][12]
+  const float* depth_values;  // [B,D]
+  int d;
+  const float* params;    // packed
+};
+hipError_t launch_cost_slice(const CostArgs& a, const SweepGeom& g, const Workspace& ws,
+                             float* omega_out, hipStream_t s);
+
+hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
+                            const Workspace& ws, int parity, hipStream_t s);
+hipError_t launch_head_wta(const float* params, const SweepGeom& g, const Workspace& ws,
+                           int parity, const float* depth_values, int d, float* cost_out,
+                           bool wta, hipStream_t s);
+hipError_t launch_finalize(const SweepGeom& g, const Workspace& ws, float* depth_out,
+                           float* conf_out, hipStream_t s);
+hipError_t launch_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
+                                hipStream_t s);
+
+int cu_count();
+
+}  // namespace aarmvs

@@ -1,0 +1,262 @@
+// C-ABI entry points of libaarmvs (include/aarmvs.h): argument validation, the
+// parameter packing kernel, the workspace carve and the per-plane sweep schedule.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "aarmvs_internal.h"
+
+namespace aarmvs {
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+static int hip_fail(hipError_t e, const char* where) {
+  return fail(AARMVS_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+const ParamLayout& param_layout() {
+  static ParamLayout L = [] {
+    ParamLayout l{};
+    size_t raw = 0, pk = 0;
+    for (int i = 0; i < P_COUNT; ++i) {
+      l.raw_off[i] = raw;
+      l.pk_off[i] = pk;
+      raw += kParamSize[i];
+      pk += ((size_t)kParamSize[i] + 63) / 64 * 64;
+    }
+    l.raw_total = raw;
+    l.pk_total = pk;
+    return l;
+  }();
+  return L;
+}
+
+int cu_count() {
+  static int cu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      return 256;
+    return n;
+  }();
+  return cu;
+}
+
+static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
+  Workspace ws{};
+  char* p = static_cast<char*>(base);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* r = p ? p + off : nullptr;
+    off = align_up(off + bytes, 256);
+    return r;
+  };
+  const size_t HW = (size_t)H * W, HW2 = HW / 4, HW4 = HW / 16;
+  ws.stats_bytes = (size_t)B * nstat(nsrc) * kSlots * 2 * sizeof(double);
+  ws.stats = reinterpret_cast<double*>(take(ws.stats_bytes));
+  const size_t wta_begin = off;
+  ws.max_prob = reinterpret_cast<float*>(take(B * HW * 4));
+  ws.exp_sum = reinterpret_cast<float*>(take(B * HW * 4));
+  ws.depth = reinterpret_cast<float*>(take(B * HW * 4));
+  ws.wta_bytes = off - wta_begin;
+  ws.x = reinterpret_cast<float*>(take(B * kC * HW * 4));
+  ws.t1 = reinterpret_cast<float*>(take((size_t)B * nsrc * HW * 16));
+  ws.u0 = reinterpret_cast<float*>(take(B * 16 * HW2 * 4));
+  ws.u1 = reinterpret_cast<float*>(take(B * 16 * HW * 4));
+  const size_t state_begin = off;
+  ws.state_begin = p ? p + off : nullptr;
+  const size_t cell_px[5] = {HW, HW2, HW4, HW2, HW};
+  for (int k = 0; k < 5; ++k) {
+    const size_t n = (size_t)B * kCellHid[k] * cell_px[k] * 4;
+    ws.h[k][0] = reinterpret_cast<float*>(take(n));
+    ws.h[k][1] = reinterpret_cast<float*>(take(n));
+    ws.c[k] = reinterpret_cast<float*>(take(n));
+  }
+  ws.state_bytes = off - state_begin;
+  ws.bytes = off;
+  return ws;
+}
+
+// ---------------------------------------------------------------------------
+// Parameter packing: cell weights [4*hid][cin][3][3] -> MFMA A operands
+// [K/2][MT][64] with k = tap*cin + ci and m-tile row r -> cout (r>>3)*hid + 8*mt + (r&7).
+// Everything else is copied (64-float aligned sections).
+// ---------------------------------------------------------------------------
+__global__ void pack_params_kernel(const float* __restrict__ raw, float* __restrict__ pk,
+                                   ParamLayout L) {
+  const int id = blockIdx.y;
+  const int n = kParamSize[id];
+  const float* src = raw + L.raw_off[id];
+  float* dst = pk + L.pk_off[id];
+  const bool is_cell_w = id >= P_C0W && id <= P_C4W && ((id - P_C0W) % 2 == 0);
+  const int k = (id - P_C0W) / 2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (!is_cell_w) {
+      dst[i] = src[i];
+      continue;
+    }
+    const int hid = kCellHid[k], cin = kCellCX[k] + hid, mt_n = hid / 8;
+    const int l = i % 64, mt = (i / 64) % mt_n, s = i / (64 * mt_n);
+    const int kk = 2 * s + (l >> 5);
+    const int tap = kk / cin, ci = kk % cin;
+    const int r = l & 31;
+    const int cout = (r >> 3) * hid + 8 * mt + (r & 7);
+    dst[i] = src[(cout * cin + ci) * 9 + tap];
+  }
+}
+
+hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s) {
+  const ParamLayout& L = param_layout();
+  hipError_t e = hipMemsetAsync(packed, 0, L.pk_total * sizeof(float), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pack_params_kernel, dim3(32, P_COUNT), dim3(256), 0, s, raw, packed, L);
+  return hipGetLastError();
+}
+
+}  // namespace aarmvs
+
+using namespace aarmvs;
+
+extern "C" {
+
+const char* aarmvs_last_error(void) { return g_err.c_str(); }
+const char* aarmvs_version(void) { return "aarmvs-mi355x 0.1 (gfx950)"; }
+
+size_t aarmvs_param_count(void) { return param_layout().raw_total; }
+size_t aarmvs_packed_param_bytes(void) { return param_layout().pk_total * sizeof(float); }
+
+int aarmvs_pack_params(const float* raw_params, void* packed, hipStream_t stream) {
+  if (!raw_params || !packed) return fail(AARMVS_ERR_INVALID, "pack_params: null pointer");
+  hipError_t e = launch_pack_params(raw_params, static_cast<float*>(packed), stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "pack_params");
+}
+
+int aarmvs_homo_warp(const float* src_fea, const float* rel_proj, const float* depth, int B,
+                     int C, int H, int W, float* out, hipStream_t stream) {
+  if (!src_fea || !rel_proj || !depth || !out) return fail(AARMVS_ERR_INVALID, "homo_warp: null pointer");
+  if (B < 1 || C < 1 || H < 2 || W < 2)
+    return fail(AARMVS_ERR_INVALID, "homo_warp: need B>=1, C>=1, H>=2, W>=2");
+  hipError_t e = launch_homo_warp(src_fea, rel_proj, depth, B, C, H, W, out, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "homo_warp");
+}
+
+static int check_geom(int B, int H, int W, int nsrc) {
+  if (B < 1) return fail(AARMVS_ERR_INVALID, "B must be >= 1");
+  if (H < 4 || W < 4 || H % 4 || W % 4)
+    return fail(AARMVS_ERR_INVALID,
+                "H and W must be positive multiples of 4 (two 2x2 pools + two stride-2 deconvs)");
+  if (nsrc < 1 || nsrc > AARMVS_MAX_SRC)
+    return fail(AARMVS_ERR_INVALID, "nsrc must be in [1, AARMVS_MAX_SRC]");
+  return AARMVS_OK;
+}
+
+size_t aarmvs_sweep_workspace_bytes(int B, int H, int W, int nsrc) {
+  if (check_geom(B, H, W, nsrc) != AARMVS_OK) return 0;
+  return carve_workspace(nullptr, B, H, W, nsrc).bytes;
+}
+
+float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int plane_parity,
+                        int cell, int which) {
+  if (!workspace || cell < 0 || cell > 4 || check_geom(B, H, W, nsrc) != AARMVS_OK) return nullptr;
+  Workspace ws = carve_workspace(workspace, B, H, W, nsrc);
+  return which == 0 ? ws.h[cell][plane_parity & 1] : ws.c[cell];
+}
+
+int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
+  if (!a) return fail(AARMVS_ERR_INVALID, "sweep: null args");
+  int rc = check_geom(a->B, a->H, a->W, a->nsrc);
+  if (rc) return rc;
+  if (a->C != kC) return fail(AARMVS_ERR_INVALID, "sweep: feature channels C must be 32");
+  if (a->D < 1 || a->d_begin < 0 || a->d_end > a->D || a->d_begin >= a->d_end)
+    return fail(AARMVS_ERR_INVALID, "sweep: need 0 <= d_begin < d_end <= D");
+  if (!a->ref_fea || !a->rel_proj || !a->depth_values || !a->packed_params || !a->workspace)
+    return fail(AARMVS_ERR_INVALID, "sweep: null pointer argument");
+  for (int v = 0; v < a->nsrc; ++v)
+    if (!a->src_fea[v]) return fail(AARMVS_ERR_INVALID, "sweep: null src_fea pointer");
+
+  SweepGeom g{a->B, a->H, a->W, a->nsrc, a->D, cu_count()};
+  Workspace ws = carve_workspace(a->workspace, a->B, a->H, a->W, a->nsrc);
+  const float* params = static_cast<const float*>(a->packed_params);
+  hipError_t e;
+  if (a->d_begin == 0) {
+    // UNetConvLSTM._init_hidden (drmvsnet.py:133-134, 202-206) and the WTA images
+    // (drmvsnet.py:302-304)
+    if ((e = hipMemsetAsync(ws.state_begin, 0, ws.state_bytes, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: state init");
+    if ((e = hipMemsetAsync(ws.max_prob, 0, ws.wta_bytes, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: wta init");
+  }
+  CostArgs ca{};
+  ca.ref = a->ref_fea;
+  for (int v = 0; v < a->nsrc; ++v) ca.src[v] = a->src_fea[v];
+  ca.rel = a->rel_proj;
+  ca.depth_values = a->depth_values;
+  ca.params = params;
+  const bool wta = a->depth_out || a->conf_out;
+  for (int d = a->d_begin; d < a->d_end; ++d) {
+    ca.d = d;
+    const bool last = d == a->d_end - 1;
+    if ((e = hipMemsetAsync(ws.stats, 0, ws.stats_bytes, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: stats reset");
+    if ((e = launch_cost_slice(ca, g, ws, last ? a->omega_out : nullptr, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: cost slice");
+    if (last && a->slice_out) {
+      e = hipMemcpyAsync(a->slice_out, ws.x, (size_t)a->B * kC * a->H * a->W * 4,
+                         hipMemcpyDeviceToDevice, stream);
+      if (e != hipSuccess) return hip_fail(e, "sweep: slice copy");
+    }
+    if ((e = launch_unet_step(ws.x, params, g, ws, d & 1, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: regulariser step");
+    if ((e = launch_head_wta(params, g, ws, d & 1, a->depth_values, d, a->cost_out, wta, stream)) !=
+        hipSuccess)
+      return hip_fail(e, "sweep: head/wta");
+  }
+  if (wta && a->d_end == a->D) {
+    if ((e = launch_finalize(g, ws, a->depth_out, a->conf_out, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: finalize");
+  }
+  return AARMVS_OK;
+}
+
+int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
+                     const void* packed_params, void* workspace, float* cost_out,
+                     hipStream_t stream) {
+  int rc = check_geom(B, H, W, nsrc);
+  if (rc) return rc;
+  if (!x || !packed_params || !workspace || !cost_out || step < 0)
+    return fail(AARMVS_ERR_INVALID, "unet_step: null pointer or negative step");
+  SweepGeom g{B, H, W, nsrc, 1, cu_count()};
+  Workspace ws = carve_workspace(workspace, B, H, W, nsrc);
+  const float* params = static_cast<const float*>(packed_params);
+  hipError_t e;
+  if (step == 0 && (e = hipMemsetAsync(ws.state_begin, 0, ws.state_bytes, stream)) != hipSuccess)
+    return hip_fail(e, "unet_step: state init");
+  if ((e = hipMemsetAsync(ws.stats, 0, ws.stats_bytes, stream)) != hipSuccess)
+    return hip_fail(e, "unet_step: stats reset");
+  if ((e = launch_unet_step(x, params, g, ws, step & 1, stream)) != hipSuccess)
+    return hip_fail(e, "unet_step");
+  // head conv only (no WTA): cost_out is [B,1,H,W] == [B,D=1,H,W] at plane 0
+  if ((e = launch_head_wta(params, g, ws, step & 1, nullptr, 0, cost_out, false, stream)) !=
+      hipSuccess)
+    return hip_fail(e, "unet_step: head");
+  return AARMVS_OK;
+}
+
+int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW, hipStream_t stream) {
+  if (!cost || !prob || B < 1 || D < 1 || HW < 1)
+    return fail(AARMVS_ERR_INVALID, "softmax_depth: bad arguments");
+  hipError_t e = launch_softmax_depth(cost, prob, B, D, HW, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "softmax_depth");
+}
+
+}  // extern "C"

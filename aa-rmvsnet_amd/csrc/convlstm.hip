@@ -1,0 +1,440 @@
+// Recurrent regulariser step (UNetConvLSTM, models/drmvsnet.py:119-167) for gfx950.
+//
+// ConvLSTM cell (models/module.py:76-92) = implicit-GEMM 3x3 conv on the fp32
+// matrix cores (v_mfma_f32_32x32x2_f32, exact f32 FMA chain) with the LSTM gate
+// math fused into the epilogue:
+//   M = 4*hid output channels (gates i,f,o,g), N = pixels, K = 9 taps x Cin.
+//   One m-tile = 32 rows = the 4 gates of 8 hidden channels, so every lane holds
+//   i,f,o,g of the same (pixel, channel) in its accumulator registers and the
+//   c/h update needs no data exchange.
+//   A (weights) and the haloed input tile live in LDS; B operands are read
+//   straight from the tile (lanes 0-31: 32 consecutive pixels, lanes 32-63: the
+//   next channel), conflict-free ds_read_b32.
+// Input staging fuses the U-Net glue: 2x2 max-pool (drmvsnet.py:148,152),
+// GroupNorm(2,16)+ReLU of the deconv output (module.py:286-287) and the channel
+// concatenations (drmvsnet.py:80, 157, 161).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device_common.h"
+
+namespace aarmvs {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+enum SrcMode : int { SRC_PLAIN = 0, SRC_POOL = 1, SRC_GNRELU = 2 };
+
+struct ChanSrc {
+  const float* ptr;     // [B][nch][Hs][Ws]
+  int nch;
+  int mode;
+  const double* stats;  // SRC_GNRELU: 2 statistics (groups of 8 channels)
+  const float* gamma;
+  const float* beta;
+};
+
+struct CellArgs {
+  ChanSrc part[3];
+  int nparts;
+  float* h_new;
+  float* c;
+  const float* wpk;     // packed A operands [K/2][MT][64]
+  const float* bias;    // [4*hid]
+  int B, H, W;          // cell resolution
+};
+
+constexpr int kLDW = 34;   // 32-pixel tile row + 1-px halo each side
+
+template <int CIN, int HID, int TH>
+struct CellCfg {
+  static constexpr int MT = HID / 8;
+  static constexpr int COUT = 4 * HID;
+  static constexpr int K = 9 * CIN;
+  static constexpr int TROWS = TH + 2;
+  static constexpr int IN_FLOATS = CIN * TROWS * kLDW;
+  static constexpr int W_FLOATS = COUT * K;
+  static constexpr int GN_FLOATS = 2 * 16;
+  static constexpr size_t LDS_BYTES = (size_t)(W_FLOATS + IN_FLOATS + GN_FLOATS) * 4;
+  static constexpr int THREADS = TH * 64;
+};
+
+template <int CIN, int HID, int TH>
+__global__ void __launch_bounds__(TH * 64) lstm_cell_kernel(CellArgs a) {
+  using Cfg = CellCfg<CIN, HID, TH>;
+  constexpr int MT = Cfg::MT;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* wl = lds;
+  float* in = lds + Cfg::W_FLOATS;
+  float* gn = in + Cfg::IN_FLOATS;   // [16] scale, [16] shift for a SRC_GNRELU part
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, W = a.W;
+
+  // weights -> LDS once per block (persistent over tiles)
+  {
+    const float4* s = reinterpret_cast<const float4*>(a.wpk);
+    float4* d = reinterpret_cast<float4*>(wl);
+    for (int i = tid; i < Cfg::W_FLOATS / 4; i += Cfg::THREADS) d[i] = s[i];
+  }
+  // fused GroupNorm(2,16) parameters of the (single) normalised part
+  for (int p = 0; p < a.nparts; ++p) {
+    if (a.part[p].mode == SRC_GNRELU && tid < 16) {
+      const double n = 8.0 * H * W;
+      const GnStat st = stat_read(a.part[p].stats + (tid >> 3) * kSlots * 2, n);
+      const float sc = st.rstd * a.part[p].gamma[tid];
+      gn[tid] = sc;
+      gn[16 + tid] = a.part[p].beta[tid] - st.mean * sc;
+    }
+  }
+
+  const int tiles_x = (W + 31) / 32, tiles_y = (H + TH - 1) / TH;
+  const int ntiles = a.B * tiles_x * tiles_y;
+  const int n0 = a.part[0].nch, n1 = n0 + (a.nparts > 1 ? a.part[1].nch : 0);
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / (tiles_x * tiles_y);
+    const int rem = tile % (tiles_x * tiles_y);
+    const int y0 = (rem / tiles_x) * TH, x0 = (rem % tiles_x) * 32;
+    __syncthreads();   // previous tile's LDS reads complete (and gn/weights visible)
+    for (int i = tid; i < Cfg::IN_FLOATS; i += Cfg::THREADS) {
+      const int ci = i / (Cfg::TROWS * kLDW);
+      const int r = (i / kLDW) % Cfg::TROWS, cc = i % kLDW;
+      const int gy = y0 - 1 + r, gx = x0 - 1 + cc;
+      float v = 0.0f;
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        const int p = ci < n0 ? 0 : (ci < n1 ? 1 : 2);
+        const int lc = ci - (p == 0 ? 0 : (p == 1 ? n0 : n1));
+        const ChanSrc& s = a.part[p];
+        if (s.mode == SRC_POOL) {
+          const int Ws = 2 * W, Hs = 2 * H;
+          const float* q = s.ptr + (((size_t)b * s.nch + lc) * Hs + 2 * gy) * Ws + 2 * gx;
+          v = fmaxf(fmaxf(q[0], q[1]), fmaxf(q[Ws], q[Ws + 1]));
+        } else {
+          v = s.ptr[(((size_t)b * s.nch + lc) * H + gy) * W + gx];
+          if (s.mode == SRC_GNRELU) v = fmaxf(v * gn[lc] + gn[16 + lc], 0.0f);
+        }
+      }
+      in[i] = v;
+    }
+    __syncthreads();
+
+    floatx16 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[m][j] = 0.0f;
+
+    const int hi = lane >> 5, col = lane & 31;
+    const float* inb = in + hi * Cfg::TROWS * kLDW + wave * kLDW + col;
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3, dx = tap % 3;
+      const float* bt = inb + dy * kLDW + dx;
+      const float* at = wl + (tap * (CIN / 2)) * MT * 64 + lane;
+#pragma unroll
+      for (int cp = 0; cp < CIN / 2; ++cp) {
+        const float bv = bt[2 * cp * Cfg::TROWS * kLDW];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(at[(cp * MT + m) * 64], bv, acc[m], 0, 0, 0);
+      }
+    }
+
+    // epilogue: LSTM gates (module.py:83-90)
+    const int y = y0 + wave, x = x0 + col;
+    if (y < H && x < W) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ch = m * 8 + 4 * hi + q;
+          const float gi = acc[m][q] + a.bias[ch];
+          const float gf = acc[m][4 + q] + a.bias[HID + ch];
+          const float go = acc[m][8 + q] + a.bias[2 * HID + ch];
+          const float gg = acc[m][12 + q] + a.bias[3 * HID + ch];
+          const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
+          const float cn = sigmoidf_(gf) * a.c[idx] + sigmoidf_(gi) * tanhf(gg);
+          a.c[idx] = cn;
+          a.h_new[idx] = sigmoidf_(go) * tanhf(cn);
+        }
+      }
+    }
+  }
+}
+
+template <int CIN, int HID, int TH>
+static hipError_t run_cell(const CellArgs& a, int cu, hipStream_t s) {
+  using Cfg = CellCfg<CIN, HID, TH>;
+  static_assert(Cfg::LDS_BYTES <= 160 * 1024, "cell tile exceeds LDS");
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_kernel<CIN, HID, TH>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)Cfg::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int ntiles = a.B * ((a.W + 31) / 32) * ((a.H + TH - 1) / TH);
+  const int grid = std::max(1, std::min(ntiles, cu));
+  hipLaunchKernelGGL((lstm_cell_kernel<CIN, HID, TH>), dim3(grid), dim3(Cfg::THREADS),
+                     Cfg::LDS_BYTES, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// deConvGnReLU's transposed conv (module.py:281): ConvTranspose2d(16,16,3,s2,p1,op1).
+// One thread per input pixel produces its 2x2 output quad (uniform weight taps),
+// plus GroupNorm(2,16) partial sums (the GN+ReLU itself is fused into the
+// consuming cell's input staging).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) deconv_kernel(const float* __restrict__ in,
+                                                     const float* __restrict__ w,
+                                                     const float* __restrict__ bias, int Hi,
+                                                     int Wi, float* __restrict__ out,
+                                                     double* __restrict__ stats) {
+  __shared__ float red[4 * 4];
+  const int b = blockIdx.y;
+  const int HWi = Hi * Wi, Ho = 2 * Hi, Wo = 2 * Wi;
+  const float* ib = in + (size_t)b * 16 * HWi;
+  float* ob = out + (size_t)b * 16 * Ho * Wo;
+  float part[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HWi; p += gridDim.x * blockDim.x) {
+    const int iy = p / Wi, ix = p % Wi;
+    const bool hy = iy + 1 < Hi, hx = ix + 1 < Wi;
+    float o[4][16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int co = 0; co < 16; ++co) o[q][co] = 0.f;
+    for (int ci = 0; ci < 16; ++ci) {
+      const float* ic = ib + (size_t)ci * HWi + p;
+      const float v00 = ic[0];
+      const float v01 = hx ? ic[1] : 0.f;
+      const float v10 = hy ? ic[Wi] : 0.f;
+      const float v11 = (hx && hy) ? ic[Wi + 1] : 0.f;
+      const float* wc = w + ci * 16 * 9;   // [ci][co][ky][kx]
+#pragma unroll
+      for (int co = 0; co < 16; ++co) {
+        const float* k = wc + co * 9;
+        // out(2iy,2ix): (ky,kx)=(1,1) from (iy,ix)
+        o[0][co] = fmaf(v00, k[4], o[0][co]);
+        // out(2iy,2ix+1): kx=2 from ix, kx=0 from ix+1 (ky=1)
+        o[1][co] = fmaf(v00, k[5], fmaf(v01, k[3], o[1][co]));
+        // out(2iy+1,2ix): ky=2 from iy, ky=0 from iy+1 (kx=1)
+        o[2][co] = fmaf(v00, k[7], fmaf(v10, k[1], o[2][co]));
+        // out(2iy+1,2ix+1)
+        o[3][co] = fmaf(v00, k[8], fmaf(v01, k[6], fmaf(v10, k[2], fmaf(v11, k[0], o[3][co]))));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oy = 2 * iy + (q >> 1), ox = 2 * ix + (q & 1);
+#pragma unroll
+      for (int co = 0; co < 16; ++co) {
+        const float r = o[q][co] + bias[co];
+        ob[((size_t)co * Ho + oy) * Wo + ox] = r;
+        part[(co >> 3) * 2] += r;
+        part[(co >> 3) * 2 + 1] += r * r;
+      }
+    }
+  }
+  block_sum<4>(part, red);
+  if (threadIdx.x == 0) {
+    stat_add(stats, part[0], part[1]);
+    stat_add(stats + kSlots * 2, part[2], part[3]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// conv_0 head (drmvsnet.py:117,165: Conv2d(8,1,3,pad 1)) fused with the online
+// winner-take-all update (drmvsnet.py:324-334) and the optional cost-volume store.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__ h4,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ bias, int H,
+                                                       int W, const float* __restrict__ dvals,
+                                                       int d, int D, float* __restrict__ cost_out,
+                                                       int wta, float* __restrict__ max_prob,
+                                                       float* __restrict__ exp_sum,
+                                                       float* __restrict__ depth) {
+  const int b = blockIdx.y, HW = H * W;
+  const float* hb = h4 + (size_t)b * 8 * HW;
+  const float dv = wta ? dvals[b * D + d] : 0.0f;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
+    const int y = p / W, x = p % W;
+    float acc = 0.f;
+    for (int ci = 0; ci < 8; ++ci) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+          acc = fmaf(hb[(size_t)ci * HW + yy * W + xx], w[ci * 9 + tap], acc);
+      }
+    }
+    const float cost = acc + bias[0];
+    if (cost_out) cost_out[((size_t)b * D + d) * HW + p] = cost;
+    if (wta) {
+      const size_t q = (size_t)b * HW + p;
+      const float pr = expf(cost);
+      const float mp = max_prob[q];
+      const float f = (mp < pr) ? 1.0f : 0.0f;
+      max_prob[q] = __fadd_rn(__fmul_rn(f, pr), __fmul_rn(1.0f - f, mp));
+      depth[q] = __fadd_rn(__fmul_rn(f, dv), __fmul_rn(1.0f - f, depth[q]));
+      exp_sum[q] = __fadd_rn(exp_sum[q], pr);
+    }
+  }
+}
+
+__global__ void finalize_kernel(const float* __restrict__ max_prob, const float* __restrict__ exp_sum,
+                                const float* __restrict__ depth, size_t n, float* depth_out,
+                                float* conf_out) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    if (depth_out) depth_out[i] = depth[i];
+    if (conf_out) conf_out[i] = __fdiv_rn(max_prob[i], exp_sum[i]);
+  }
+}
+
+// softmax over D (dim=1 of [B,D,H,W]); one thread per (b, pixel), coalesced over pixels.
+__global__ void __launch_bounds__(256) softmax_depth_kernel(const float* __restrict__ cost,
+                                                            float* __restrict__ prob, int D,
+                                                            int HW) {
+  const int b = blockIdx.y;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
+    const float* c = cost + (size_t)b * D * HW + p;
+    float* o = prob + (size_t)b * D * HW + p;
+    float m = -INFINITY;
+    for (int d = 0; d < D; ++d) m = fmaxf(m, c[(size_t)d * HW]);
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s += expf(c[(size_t)d * HW] - m);
+    const float inv = 1.0f / s;
+    for (int d = 0; d < D; ++d) o[(size_t)d * HW] = expf(c[(size_t)d * HW] - m) * inv;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
+                            const Workspace& ws, int parity, hipStream_t s) {
+  const ParamLayout& L = param_layout();
+  const int cur = parity & 1, nxt = cur ^ 1;
+  const int H = g.H, W = g.W, B = g.B, cu = g.cu_count;
+  hipError_t e;
+  auto cell = [&](int k, std::initializer_list<ChanSrc> parts, int scale) {
+    CellArgs a{};
+    int i = 0;
+    for (const ChanSrc& p : parts) a.part[i++] = p;
+    a.nparts = i;
+    a.h_new = ws.h[k][nxt];
+    a.c = ws.c[k];
+    a.wpk = params + L.pk_off[P_C0W + 2 * k];
+    a.bias = params + L.pk_off[P_C0B + 2 * k];
+    a.B = B;
+    a.H = H / scale;
+    a.W = W / scale;
+    return a;
+  };
+  // cell 0: [x, h0] @ H
+  CellArgs a0 = cell(0, {{x, 32, SRC_PLAIN, nullptr, nullptr, nullptr},
+                         {ws.h[0][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
+  if ((e = run_cell<48, 16, 4>(a0, cu, s)) != hipSuccess) return e;
+  // cell 1: [maxpool(h0'), h1] @ H/2
+  CellArgs a1 = cell(1, {{ws.h[0][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},
+                         {ws.h[1][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 2);
+  if ((e = run_cell<32, 16, 8>(a1, cu, s)) != hipSuccess) return e;
+  // cell 2: [maxpool(h1'), h2] @ H/4
+  CellArgs a2 = cell(2, {{ws.h[1][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},
+                         {ws.h[2][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
+  if ((e = run_cell<32, 16, 8>(a2, cu, s)) != hipSuccess) return e;
+  // GroupNorm statistics are per batch element, so the deconvs and the two cells that
+  // consume their normalised output are launched per batch element.
+  const size_t sstride = (size_t)nstat(g.nsrc) * kSlots * 2;
+  // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
+  {
+    const int Hi = H / 4, Wi = W / 4;
+    const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 2 * cu / std::max(1, B)));
+    for (int b = 0; b < B; ++b) {
+      double* st = ws.stats + b * sstride + (size_t)stat_deconv(g.nsrc, 0, 0) * kSlots * 2;
+      hipLaunchKernelGGL(deconv_kernel, dim3(blocks, 1), dim3(256), 0, s,
+                         ws.h[2][nxt] + (size_t)b * 16 * Hi * Wi, params + L.pk_off[P_D0W],
+                         params + L.pk_off[P_D0B], Hi, Wi, ws.u0 + (size_t)b * 16 * 4 * Hi * Wi,
+                         st);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+  }
+  // cell 3: [gnrelu(u0), h1', h3] @ H/2
+  for (int b = 0; b < B; ++b) {
+    const double* st = ws.stats + b * sstride + (size_t)stat_deconv(g.nsrc, 0, 0) * kSlots * 2;
+    const size_t hq = (size_t)(H / 2) * (W / 2);
+    CellArgs a3 = cell(3, {{ws.u0 + b * 16 * hq, 16, SRC_GNRELU, st, params + L.pk_off[P_D0GW],
+                            params + L.pk_off[P_D0GB]},
+                           {ws.h[1][nxt] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr},
+                           {ws.h[3][cur] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr}},
+                       2);
+    a3.B = 1;
+    a3.h_new += b * 16 * hq;
+    a3.c += b * 16 * hq;
+    if ((e = run_cell<48, 16, 4>(a3, cu, s)) != hipSuccess) return e;
+  }
+  // deconv_1: h3' (H/2) -> u1 (H) + GN stats
+  {
+    const int Hi = H / 2, Wi = W / 2;
+    const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 2 * cu / std::max(1, B)));
+    for (int b = 0; b < B; ++b) {
+      double* st = ws.stats + b * sstride + (size_t)stat_deconv(g.nsrc, 1, 0) * kSlots * 2;
+      hipLaunchKernelGGL(deconv_kernel, dim3(blocks, 1), dim3(256), 0, s,
+                         ws.h[3][nxt] + (size_t)b * 16 * Hi * Wi, params + L.pk_off[P_D1W],
+                         params + L.pk_off[P_D1B], Hi, Wi, ws.u1 + (size_t)b * 16 * 4 * Hi * Wi,
+                         st);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+  }
+  // cell 4: [gnrelu(u1), h0', h4] @ H
+  for (int b = 0; b < B; ++b) {
+    const double* st = ws.stats + b * sstride + (size_t)stat_deconv(g.nsrc, 1, 0) * kSlots * 2;
+    const size_t hw = (size_t)H * W;
+    CellArgs a4 = cell(4, {{ws.u1 + b * 16 * hw, 16, SRC_GNRELU, st, params + L.pk_off[P_D1GW],
+                            params + L.pk_off[P_D1GB]},
+                           {ws.h[0][nxt] + b * 16 * hw, 16, SRC_PLAIN, nullptr, nullptr, nullptr},
+                           {ws.h[4][cur] + b * 8 * hw, 8, SRC_PLAIN, nullptr, nullptr, nullptr}},
+                       1);
+    a4.B = 1;
+    a4.h_new += b * 8 * hw;
+    a4.c += b * 8 * hw;
+    if ((e = run_cell<40, 8, 8>(a4, cu, s)) != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_head_wta(const float* params, const SweepGeom& g, const Workspace& ws,
+                           int parity, const float* depth_values, int d, float* cost_out,
+                           bool wta, hipStream_t s) {
+  const ParamLayout& L = param_layout();
+  const int nxt = (parity & 1) ^ 1;
+  const int HW = g.H * g.W;
+  const int blocks = std::max(1, std::min((HW + 255) / 256, 8 * g.cu_count / std::max(1, g.B)));
+  hipLaunchKernelGGL(head_wta_kernel, dim3(blocks, g.B), dim3(256), 0, s, ws.h[4][nxt],
+                     params + L.pk_off[P_HW], params + L.pk_off[P_HB], g.H, g.W, depth_values, d,
+                     g.D, cost_out, wta ? 1 : 0, ws.max_prob, ws.exp_sum, ws.depth);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize(const SweepGeom& g, const Workspace& ws, float* depth_out,
+                           float* conf_out, hipStream_t s) {
+  const size_t n = (size_t)g.B * g.H * g.W;
+  const int blocks = (int)std::min<size_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(finalize_kernel, dim3(blocks), dim3(256), 0, s, ws.max_prob, ws.exp_sum,
+                     ws.depth, n, depth_out, conf_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
+                                hipStream_t s) {
+  const int blocks = std::max(1, std::min((HW + 255) / 256, 4096));
+  hipLaunchKernelGGL(softmax_depth_kernel, dim3(blocks, B), dim3(256), 0, s, cost, prob, D, HW);
+  return hipGetLastError();
+}
+
+}  // namespace aarmvs

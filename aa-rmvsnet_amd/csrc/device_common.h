@@ -1,0 +1,70 @@
+// Device-side helpers shared by the kernels: wave/block reductions, GroupNorm
+// statistics in fp64 atomic slots, activation functions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "aarmvs_internal.h"
+
+namespace aarmvs {
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum of NV values per thread; result valid in thread 0.
+// `red` is LDS scratch of at least NV * (blockDim.x / 64) floats.
+template <int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[i * nw + wid] = v[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float s = 0.f;
+      for (int w = 0; w < nw; ++w) s += red[i * nw + w];
+      v[i] = s;
+    }
+  }
+  __syncthreads();
+}
+
+// Add (sum, sumsq) into the statistic's slot picked by the block id.
+__device__ __forceinline__ void stat_add(double* stat, double s, double ss) {
+  double* slot = stat + 2 * (blockIdx.x % kSlots);
+  atomicAdd(slot, s);
+  atomicAdd(slot + 1, ss);
+}
+
+// GroupNorm fused parameters from fp64 slot sums: y = x * a + b with
+// a = rstd * gamma, b = beta - mean * a  (the ATen CPU group_norm form).
+struct GnStat {
+  float mean, rstd;
+};
+__device__ __forceinline__ GnStat stat_read(const double* stat, double n) {
+  double s = 0.0, ss = 0.0;
+  for (int i = 0; i < kSlots; ++i) {
+    s += stat[2 * i];
+    ss += stat[2 * i + 1];
+  }
+  const double mean = s / n;
+  double var = ss / n - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  GnStat r;
+  r.mean = (float)mean;
+  r.rstd = (float)(1.0 / sqrt(var + (double)kGnEps));
+  return r;
+}
+
+}  // namespace aarmvs

@@ -1,0 +1,123 @@
+/*
+ * aarmvs.h — C ABI of the MI355X (gfx950) depth-sweep library (libaarmvs.so).
+ *
+ * This is the drop-in boundary beneath the reference's Python API
+ * (BuTTerK3ks/AA-RMVSNet, models/drmvsnet.py).  The reference has no native
+ * layer: every entry point below replaces a block of PyTorch ops inside
+ * EMVSNet.forward's depth loop (models/drmvsnet.py:255-345).  The Python mirror
+ * in aa-rmvsnet_amd/models binds these with ctypes.
+ *
+ * Conventions
+ *   - All tensors are fp32, contiguous, NCHW, resident in device memory and owned
+ *     by the caller; the library never allocates device memory and keeps no
+ *     pointer across calls.
+ *   - Every launch goes to the caller's stream; no host synchronisation happens
+ *     inside any entry point (graph-capturable).
+ *   - Return 0 on success, a nonzero aarmvs_status otherwise; the message is in
+ *     aarmvs_last_error() (thread-local).  Shapes are validated before launch.
+ *   - Constraints (from the reference's own shape rules): C == 32 feature
+ *     channels, H % 4 == 0 and W % 4 == 0 (two 2x2 max-pools and two stride-2
+ *     deconvs must round-trip, drmvsnet.py:148-161), 1 <= nsrc <= AARMVS_MAX_SRC.
+ */
+#ifndef AARMVS_H_
+#define AARMVS_H_
+
+#include <stddef.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AARMVS_MAX_SRC 16
+#define AARMVS_FEAT_C 32
+
+typedef enum aarmvs_status {
+  AARMVS_OK = 0,
+  AARMVS_ERR_INVALID = 1,   /* bad shape / null pointer / unsupported argument */
+  AARMVS_ERR_HIP = 2        /* a HIP runtime call or kernel launch failed     */
+} aarmvs_status;
+
+const char* aarmvs_last_error(void);
+const char* aarmvs_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Parameters.
+ * The raw blob is the sweep's checkpoint tensors (the 48 omega.* and
+ * cost_regularization.* keys of the reference state_dict, drmvsnet.py:66-117 and
+ * :27-38) flattened and concatenated in this order:
+ *   omega.reweight_network.0.0.weight [4,32,3,3], .0.0.bias [4], .0.1.weight [4],
+ *   .0.1.bias [4], .1.stem.0.0.weight [4,4,1,1], .1.stem.0.0.bias [4],
+ *   .1.stem.0.1.weight [4], .1.stem.0.1.bias [4], .1.stem.1.weight [4,4,1,1],
+ *   .1.stem.1.bias [4], .1.stem.2.weight [4], .1.stem.2.bias [4],
+ *   .2.weight [1,4,1,1], .2.bias [1],
+ *   cost_regularization.cell_list.{0..4}.conv.{weight,bias}
+ *     ([64,48,3,3],[64],[64,32,3,3],[64],[64,32,3,3],[64],[64,48,3,3],[64],[32,40,3,3],[32]),
+ *   cost_regularization.deconv_{0,1}.{conv.weight [16,16,3,3], conv.bias [16],
+ *     gn.weight [16], gn.bias [16]},
+ *   cost_regularization.conv_0.weight [1,8,3,3], cost_regularization.conv_0.bias [1].
+ * aarmvs_pack_params rearranges it (on the device) into the kernels' layout.
+ * ------------------------------------------------------------------------- */
+size_t aarmvs_param_count(void);            /* floats in the raw blob            */
+size_t aarmvs_packed_param_bytes(void);     /* bytes of the packed device buffer */
+int aarmvs_pack_params(const float* raw_params, void* packed, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * homo_warping_depthwise (models/module.py:6-38): bilinear warp of src_fea
+ * [B,C,H,W] into the reference view at one depth per batch element.
+ * rel_proj [B,12] = rows 0..2 of src_proj @ inverse(ref_proj) (module.py:16-18),
+ * depth [B].  grid_sample semantics: bilinear, zero padding, align_corners=False
+ * applied to the align_corners=True-normalised grid.
+ * ------------------------------------------------------------------------- */
+int aarmvs_homo_warp(const float* src_fea, const float* rel_proj, const float* depth,
+                     int B, int C, int H, int W, float* out, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Whole depth sweep (drmvsnet.py:273-291 train / :306-342 eval).
+ * Replaces, per plane d: homo_warping_depthwise x nsrc, (warp-ref)^2, omega
+ * re-weighting, weighted accumulation, UNetConvLSTM.forward and the online WTA.
+ * ------------------------------------------------------------------------- */
+typedef struct aarmvs_sweep_args {
+  int B, C, H, W;                         /* C must be 32                         */
+  int nsrc;                               /* N-1 source views                     */
+  int D;                                  /* depth hypotheses (depth_values.shape[1]) */
+  int d_begin, d_end;                     /* plane range; d_begin == 0 resets state */
+  const float* ref_fea;                   /* [B,C,H,W]                             */
+  const float* src_fea[AARMVS_MAX_SRC];   /* nsrc x [B,C,H,W]                      */
+  const float* rel_proj;                  /* [nsrc][B][12]                         */
+  const float* depth_values;              /* [B,D]                                 */
+  const void* packed_params;              /* from aarmvs_pack_params               */
+  void* workspace;                        /* aarmvs_sweep_workspace_bytes() bytes  */
+  float* depth_out;                       /* [B,H,W] WTA depth, or NULL            */
+  float* conf_out;                        /* [B,H,W] max_prob / exp_sum, or NULL   */
+  float* cost_out;                        /* [B,D,H,W] regulariser output, or NULL */
+  float* slice_out;                       /* debug: [B,32,H,W] last plane's cost slice, or NULL */
+  float* omega_out;                       /* debug: [nsrc,B,H,W] last plane's omega weights, or NULL */
+} aarmvs_sweep_args;
+
+size_t aarmvs_sweep_workspace_bytes(int B, int H, int W, int nsrc);
+int aarmvs_sweep(const aarmvs_sweep_args* args, hipStream_t stream);
+
+/* Hidden state of the regulariser inside the workspace, for inspection/BPTT:
+ * cell k in 0..4, which = 0 for h, 1 for c.  Valid after an aarmvs_sweep call;
+ * returns a device pointer to [B,hid_k,H_k,W_k] or NULL. */
+float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int plane_parity,
+                        int cell, int which);
+
+/* ---------------------------------------------------------------------------
+ * One UNetConvLSTM step (drmvsnet.py:119-167) on a given cost slice x [B,32,H,W]
+ * using the hidden state held in `workspace` (same layout as aarmvs_sweep).
+ * step == 0 zero-initialises the state (drmvsnet.py:133-134).  cost_out [B,1,H,W].
+ * ------------------------------------------------------------------------- */
+int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
+                     const void* packed_params, void* workspace, float* cost_out,
+                     hipStream_t stream);
+
+/* softmax over the depth axis of cost [B,D,H,W] (drmvsnet.py:291/:342). */
+int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
+                         hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AARMVS_H_ */

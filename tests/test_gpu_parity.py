@@ -1,0 +1,157 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the golden fixtures
+made by running the reference, and against the CPU oracle at larger sizes.
+
+Tolerances: per-op <= 1e-5 abs where the reference computes a single op, cost
+slices/states 1e-4 (fp32 reassociation in conv sums), depth maps <= 1e-3
+relative L1 (BASELINE.json north_star).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from aarmvs import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def rel_l1(a, b):
+    return float(np.abs(a - b).sum() / max(np.abs(b).sum(), 1e-30))
+
+
+def P_of(wseed, device=DEV):
+    return {k: torch.from_numpy(v).to(device) for k, v in syn.sweep_weights(wseed).items()}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+    from aarmvs import ops  # noqa: F401  (loads libaarmvs.so, raises if missing)
+
+
+def test_homo_warp_matches_reference():
+    from aarmvs import ops
+    g = load("warp.npz")
+    B, N, H, W, C = (int(x) for x in g["shape"])
+    sc = syn.scene(B, N, H, W, D=4, seed=int(g["seed"]), C=C)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    feats = torch.from_numpy(sc["features"]).to(DEV)
+    for v in range(1, N):
+        rel = ops.relative_projection(proj[:, v], proj[:, 0])
+        for d in range(4):
+            out = ops.homo_warp(feats[v], rel, torch.from_numpy(g["depths"][:, d]))
+            np.testing.assert_allclose(out.cpu().numpy(), g["out"][v - 1, d], atol=1e-5, rtol=0)
+
+
+def _sweep_obj(wseed):
+    from aarmvs import ops
+    return ops.DepthSweep(P_of(wseed), DEV)
+
+
+def test_cost_slice_and_omega_match_reference():
+    g = load("cost_slice.npz")
+    B, N, H, W, D = (int(x) for x in g["shape"])
+    sc = syn.scene(B, N, H, W, D, seed=int(g["seed"]))
+    feats = torch.from_numpy(sc["features"]).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    d = int(g["plane"])
+    sw = _sweep_obj(int(g["wseed"]))
+    out = sw(feats[0], [feats[v] for v in range(1, N)], proj[:, 0], [proj[:, v] for v in range(1, N)],
+             torch.from_numpy(sc["depth_values"][:, d:d + 1].copy()), want_depth=False, debug=True)
+    np.testing.assert_allclose(out["omega"].cpu().numpy(), g["omega"], atol=1e-5)
+    np.testing.assert_allclose(out["slice"].cpu().numpy(), g["slice"], atol=1e-4, rtol=1e-5)
+
+
+def test_unet_steps_match_reference():
+    g = load("unet.npz")
+    B, H, W, steps = (int(x) for x in g["shape"])
+    xs = np.random.default_rng(int(g["seed"])).standard_normal((steps, B, 32, H, W), dtype=np.float32)
+    sw = _sweep_obj(int(g["wseed"]))
+    for s in range(steps):
+        cost = sw.unet_step(torch.from_numpy(xs[s]).to(DEV), s)
+        np.testing.assert_allclose(cost.cpu().numpy(), g["cost"][s], atol=1e-5, rtol=1e-5)
+    for i in range(5):
+        h = sw.state(B, H, W, 1, steps & 1, i, 0).cpu().numpy()
+        c = sw.state(B, H, W, 1, steps & 1, i, 1).cpu().numpy()
+        np.testing.assert_allclose(h, g[f"h{i}"], atol=1e-5)
+        np.testing.assert_allclose(c, g[f"c{i}"], atol=1e-5)
+
+
+def _run(g, **kw):
+    B, N, H, W, D = (int(x) for x in g["shape"])
+    desc = bool(g["descending"]) if "descending" in g.files else False
+    sc = syn.scene(B, N, H, W, D, seed=int(g["seed"]), descending=desc)
+    assert syn.array_digest(sc["features"], sc["proj_matrices"], sc["depth_values"]) == str(g["digest"])
+    feats = torch.from_numpy(sc["features"]).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    sw = _sweep_obj(int(g["wseed"]))
+    return sw(feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+              [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]), **kw)
+
+
+@pytest.mark.parametrize("name", ["sweep_eval.npz", "sweep_eval_desc.npz"])
+def test_eval_sweep_matches_reference(name):
+    g = load(name)
+    out = _run(g)
+    assert rel_l1(out["depth"].cpu().numpy(), g["depth"]) <= 1e-3
+    np.testing.assert_allclose(out["conf"].cpu().numpy(), g["conf"], atol=1e-4)
+
+
+def test_train_sweep_prob_volume_matches_reference():
+    from aarmvs import ops
+    g = load("sweep_train.npz")
+    out = _run(g, want_depth=False, want_cost=True)
+    prob = ops.softmax_depth(out["cost"])
+    np.testing.assert_allclose(prob.cpu().numpy(), g["prob"], atol=1e-5)
+
+
+def test_config1_matches_reference():
+    from aarmvs import ops
+    g = load("config1.npz")
+    out = _run(g, want_cost=True)
+    assert rel_l1(out["depth"].cpu().numpy(), g["depth"]) <= 1e-3
+    np.testing.assert_allclose(out["conf"].cpu().numpy(), g["conf"], atol=1e-4)
+    p = ops.softmax_depth(out["cost"]).cpu().numpy()
+    np.testing.assert_allclose(p[:, :, ::8, ::8], g["prob_sub"], atol=1e-5)
+    np.testing.assert_allclose(p.mean(axis=(2, 3)), g["prob_plane_mean"], atol=1e-6)
+
+
+def test_larger_views_and_batch_match_oracle():
+    """N=6 views, B=2, 96x200 (W not a multiple of 32): HIP vs the CPU oracle."""
+    from oracle import sweep_oracle as orc
+    B, N, H, W, D = 2, 6, 96, 200, 5
+    sc = syn.scene(B, N, H, W, D, seed=41)
+    P = {k: torch.from_numpy(v) for k, v in syn.sweep_weights(3).items()}
+    feats = torch.from_numpy(sc["features"])
+    proj = torch.from_numpy(sc["proj_matrices"])
+    ref = orc.sweep(feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+                    [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]), P)
+    from aarmvs import ops
+    sw = ops.DepthSweep({k: v.to(DEV) for k, v in P.items()}, DEV)
+    fd = feats.to(DEV)
+    out = sw(fd[0], [fd[v] for v in range(1, N)], proj[:, 0], [proj[:, v] for v in range(1, N)],
+             torch.from_numpy(sc["depth_values"]), want_cost=True)
+    np.testing.assert_allclose(out["cost"].cpu().numpy(), ref["cost"].numpy(), atol=1e-4, rtol=1e-4)
+    assert rel_l1(out["depth"].cpu().numpy(), ref["depth"].numpy()) <= 1e-3
+
+
+def test_rejects_cpu_tensors_and_bad_shapes():
+    from aarmvs import ops
+    from aarmvs._lib import AarmvsError
+    sw = _sweep_obj(1)
+    x = torch.zeros(1, 32, 16, 16)
+    proj = torch.eye(4).expand(1, 4, 4)
+    with pytest.raises(AarmvsError):
+        sw(x, [x], proj, [proj], torch.ones(1, 2))
+    y = torch.zeros(1, 32, 18, 16, device=DEV)
+    with pytest.raises(AarmvsError):
+        sw(y, [y], proj, [proj], torch.ones(1, 2))

@@ -1,0 +1,44 @@
+"""CPU-side checks of the C-ABI library: it loads, and exports every function that
+include/aarmvs.h declares (no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "aarmvs.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(aarmvs_[a-z_]+)\s*\(", text)))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    for n in ("aarmvs_sweep", "aarmvs_homo_warp", "aarmvs_pack_params", "aarmvs_unet_step",
+              "aarmvs_softmax_depth", "aarmvs_sweep_workspace_bytes", "aarmvs_last_error"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    from aarmvs import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail("libaarmvs.so is not built (run __graft_entry__.build())")
+    handle = ctypes.CDLL(_lib.LIB_PATH)
+    for n in declared_functions():
+        assert hasattr(handle, n), n
+    assert set(_lib.SIGNATURES) == set(declared_functions())
+
+
+def test_host_only_queries():
+    from aarmvs import lib
+    L = lib()
+    assert L.aarmvs_param_count() == 109970          # omega 1,225 + regulariser 108,745
+    assert L.aarmvs_packed_param_bytes() >= 109970 * 4
+    assert L.aarmvs_sweep_workspace_bytes(1, 128, 160, 2) > 0
+    assert L.aarmvs_sweep_workspace_bytes(1, 130, 160, 2) == 0   # H % 4 != 0 rejected
+    assert b"multiple" in L.aarmvs_last_error()

@@ -1,0 +1,113 @@
+"""Pin the CPU oracle against the golden fixtures produced by running the reference.
+
+CPU-only (``-m "not gpu"``).  Tolerances: per-op <=1e-5 abs, end-to-end
+depth <=1e-3 relative L1 (BASELINE.json north_star).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from aarmvs import synthetic as syn
+from oracle import sweep_oracle as orc
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def P_of(wseed):
+    return {k: torch.from_numpy(v) for k, v in syn.sweep_weights(wseed).items()}
+
+
+def rel_l1(a, b):
+    return float(np.abs(a - b).sum() / max(np.abs(b).sum(), 1e-30))
+
+
+def test_inputs_regenerate_bit_identically():
+    g = load("warp.npz")
+    B, N, H, W, C = g["shape"]
+    sc = syn.scene(B, N, H, W, D=4, seed=int(g["seed"]), C=C)
+    assert syn.array_digest(sc["features"], sc["proj_matrices"]) == str(g["digest"])
+
+
+def test_warp_matches_reference():
+    g = load("warp.npz")
+    B, N, H, W, C = (int(x) for x in g["shape"])
+    sc = syn.scene(B, N, H, W, D=4, seed=int(g["seed"]), C=C)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    feats = torch.from_numpy(sc["features"])
+    for v in range(1, N):
+        rel = orc.relative_projection(proj[:, v], proj[:, 0])
+        for d in range(4):
+            out = orc.homo_warp(feats[v], rel, torch.from_numpy(g["depths"][:, d])).numpy()
+            np.testing.assert_allclose(out, g["out"][v - 1, d], atol=1e-5, rtol=0)
+
+
+def test_omega_and_cost_slice_match_reference():
+    g = load("cost_slice.npz")
+    B, N, H, W, D = (int(x) for x in g["shape"])
+    sc = syn.scene(B, N, H, W, D, seed=int(g["seed"]))
+    P = P_of(int(g["wseed"]))
+    proj = torch.from_numpy(sc["proj_matrices"])
+    feats = torch.from_numpy(sc["features"])
+    d = int(g["plane"])
+    dv = torch.from_numpy(sc["depth_values"][:, d])
+    rels = [orc.relative_projection(proj[:, v], proj[:, 0]) for v in range(1, N)]
+    for v in range(1, N):
+        sq = (orc.homo_warp(feats[v], rels[v - 1], dv) - feats[0]).pow(2)
+        np.testing.assert_allclose(orc.omega_weight(sq, P).numpy(), g["omega"][v - 1], atol=1e-5)
+    x = orc.cost_slice(feats[0], [feats[v] for v in range(1, N)], rels, dv, P).numpy()
+    np.testing.assert_allclose(x, g["slice"], atol=1e-4, rtol=1e-5)
+
+
+def test_unet_steps_match_reference():
+    g = load("unet.npz")
+    B, H, W, steps = (int(x) for x in g["shape"])
+    P = P_of(int(g["wseed"]))
+    xs = np.random.default_rng(int(g["seed"])).standard_normal((steps, B, 32, H, W), dtype=np.float32)
+    state = orc.init_state(B, H, W)
+    for s in range(steps):
+        cost, state = orc.unet_step(torch.from_numpy(xs[s]), state, P)
+        np.testing.assert_allclose(cost.numpy(), g["cost"][s], atol=1e-5)
+    for i in range(5):
+        np.testing.assert_allclose(state[i][0].numpy(), g[f"h{i}"], atol=1e-5)
+        np.testing.assert_allclose(state[i][1].numpy(), g[f"c{i}"], atol=1e-5)
+
+
+def _sweep(g, want_volume):
+    B, N, H, W, D = (int(x) for x in g["shape"])
+    desc = bool(g["descending"]) if "descending" in g.files else False
+    sc = syn.scene(B, N, H, W, D, seed=int(g["seed"]), descending=desc)
+    assert syn.array_digest(sc["features"], sc["proj_matrices"], sc["depth_values"]) == str(g["digest"])
+    feats = torch.from_numpy(sc["features"])
+    proj = torch.from_numpy(sc["proj_matrices"])
+    return orc.sweep(feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+                     [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]),
+                     P_of(int(g["wseed"])), want_volume=want_volume)
+
+
+@pytest.mark.parametrize("name", ["sweep_eval.npz", "sweep_eval_desc.npz"])
+def test_eval_sweep_matches_reference(name):
+    g = load(name)
+    out = _sweep(g, want_volume=False)
+    assert rel_l1(out["depth"].numpy(), g["depth"]) <= 1e-3
+    np.testing.assert_allclose(out["conf"].numpy(), g["conf"], atol=1e-4)
+
+
+def test_train_sweep_prob_volume_matches_reference():
+    g = load("sweep_train.npz")
+    out = _sweep(g, want_volume=True)
+    np.testing.assert_allclose(out["prob"].numpy(), g["prob"], atol=1e-5)
+
+
+def test_config1_matches_reference():
+    g = load("config1.npz")
+    out = _sweep(g, want_volume=True)
+    assert rel_l1(out["depth"].numpy(), g["depth"]) <= 1e-3
+    np.testing.assert_allclose(out["conf"].numpy(), g["conf"], atol=1e-4)
+    p = out["prob"].numpy()
+    np.testing.assert_allclose(p[:, :, ::8, ::8], g["prob_sub"], atol=1e-5)
+    np.testing.assert_allclose(p.mean(axis=(2, 3)), g["prob_plane_mean"], atol=1e-6)
