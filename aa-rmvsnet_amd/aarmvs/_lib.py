@@ -50,6 +50,12 @@ SIGNATURES = {
     "aarmvs_unet_step": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),
     "aarmvs_softmax_depth": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "aarmvs_profile_enable": (None, [c_int]),
+    "aarmvs_profile_reset": (None, []),
+    "aarmvs_profile_kernel_count": (c_int, []),
+    "aarmvs_profile_kernel_name": (c_char_p, [c_int]),
+    "aarmvs_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_longlong),
+                                    ctypes.POINTER(ctypes.c_double)]),
 }
 
 _LIB = None

@@ -176,3 +176,27 @@ class DepthSweep:
         check(lib().aarmvs_unet_step(x.data_ptr(), B, H, W, nsrc, step, self.packed.data_ptr(),
                                      ws.data_ptr(), cost.data_ptr(), _stream()), "unet_step")
         return cost
+
+
+# ----------------------------------------------------------------------------------
+# opt-in per-kernel timing (aarmvs_profile_*): hipEvents on the launch stream
+# ----------------------------------------------------------------------------------
+def profile_enable(on: bool = True) -> None:
+    lib().aarmvs_profile_enable(1 if on else 0)
+
+
+def profile_reset() -> None:
+    lib().aarmvs_profile_reset()
+
+
+def profile_read() -> dict:
+    """{kernel name: (launches, total device ms)} since the last reset."""
+    L = lib()
+    out = {}
+    for i in range(L.aarmvs_profile_kernel_count()):
+        n = ctypes.c_longlong(0)
+        ms = ctypes.c_double(0.0)
+        check(L.aarmvs_profile_read(i, ctypes.byref(n), ctypes.byref(ms)), "profile_read")
+        if n.value:
+            out[L.aarmvs_profile_kernel_name(i).decode()] = (int(n.value), float(ms.value))
+    return out

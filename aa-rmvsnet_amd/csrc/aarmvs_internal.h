@@ -106,4 +106,27 @@ hipError_t launch_softmax_depth(const float* cost, float* prob, int B, int D, in
 
 int cu_count();
 
+// ---------------------------------------------------------------------------
+// Opt-in per-kernel timing (aarmvs_profile_*): hipEvents recorded on the launch
+// stream around each kernel.  Off by default; costs nothing when off.
+// ---------------------------------------------------------------------------
+enum KernelId : int {
+  K_COST_T1, K_OMEGA1, K_OMEGA2, K_COST_FINAL,
+  K_CELL0, K_CELL1, K_CELL2, K_CELL3, K_CELL4,
+  K_DECONV0, K_DECONV1, K_HEAD_WTA, K_FINALIZE, K_SOFTMAX, K_WARP,
+  K_COUNT
+};
+extern bool g_prof_on;
+void prof_mark(hipStream_t s, int id, bool begin);
+struct ProfScope {
+  hipStream_t s;
+  int id;
+  ProfScope(hipStream_t s_, int id_) : s(s_), id(id_) {
+    if (g_prof_on) prof_mark(s, id, true);
+  }
+  ~ProfScope() {
+    if (g_prof_on) prof_mark(s, id, false);
+  }
+};
+
 }  // namespace aarmvs

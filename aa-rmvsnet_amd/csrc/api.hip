@@ -5,7 +5,9 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "aarmvs_internal.h"
 
@@ -37,6 +39,62 @@ const ParamLayout& param_layout() {
     return l;
   }();
   return L;
+}
+
+// ---------------------------------------------------------------------------
+// Opt-in kernel timer (aarmvs_profile_*).  Events come from a pool that grows to
+// the largest profiling window and is reused after aarmvs_profile_reset.
+// ---------------------------------------------------------------------------
+bool g_prof_on = false;
+static std::mutex g_prof_mu;
+static std::vector<hipEvent_t> g_prof_pool;
+static size_t g_prof_used = 0;
+struct ProfRec {
+  int id;
+  hipEvent_t a, b;
+};
+static std::vector<ProfRec> g_prof_recs;
+static hipEvent_t g_prof_open[K_COUNT];
+static double g_prof_ms[K_COUNT];
+static long long g_prof_n[K_COUNT];
+
+static const char* kKernelNames[K_COUNT] = {
+    "cost_t1", "omega_stats1", "omega_stats2", "cost_final",
+    "lstm_cell0", "lstm_cell1", "lstm_cell2", "lstm_cell3", "lstm_cell4",
+    "deconv0", "deconv1", "head_wta", "finalize", "softmax_depth", "homo_warp"};
+
+static hipEvent_t prof_event() {
+  if (g_prof_used == g_prof_pool.size()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    g_prof_pool.push_back(e);
+  }
+  return g_prof_pool[g_prof_used++];
+}
+
+void prof_mark(hipStream_t s, int id, bool begin) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  hipEvent_t e = prof_event();
+  if (!e) return;
+  (void)hipEventRecord(e, s);
+  if (begin) {
+    g_prof_open[id] = e;
+  } else if (g_prof_open[id]) {
+    g_prof_recs.push_back({id, g_prof_open[id], e});
+    g_prof_open[id] = nullptr;
+  }
+}
+
+static void prof_fold() {
+  for (const ProfRec& r : g_prof_recs) {
+    float ms = 0.f;
+    if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+      g_prof_ms[r.id] += ms;
+      g_prof_n[r.id] += 1;
+    }
+  }
+  g_prof_recs.clear();
+  g_prof_used = 0;
 }
 
 int cu_count() {
@@ -130,6 +188,37 @@ using namespace aarmvs;
 extern "C" {
 
 const char* aarmvs_last_error(void) { return g_err.c_str(); }
+
+void aarmvs_profile_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_on = on != 0;
+}
+
+void aarmvs_profile_reset(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  prof_fold();
+  for (int i = 0; i < K_COUNT; ++i) {
+    g_prof_ms[i] = 0.0;
+    g_prof_n[i] = 0;
+    g_prof_open[i] = nullptr;
+  }
+}
+
+int aarmvs_profile_kernel_count(void) { return K_COUNT; }
+
+const char* aarmvs_profile_kernel_name(int id) {
+  return (id >= 0 && id < K_COUNT) ? kKernelNames[id] : nullptr;
+}
+
+int aarmvs_profile_read(int id, long long* launches, double* total_ms) {
+  if (id < 0 || id >= K_COUNT || !launches || !total_ms)
+    return fail(AARMVS_ERR_INVALID, "profile_read: bad arguments");
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  prof_fold();
+  *launches = g_prof_n[id];
+  *total_ms = g_prof_ms[id];
+  return AARMVS_OK;
+}
 const char* aarmvs_version(void) { return "aarmvs-mi355x 0.1 (gfx950)"; }
 
 size_t aarmvs_param_count(void) { return param_layout().raw_total; }

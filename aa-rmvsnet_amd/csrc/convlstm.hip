@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(TH * 64) lstm_cell_kernel(CellArgs a) {
 }
 
 template <int CIN, int HID, int TH>
-static hipError_t run_cell(const CellArgs& a, int cu, hipStream_t s) {
+static hipError_t run_cell(const CellArgs& a, int cu, int kid, hipStream_t s) {
   using Cfg = CellCfg<CIN, HID, TH>;
   static_assert(Cfg::LDS_BYTES <= 160 * 1024, "cell tile exceeds LDS");
   static bool attr_set = false;
@@ -177,6 +177,7 @@ static hipError_t run_cell(const CellArgs& a, int cu, hipStream_t s) {
   }
   const int ntiles = a.B * ((a.W + 31) / 32) * ((a.H + TH - 1) / TH);
   const int grid = std::max(1, std::min(ntiles, cu));
+  ProfScope ps(s, kid);
   hipLaunchKernelGGL((lstm_cell_kernel<CIN, HID, TH>), dim3(grid), dim3(Cfg::THREADS),
                      Cfg::LDS_BYTES, s, a);
   return hipGetLastError();
@@ -258,6 +259,8 @@ __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__
                                                        int wta, float* __restrict__ max_prob,
                                                        float* __restrict__ exp_sum,
                                                        float* __restrict__ depth) {
+#pragma clang fp contract(off)
+  // the select arithmetic of drmvsnet.py:328-333 is reproduced op for op
   const int b = blockIdx.y, HW = H * W;
   const float* hb = h4 + (size_t)b * 8 * HW;
   const float dv = wta ? dvals[b * D + d] : 0.0f;
@@ -339,15 +342,15 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // cell 0: [x, h0] @ H
   CellArgs a0 = cell(0, {{x, 32, SRC_PLAIN, nullptr, nullptr, nullptr},
                          {ws.h[0][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
-  if ((e = run_cell<48, 16, 4>(a0, cu, s)) != hipSuccess) return e;
+  if ((e = run_cell<48, 16, 4>(a0, cu, K_CELL0, s)) != hipSuccess) return e;
   // cell 1: [maxpool(h0'), h1] @ H/2
   CellArgs a1 = cell(1, {{ws.h[0][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {ws.h[1][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 2);
-  if ((e = run_cell<32, 16, 8>(a1, cu, s)) != hipSuccess) return e;
+  if ((e = run_cell<32, 16, 8>(a1, cu, K_CELL1, s)) != hipSuccess) return e;
   // cell 2: [maxpool(h1'), h2] @ H/4
   CellArgs a2 = cell(2, {{ws.h[1][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {ws.h[2][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
-  if ((e = run_cell<32, 16, 8>(a2, cu, s)) != hipSuccess) return e;
+  if ((e = run_cell<32, 16, 8>(a2, cu, K_CELL2, s)) != hipSuccess) return e;
   // GroupNorm statistics are per batch element, so the deconvs and the two cells that
   // consume their normalised output are launched per batch element.
   const size_t sstride = (size_t)nstat(g.nsrc) * kSlots * 2;
@@ -357,6 +360,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 2 * cu / std::max(1, B)));
     for (int b = 0; b < B; ++b) {
       double* st = ws.stats + b * sstride + (size_t)stat_deconv(g.nsrc, 0, 0) * kSlots * 2;
+      ProfScope ps(s, K_DECONV0);
       hipLaunchKernelGGL(deconv_kernel, dim3(blocks, 1), dim3(256), 0, s,
                          ws.h[2][nxt] + (size_t)b * 16 * Hi * Wi, params + L.pk_off[P_D0W],
                          params + L.pk_off[P_D0B], Hi, Wi, ws.u0 + (size_t)b * 16 * 4 * Hi * Wi,
@@ -376,7 +380,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a3.B = 1;
     a3.h_new += b * 16 * hq;
     a3.c += b * 16 * hq;
-    if ((e = run_cell<48, 16, 4>(a3, cu, s)) != hipSuccess) return e;
+    if ((e = run_cell<48, 16, 4>(a3, cu, K_CELL3, s)) != hipSuccess) return e;
   }
   // deconv_1: h3' (H/2) -> u1 (H) + GN stats
   {
@@ -384,6 +388,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 2 * cu / std::max(1, B)));
     for (int b = 0; b < B; ++b) {
       double* st = ws.stats + b * sstride + (size_t)stat_deconv(g.nsrc, 1, 0) * kSlots * 2;
+      ProfScope ps(s, K_DECONV1);
       hipLaunchKernelGGL(deconv_kernel, dim3(blocks, 1), dim3(256), 0, s,
                          ws.h[3][nxt] + (size_t)b * 16 * Hi * Wi, params + L.pk_off[P_D1W],
                          params + L.pk_off[P_D1B], Hi, Wi, ws.u1 + (size_t)b * 16 * 4 * Hi * Wi,
@@ -403,7 +408,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a4.B = 1;
     a4.h_new += b * 8 * hw;
     a4.c += b * 8 * hw;
-    if ((e = run_cell<40, 8, 8>(a4, cu, s)) != hipSuccess) return e;
+    if ((e = run_cell<40, 8, 8>(a4, cu, K_CELL4, s)) != hipSuccess) return e;
   }
   return hipSuccess;
 }
@@ -415,6 +420,7 @@ hipError_t launch_head_wta(const float* params, const SweepGeom& g, const Worksp
   const int nxt = (parity & 1) ^ 1;
   const int HW = g.H * g.W;
   const int blocks = std::max(1, std::min((HW + 255) / 256, 8 * g.cu_count / std::max(1, g.B)));
+  ProfScope ps(s, K_HEAD_WTA);
   hipLaunchKernelGGL(head_wta_kernel, dim3(blocks, g.B), dim3(256), 0, s, ws.h[4][nxt],
                      params + L.pk_off[P_HW], params + L.pk_off[P_HB], g.H, g.W, depth_values, d,
                      g.D, cost_out, wta ? 1 : 0, ws.max_prob, ws.exp_sum, ws.depth);
@@ -425,6 +431,7 @@ hipError_t launch_finalize(const SweepGeom& g, const Workspace& ws, float* depth
                            float* conf_out, hipStream_t s) {
   const size_t n = (size_t)g.B * g.H * g.W;
   const int blocks = (int)std::min<size_t>((n + 255) / 256, 4096);
+  ProfScope ps(s, K_FINALIZE);
   hipLaunchKernelGGL(finalize_kernel, dim3(blocks), dim3(256), 0, s, ws.max_prob, ws.exp_sum,
                      ws.depth, n, depth_out, conf_out);
   return hipGetLastError();
@@ -433,6 +440,7 @@ hipError_t launch_finalize(const SweepGeom& g, const Workspace& ws, float* depth
 hipError_t launch_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
                                 hipStream_t s) {
   const int blocks = std::max(1, std::min((HW + 255) / 256, 4096));
+  ProfScope ps(s, K_SOFTMAX);
   hipLaunchKernelGGL(softmax_depth_kernel, dim3(blocks, B), dim3(256), 0, s, cost, prob, D, HW);
   return hipGetLastError();
 }

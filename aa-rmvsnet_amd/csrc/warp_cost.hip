@@ -108,6 +108,7 @@ hipError_t launch_homo_warp(const float* src, const float* rel, const float* dep
                             int H, int W, float* out, hipStream_t s) {
   const int HW = H * W;
   dim3 grid((unsigned)std::min((HW + 255) / 256, 4096), (unsigned)B);
+  ProfScope ps(s, K_WARP);
   hipLaunchKernelGGL(homo_warp_kernel, grid, dim3(256), 0, s, src, rel, depth, C, H, W, out);
   return hipGetLastError();
 }
@@ -397,16 +398,28 @@ hipError_t launch_cost_slice(const CostArgs& ca, const SweepGeom& g, const Works
   const int HW = g.H * g.W;
   const int ntiles = ((g.W + T1_TW - 1) / T1_TW) * ((g.H + T1_TH - 1) / T1_TH);
   const int per_b = std::max(1, std::min(ntiles, 4 * g.cu_count / std::max(1, g.B)));
-  hipLaunchKernelGGL(cost_t1_kernel, dim3(per_b, g.B), dim3(256), 0, s, a);
+  {
+    ProfScope ps(s, K_COST_T1);
+    hipLaunchKernelGGL(cost_t1_kernel, dim3(per_b, g.B), dim3(256), 0, s, a);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int pblk = std::max(1, std::min((HW + 255) / 256, 2 * g.cu_count / std::max(1, g.B * g.nsrc) + 1));
-  hipLaunchKernelGGL(omega_stats_kernel<1>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a);
+  {
+    ProfScope ps(s, K_OMEGA1);
+    hipLaunchKernelGGL(omega_stats_kernel<1>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(omega_stats_kernel<2>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a);
+  {
+    ProfScope ps(s, K_OMEGA2);
+    hipLaunchKernelGGL(omega_stats_kernel<2>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int fblk = std::max(1, std::min((HW + 255) / 256, 8 * g.cu_count / std::max(1, g.B)));
-  hipLaunchKernelGGL(cost_final_kernel, dim3(fblk, g.B), dim3(256), 0, s, a);
+  {
+    ProfScope ps(s, K_COST_FINAL);
+    hipLaunchKernelGGL(cost_final_kernel, dim3(fblk, g.B), dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -1,0 +1,268 @@
+"""Depth-sweep throughput benchmark (BASELINE.json metric: depth-hypotheses/s).
+
+One "step" = one full D-plane sweep (EMVSNet's eval depth loop, drmvsnet.py:306-342:
+warp x (N-1), omega aggregation, ConvLSTM U-Net step, online WTA) over B reference
+views per GPU, with the per-view features already resident in HBM (FeatNet is out of
+scope).  ``value`` = ref-views x H x W x D x steps (all ranks) / max-over-ranks
+wall time of the timed region.
+
+Multi-GPU: one process per GPU (torchrun), reference views sharded across ranks, no
+data-path collective; the only collectives are the timing barrier and the
+max-over-ranks reduction of the elapsed time.
+
+Also reported on the same JSON line:
+  roofline      the dominant kernel's achieved algorithmic bytes (HBM-bound) or flops
+                (MFMA-bound) per launch / its average launch time, from hipEvents
+                recorded on the launch stream over the timed region;
+  kernels       the same figures for every kernel of the sweep;
+  cpu_baseline  the CPU oracle (oracle/sweep_oracle.py, a from-scratch fp32 restatement
+                of the reference, pinned to fixtures made by running the reference) timed
+                on this host's cores on a bounded sample (the first planes of the same
+                workload), rank 0 at N=1 only;
+  parity        HIP vs the oracle on that sample (cost max|err|, depth rel-L1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "aa-rmvsnet_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+from aarmvs import ops, synthetic as syn  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= vector) dense peak
+
+# BASELINE.json configs (name -> views N, H, W, D)
+CONFIGS = {
+    "plumbing_160x128_n3_d48": dict(N=3, H=128, W=160, D=48),       # configs[0]
+    "dtu_eval_800x600_n5_d256": dict(N=5, H=600, W=800, D=256),     # configs[1]
+    "dtu_eval_1600x1184_n7_d512": dict(N=7, H=1184, W=1600, D=512),  # configs[2] (headline)
+    "dtu_train_640x512_n3_d192": dict(N=3, H=512, W=640, D=192),    # configs[3] (sweep only)
+    "tnt_1920x1056_n11_d898": dict(N=11, H=1056, W=1920, D=898),    # configs[4]
+}
+DEFAULT_CONFIG = "dtu_eval_1600x1184_n7_d512"
+
+# ConvLSTM cells (drmvsnet.py:241-244): (input ch incl. hidden, 4*hid, resolution divisor)
+CELL_GEOM = {0: (48, 64, 1), 1: (32, 64, 2), 2: (32, 64, 4), 3: (48, 64, 2), 4: (40, 32, 1)}
+
+
+def algorithmic_work(name: str, B: int, N: int, H: int, W: int, launches_per_plane: int):
+    """(kind, amount per launch) of a sweep kernel; kind 'bytes' (HBM) or 'flops' (MFMA).
+
+    Per-unit figures:
+      cost_final   128*(N+1) B per hypothesis: ref + N-1 source features read once,
+                   the 32-ch cost slice written once (fp32);
+      cost_t1      same source/ref reads + the 16-B/px/view omega conv output;
+      lstm_cell k  2*9*Cin*Cout FLOP per cell pixel;
+      deconv       2*16*16*9 FLOP per output pixel / 4 (stride 2 -> 9 taps per 4 outputs... exact: 2*16*16*9 per input px);
+      head_wta     8*9*2 FLOP per pixel.
+    """
+    HW = H * W
+    nsrc = N - 1
+    if name == "cost_final":
+        return "bytes", 128.0 * (N + 1) * B * HW / launches_per_plane
+    if name == "cost_t1":
+        return "bytes", (128.0 * N + 16.0 * nsrc) * B * HW / launches_per_plane
+    if name in ("omega_stats1", "omega_stats2"):
+        return "bytes", 16.0 * nsrc * B * HW / launches_per_plane
+    if name.startswith("lstm_cell"):
+        k = int(name[-1])
+        cin, cout, sc = CELL_GEOM[k]
+        return "flops", 2.0 * 9 * cin * cout * B * HW / (sc * sc) / launches_per_plane
+    if name == "deconv0":
+        return "flops", 2.0 * 16 * 16 * 9 * B * HW / 16 / launches_per_plane
+    if name == "deconv1":
+        return "flops", 2.0 * 16 * 16 * 9 * B * HW / 4 / launches_per_plane
+    if name == "head_wta":
+        return "flops", 2.0 * 8 * 9 * B * HW / launches_per_plane
+    return "bytes", 0.0
+
+
+def kernel_table(prof: dict, planes: int, B: int, N: int, H: int, W: int):
+    rows = {}
+    total = sum(ms for _, ms in prof.values()) or 1.0
+    for name, (n, ms) in prof.items():
+        per_plane = max(1, round(n / planes))
+        kind, amount = algorithmic_work(name, B, N, H, W, per_plane)
+        avg_s = ms / n / 1e3
+        if kind == "bytes":
+            ach = amount / avg_s / 1e9 if amount else 0.0
+            rows[name] = dict(launches=n, avg_us=round(avg_s * 1e6, 2), share=round(ms / total, 4),
+                              bound="hbm", achieved=round(ach, 1), unit="GB/s",
+                              frac=round(ach / HBM_PEAK_GBS, 4), per_launch=amount)
+        else:
+            ach = amount / avg_s / 1e12
+            rows[name] = dict(launches=n, avg_us=round(avg_s * 1e6, 2), share=round(ms / total, 4),
+                              bound="mfma", achieved=round(ach, 2), unit="TFLOP/s",
+                              frac=round(ach / FP32_PEAK_TFLOPS, 4), per_launch=amount)
+    return rows
+
+
+def load_traffic(workload: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary, or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            tab = json.load(f)
+        return tab.get(workload, {}).get(kernel)
+    except (OSError, ValueError):
+        return None
+
+
+def make_inputs(cfg, B, seed, device):
+    N, H, W, D = cfg["N"], cfg["H"], cfg["W"], cfg["D"]
+    sc = syn.scene(B, N, H, W, D, seed=seed)
+    feats = torch.from_numpy(sc["features"])           # [N,B,32,H,W]
+    proj = torch.from_numpy(sc["proj_matrices"])       # [B,N,4,4]
+    dv = torch.from_numpy(sc["depth_values"])          # [B,D]
+    return feats, proj, dv, feats.to(device)
+
+
+def cpu_baseline(feats, proj, dv, P, planes: int):
+    """Time the CPU oracle on the first `planes` planes of the same inputs."""
+    from oracle import sweep_oracle as orc
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    N = feats.shape[0]
+    B, _, H, W = feats.shape[1:]
+    t0 = time.perf_counter()
+    ref = orc.sweep(feats[0], list(feats[1:]), proj[:, 0], list(proj[:, 1:].unbind(1)),
+                    dv[:, :planes], P, want_volume=True)
+    dt = time.perf_counter() - t0
+    hyp = B * H * W * planes
+    return ref, dict(value=hyp / dt, unit="depth-hypotheses/s", cores=torch.get_num_threads(),
+                     kind="port",
+                     sample=f"oracle/sweep_oracle.py, first {planes} of D planes, B={B}, N={N}, "
+                            f"{W}x{H}, {dt:.1f} s, torch CPU threads={torch.get_num_threads()}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default=DEFAULT_CONFIG, choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=1, help="reference views per GPU per step")
+    ap.add_argument("--cpu-planes", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = CONFIGS[args.config]
+    N, H, W, D, B = cfg["N"], cfg["H"], cfg["W"], cfg["D"], args.batch
+    P = {k: torch.from_numpy(v) for k, v in syn.sweep_weights(1).items()}
+    feats_h, proj, dv, feats = make_inputs(cfg, B, seed=rank, device=dev)
+    sweep = ops.DepthSweep({k: v.to(dev) for k, v in P.items()}, dev)
+    ref, srcs = feats[0], list(feats[1:])
+    src_proj = list(proj[:, 1:].unbind(1))
+
+    def step():
+        return sweep(ref, srcs, proj[:, 0], src_proj, dv, want_depth=True)
+
+    timing = not args.no_kernel_timing
+    ops.profile_enable(timing)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ops.profile_reset()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = ops.profile_read() if timing else {}
+    ops.profile_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    hyp = world * B * H * W * D * args.steps
+    value = hyp / elapsed
+    kernels = kernel_table(prof, D * args.steps, B, N, H, W) if prof else {}
+    roofline = None
+    if kernels:
+        dom = max(kernels, key=lambda k: kernels[k]["share"])
+        r = kernels[dom]
+        traffic = load_traffic(args.config, dom)
+        roofline = dict(kernel=dom, bound=r["bound"], achieved=r["achieved"],
+                        peak=HBM_PEAK_GBS if r["bound"] == "hbm" else FP32_PEAK_TFLOPS,
+                        unit=r["unit"], frac=r["frac"], traffic=traffic,
+                        per_launch=r["per_launch"], avg_us=r["avg_us"])
+        if "cost_final" in kernels:
+            c = kernels["cost_final"]
+            roofline["warp_aggregation"] = dict(kernel="cost_final", achieved=c["achieved"],
+                                                unit="GB/s", frac=c["frac"],
+                                                traffic=load_traffic(args.config, "cost_final"))
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        planes = max(1, min(args.cpu_planes, D))
+        orc_out, cpu = cpu_baseline(feats_h, proj, dv, P, planes)
+        g = sweep(ref, srcs, proj[:, 0], src_proj, dv[:, :planes].contiguous(), want_depth=True,
+                  want_cost=True)
+        torch.cuda.synchronize()
+        cost_err = float((g["cost"].cpu() - orc_out["cost"]).abs().max())
+        dref = orc_out["depth"]
+        rl1 = float((g["depth"].cpu() - dref).abs().sum() / dref.abs().sum())
+        parity = dict(sample_planes=planes, cost_max_abs_err=cost_err, depth_rel_l1=rl1)
+        cpu["value"] = round(cpu["value"], 1)
+
+    if rank == 0:
+        line = {
+            "metric": "depth-hypotheses/sec (ref-views x H x W x D / s)",
+            "value": round(value, 1),
+            "unit": "depth-hypotheses/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded numpy features ~N(0,1), SURVEY 8d cameras, random-init weights)",
+            "config": {"workload": args.config, "ref_views_per_gpu": B, "views": N, "H": H, "W": W,
+                       "D": D, "global_batch": B * world, "parallelism": f"ref-view shard x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "kernels": {k: {kk: vv for kk, vv in v.items() if kk != "per_launch"}
+                        for k, v in kernels.items()},
+        }
+        print(json.dumps(line), flush=True)
+    del out
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

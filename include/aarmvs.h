@@ -117,6 +117,18 @@ int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
 int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
                          hipStream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Opt-in per-kernel timing (a diagnostic, not part of the reference interface).
+ * When enabled, every launch made by the entry points above is bracketed by
+ * hipEvents on its stream; aarmvs_profile_read synchronises on the recorded
+ * events and returns the launch count and summed device time of one kernel.
+ * ------------------------------------------------------------------------- */
+void aarmvs_profile_enable(int on);
+void aarmvs_profile_reset(void);
+int aarmvs_profile_kernel_count(void);
+const char* aarmvs_profile_kernel_name(int id);
+int aarmvs_profile_read(int id, long long* launches, double* total_ms);
+
 #ifdef __cplusplus
 }
 #endif
