@@ -67,7 +67,8 @@ def test_cost_slice_and_omega_match_reference():
     sw = _sweep_obj(int(g["wseed"]))
     out = sw(feats[0], [feats[v] for v in range(1, N)], proj[:, 0], [proj[:, v] for v in range(1, N)],
              torch.from_numpy(sc["depth_values"][:, d:d + 1].copy()), want_depth=False, debug=True)
-    np.testing.assert_allclose(out["omega"].cpu().numpy(), g["omega"], atol=1e-5)
+    np.testing.assert_allclose(out["omega"].cpu().numpy(), g["omega"].reshape(N - 1, B, H, W),
+                               atol=1e-5)
     np.testing.assert_allclose(out["slice"].cpu().numpy(), g["slice"], atol=1e-4, rtol=1e-5)
 
 
