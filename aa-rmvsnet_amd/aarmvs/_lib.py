@@ -44,6 +44,8 @@ SIGNATURES = {
     "aarmvs_pack_params": (c_int, [c_void_p, c_void_p, c_void_p]),
     "aarmvs_homo_warp": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                  c_void_p, c_void_p]),
+    "aarmvs_homo_warp_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                          c_void_p, c_void_p]),
     "aarmvs_sweep_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "aarmvs_sweep": (c_int, [ctypes.POINTER(SweepArgs), c_void_p]),
     "aarmvs_state_ptr": (c_void_p, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),

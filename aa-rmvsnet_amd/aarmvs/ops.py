@@ -74,6 +74,20 @@ def homo_warp(src_fea: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor) -> 
     return out
 
 
+def homo_warp_backward(grad_out: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor,
+                       src_shape) -> torch.Tensor:
+    """d loss / d src_fea of homo_warp: bilinear scatter-add of grad_out (fp32 atomics)."""
+    _require_device(grad_out)
+    g = grad_out.contiguous()
+    B, C, H, W = src_shape
+    rel_d = rel.reshape(B, 12).to(g.device, torch.float32).contiguous()
+    dep = depth.reshape(B).to(g.device, torch.float32).contiguous()
+    grad_src = torch.zeros(B, C, H, W, device=g.device)
+    check(lib().aarmvs_homo_warp_backward(g.data_ptr(), rel_d.data_ptr(), dep.data_ptr(), B, C, H,
+                                          W, grad_src.data_ptr(), _stream()), "homo_warp_backward")
+    return grad_src
+
+
 def softmax_depth(cost: torch.Tensor) -> torch.Tensor:
     _require_device(cost)
     c = cost.contiguous()
@@ -109,8 +123,13 @@ class DepthSweep:
         return ws
 
     def __call__(self, ref_fea, src_feas, ref_proj, src_projs, depth_values, *,
-                 want_depth=True, want_cost=False, d_range=None, debug=False):
-        """Returns dict(depth, conf, cost, slice, omega) (entries None when not requested)."""
+                 want_depth=True, want_cost=False, d_range=None, debug=False, cost_out=None):
+        """Returns dict(depth, conf, cost, slice, omega) (entries None when not requested).
+
+        ``d_range=(d0, d1)`` runs planes d0..d1-1 only (d0 == 0 resets the hidden state;
+        later ranges continue from the state the previous call left in the workspace).
+        ``cost_out`` is an optional caller-owned [B,D,H,W] buffer for the regulariser output.
+        """
         ref = ref_fea.contiguous()
         srcs = [s.contiguous() for s in src_feas]
         _require_device(ref, *srcs)
@@ -130,7 +149,12 @@ class DepthSweep:
         if want_depth:
             out["depth"] = torch.empty(B, H, W, device=ref.device)
             out["conf"] = torch.empty(B, H, W, device=ref.device)
-        if want_cost:
+        if cost_out is not None:
+            if tuple(cost_out.shape) != (B, D, H, W) or not cost_out.is_contiguous():
+                raise AarmvsError("aarmvs: cost_out must be a contiguous [B,D,H,W] tensor")
+            _require_device(cost_out)
+            out["cost"] = cost_out
+        elif want_cost:
             out["cost"] = torch.empty(B, D, H, W, device=ref.device)
         if debug:
             out["slice"] = torch.empty(B, C, H, W, device=ref.device)
@@ -166,6 +190,11 @@ class DepthSweep:
         off = ptr - ws.data_ptr()
         return ws[off: off + B * hid * (H // sc) * (W // sc) * 4].view(torch.float32).view(
             B, hid, H // sc, W // sc)
+
+    def snapshot_state(self, B, H, W, nsrc, parity):
+        """Copies of the regulariser's (h, c) per cell as left for the plane of `parity`."""
+        return [[self.state(B, H, W, nsrc, parity, k, 0).clone(),
+                 self.state(B, H, W, nsrc, parity, k, 1).clone()] for k in range(5)]
 
     def unet_step(self, x: torch.Tensor, step: int, nsrc: int = 1) -> torch.Tensor:
         _require_device(x)

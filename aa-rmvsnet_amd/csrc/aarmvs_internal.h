@@ -82,6 +82,8 @@ struct SweepGeom {
 hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s);
 hipError_t launch_homo_warp(const float* src, const float* rel, const float* depth, int B, int C,
                             int H, int W, float* out, hipStream_t s);
+hipError_t launch_homo_warp_bwd(const float* gout, const float* rel, const float* depth, int B,
+                                int C, int H, int W, float* gsrc, hipStream_t s);
 
 struct CostArgs {
   const float* ref;

@@ -239,6 +239,16 @@ int aarmvs_homo_warp(const float* src_fea, const float* rel_proj, const float* d
   return e == hipSuccess ? AARMVS_OK : hip_fail(e, "homo_warp");
 }
 
+int aarmvs_homo_warp_backward(const float* grad_out, const float* rel_proj, const float* depth,
+                              int B, int C, int H, int W, float* grad_src, hipStream_t stream) {
+  if (!grad_out || !rel_proj || !depth || !grad_src)
+    return fail(AARMVS_ERR_INVALID, "homo_warp_backward: null pointer");
+  if (B < 1 || C < 1 || H < 2 || W < 2)
+    return fail(AARMVS_ERR_INVALID, "homo_warp_backward: need B>=1, C>=1, H>=2, W>=2");
+  hipError_t e = launch_homo_warp_bwd(grad_out, rel_proj, depth, B, C, H, W, grad_src, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "homo_warp_backward");
+}
+
 static int check_geom(int B, int H, int W, int nsrc) {
   if (B < 1) return fail(AARMVS_ERR_INVALID, "B must be >= 1");
   if (H < 4 || W < 4 || H % 4 || W % 4)

@@ -114,6 +114,44 @@ hipError_t launch_homo_warp(const float* src, const float* rel, const float* dep
 }
 
 // ---------------------------------------------------------------------------
+// Backward of the warp w.r.t. the source features (aarmvs_homo_warp_backward):
+// grid_sample's bilinear backward as a scatter-add of the output gradient into the
+// four taps (no-return fp32 atomics; out-of-range taps receive nothing).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) homo_warp_bwd_kernel(const float* __restrict__ gout,
+                                                            const float* __restrict__ rel,
+                                                            const float* __restrict__ depth,
+                                                            int C, int H, int W,
+                                                            float* __restrict__ gsrc) {
+  const int b = blockIdx.y;
+  const int HW = H * W;
+  const float* m = rel + 12 * b;
+  const float dep = depth[b];
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
+    float ix, iy;
+    sample_pos(m, dep, (float)(p % W), (float)(p / W), H, W, ix, iy);
+    const Taps t = make_taps(ix, iy, H, W);
+    const float* g = gout + (size_t)b * C * HW + p;
+    float* s = gsrc + (size_t)b * C * HW;
+    for (int c = 0; c < C; ++c) {
+      const float gv = g[(size_t)c * HW];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (t.ok[k]) atomicAdd(s + (size_t)c * HW + t.idx[k], t.wt[k] * gv);
+    }
+  }
+}
+
+hipError_t launch_homo_warp_bwd(const float* gout, const float* rel, const float* depth, int B,
+                                int C, int H, int W, float* gsrc, hipStream_t s) {
+  const int HW = H * W;
+  dim3 grid((unsigned)std::min((HW + 255) / 256, 4096), (unsigned)B);
+  ProfScope ps(s, K_WARP);
+  hipLaunchKernelGGL(homo_warp_bwd_kernel, grid, dim3(256), 0, s, gout, rel, depth, C, H, W, gsrc);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // K1: warp + sqdiff on a haloed tile, omega conv3x3 32->4, GN#0 partial sums.
 // Tile = 8 rows x 32 cols of output pixels; LDS holds sq for the 10x34 halo tile.
 // ---------------------------------------------------------------------------

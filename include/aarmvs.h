@@ -72,6 +72,13 @@ int aarmvs_pack_params(const float* raw_params, void* packed, hipStream_t stream
 int aarmvs_homo_warp(const float* src_fea, const float* rel_proj, const float* depth,
                      int B, int C, int H, int W, float* out, hipStream_t stream);
 
+/* Backward of aarmvs_homo_warp w.r.t. src_fea (the grid carries no gradient,
+ * module.py:15): grad_src += bilinear scatter of grad_out.  grad_src must be
+ * zero-initialised by the caller; accumulation uses fp32 atomics (order-dependent
+ * rounding). */
+int aarmvs_homo_warp_backward(const float* grad_out, const float* rel_proj, const float* depth,
+                              int B, int C, int H, int W, float* grad_src, hipStream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Whole depth sweep (drmvsnet.py:273-291 train / :306-342 eval).
  * Replaces, per plane d: homo_warping_depthwise x nsrc, (warp-ref)^2, omega

@@ -36,6 +36,10 @@ REF = "/root/reference"
 def import_reference():
     os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
     sys.dont_write_bytecode = True
+    # our drop-in package is also called ``models``: keep it off the path here
+    sys.path[:] = [p for p in sys.path if os.path.abspath(p) != os.path.join(REPO, "aa-rmvsnet_amd")]
+    for name in [m for m in sys.modules if m == "models" or m.startswith("models.")]:
+        del sys.modules[name]
     if REF not in sys.path:
         sys.path.append(REF)
     torch.Tensor.cuda = lambda self, *a, **k: self
@@ -211,12 +215,46 @@ def gen_e2e(drm, mod, out):
     out.append("e2e.npz")
 
 
+def gen_ckpt(drm, mod, out):
+    """Checkpoint contract: the shipped core checkpoint's key layout, and an
+    eval sweep run by the reference with its real (model_dtu_v2) omega/regulariser weights.
+    The checkpoint is read with torch.load(weights_only=True)."""
+    import json
+    ck = torch.load(os.path.join(REF, "checkpoints", "model_dtu_v2.ckpt"), map_location="cpu",
+                    weights_only=True)
+    sd = ck["model"]
+    layout = {k: list(v.shape) for k, v in sd.items()}
+    with open(os.path.join(HERE, "ckpt_layout.json"), "w") as f:
+        json.dump({"source": "checkpoints/model_dtu_v2.ckpt", "epoch": int(ck["epoch"]),
+                   "keys": layout}, f, indent=0, sort_keys=True)
+    out.append("ckpt_layout.json")
+    B, N, H, W, D = 1, 4, 64, 80, 24
+    sc = syn.scene(B, N, H, W, D, seed=41)
+    model = drm.EMVSNet(disparity_level=D, image_scale=1.0, max_h=H, max_w=W, return_depth=True)
+    model.load_state_dict(sd, strict=False)
+    model.feature = nn.Identity()
+    model.evidential = _NoEvidential()
+    model.eval()
+    imgs = t(np.moveaxis(sc["features"], 0, 1))
+    with torch.no_grad():
+        res = model(imgs, t(sc["proj_matrices"]), t(sc["depth_values"]))
+        model.return_depth = False
+        prob, _, _ = model(imgs, t(sc["proj_matrices"]), t(sc["depth_values"]))
+    sweep_w = {k: sd[k].numpy() for k in syn.SWEEP_SHAPES}
+    np.savez_compressed(os.path.join(HERE, "real_weights_sweep.npz"), depth=res["depth"].numpy(),
+                        conf=res["photometric_confidence"].numpy(), prob_sub=prob.numpy()[:, :, ::4, ::4],
+                        seed=41, shape=np.array([B, N, H, W, D]),
+                        digest=syn.array_digest(sc["features"], sc["proj_matrices"], sc["depth_values"]),
+                        **{"w:" + k: v for k, v in sweep_w.items()})
+    out.append("real_weights_sweep.npz")
+
+
 def main():
     torch.manual_seed(0)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     drm, mod = import_reference()
     out = []
-    for fn in (gen_warp, gen_slice_omega, gen_unet, gen_sweeps, gen_config1, gen_e2e):
+    for fn in (gen_warp, gen_slice_omega, gen_unet, gen_sweeps, gen_config1, gen_e2e, gen_ckpt):
         fn(drm, mod, out)
         print("wrote", out[-1], flush=True)
     with open(os.path.join(HERE, "MANIFEST.txt"), "w") as f:

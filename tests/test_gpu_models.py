@@ -1,0 +1,149 @@
+"""GPU tests of the drop-in ``models`` API (EMVSNet / homo_warping_depthwise) on libaarmvs:
+end-to-end against fixtures made by running the reference, the reference's real
+checkpoint weights, and the training backward against CPU autograd of the oracle.
+
+Tolerances: depth <= 1e-3 relative L1 (north_star), confidences/probabilities 1e-4/1e-5
+abs, gradients 1e-4 relative to the gradient's max magnitude (fp32 atomics and
+reassociation in the backward).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from conftest import GOLDEN
+from aarmvs import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def rel_l1(a, b):
+    return float(np.abs(a - b).sum() / max(np.abs(b).sum(), 1e-30))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+
+
+def _model(D, H, W, wseed, return_depth, identity_feature=True):
+    from models import EMVSNet
+    m = EMVSNet(disparity_level=D, image_scale=1.0, max_h=H, max_w=W, return_depth=return_depth)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    wts = syn.init_weights(shapes, seed=wseed)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in wts.items()}, strict=True)
+    if identity_feature:
+        m.feature = nn.Identity()
+    return m.to(DEV)
+
+
+def test_emvsnet_end_to_end_with_featnet():
+    """Full EMVSNet.forward (FeatNet in PyTorch + HIP sweep) vs the reference (e2e.npz)."""
+    g = load("e2e.npz")
+    B, N, H, W, D = (int(x) for x in g["shape"])
+    sc = syn.scene(B, N, H, W, D, seed=int(g["seed"]), images=True)
+    m = _model(D, H, W, int(g["wseed"]), True, identity_feature=False).eval()
+    imgs = torch.from_numpy(sc["imgs"]).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"]).to(DEV)
+    dv = torch.from_numpy(sc["depth_values"]).to(DEV)
+    with torch.no_grad():
+        out = m(imgs, proj, dv)
+        assert rel_l1(out["depth"].cpu().numpy(), g["depth"]) <= 1e-3
+        np.testing.assert_allclose(out["photometric_confidence"].cpu().numpy(), g["conf"], atol=1e-4)
+        assert out["evidential_prediction"] is None   # head out of scope
+        m.return_depth = False
+        prob, ev, comb = m(imgs, proj, dv)
+    np.testing.assert_allclose(prob.cpu().numpy(), g["prob"], atol=1e-4)
+
+
+def test_emvsnet_real_checkpoint_weights():
+    """Eval + train-mode sweep with the reference's model_dtu_v2 weights (real_weights_sweep.npz)."""
+    g = load("real_weights_sweep.npz")
+    B, N, H, W, D = (int(x) for x in g["shape"])
+    from models import EMVSNet
+    m = EMVSNet(disparity_level=D, image_scale=1.0, max_h=H, max_w=W, return_depth=True)
+    sd = {k[2:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("w:")}
+    missing = m.load_state_dict(sd, strict=False).missing_keys
+    assert all(k.startswith("feature.") for k in missing)
+    m.feature = nn.Identity()
+    m = m.to(DEV).eval()
+    sc = syn.scene(B, N, H, W, D, seed=int(g["seed"]))
+    assert syn.array_digest(sc["features"], sc["proj_matrices"], sc["depth_values"]) == str(g["digest"])
+    imgs = torch.from_numpy(np.moveaxis(sc["features"], 0, 1).copy()).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"]).to(DEV)
+    dv = torch.from_numpy(sc["depth_values"]).to(DEV)
+    with torch.no_grad():
+        out = m(imgs, proj, dv)
+        m.return_depth = False
+        prob, _, _ = m(imgs, proj, dv)
+    assert rel_l1(out["depth"].cpu().numpy(), g["depth"]) <= 1e-3
+    np.testing.assert_allclose(out["photometric_confidence"].cpu().numpy(), g["conf"], atol=1e-4)
+    np.testing.assert_allclose(prob.cpu().numpy()[:, :, ::4, ::4], g["prob_sub"], atol=1e-5)
+
+
+def test_homo_warping_depthwise_forward_backward():
+    """models.homo_warping_depthwise (HIP) vs the warp fixture and CPU autograd of the oracle."""
+    from models import homo_warping_depthwise
+    from oracle import sweep_oracle as orc
+    g = load("warp.npz")
+    B, N, H, W, C = (int(x) for x in g["shape"])
+    sc = syn.scene(B, N, H, W, D=4, seed=int(g["seed"]), C=C)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    src = torch.from_numpy(sc["features"][1]).to(DEV).requires_grad_(True)
+    dep = torch.from_numpy(g["depths"][:, 1])
+    out = homo_warping_depthwise(src, proj[:, 1].to(DEV), proj[:, 0].to(DEV), dep.to(DEV))
+    np.testing.assert_allclose(out.detach().cpu().numpy(), g["out"][0, 1], atol=1e-4)
+    gout = torch.randn(out.shape, generator=torch.Generator().manual_seed(0))
+    out.backward(gout.to(DEV))
+    src_c = torch.from_numpy(sc["features"][1]).requires_grad_(True)
+    rel = orc.relative_projection(proj[:, 1], proj[:, 0])
+    orc.homo_warp(src_c, rel, dep).backward(gout)
+    ref_g = src_c.grad.numpy()
+    np.testing.assert_allclose(src.grad.cpu().numpy(), ref_g, atol=1e-4 * np.abs(ref_g).max())
+
+
+def test_training_backward_matches_cpu_autograd():
+    """BPTT through the sweep (HIP forward + per-plane recompute) vs CPU autograd."""
+    from oracle import sweep_oracle as orc
+    B, N, H, W, D = 1, 3, 16, 24, 4
+    sc = syn.scene(B, N, H, W, D, seed=51)
+    m = _model(D, H, W, 4, False)
+    P_cpu = {k: v.detach().cpu().clone().requires_grad_(True)
+             for k, v in m.named_parameters() if k in syn.SWEEP_SHAPES}
+    feats = torch.from_numpy(sc["features"])                       # [N,B,C,H,W]
+    proj = torch.from_numpy(sc["proj_matrices"])
+    dv = torch.from_numpy(sc["depth_values"])
+    R = torch.randn(B, D, H, W, generator=torch.Generator().manual_seed(1))
+
+    # CPU reference: autograd through the oracle's fp32 restatement
+    fc = feats.clone().requires_grad_(True)
+    rels = [orc.relative_projection(proj[:, v], proj[:, 0]) for v in range(1, N)]
+    state = orc.init_state(B, H, W)
+    costs = []
+    for d in range(D):
+        x = orc.cost_slice(fc[0], [fc[v] for v in range(1, N)], rels, dv[:, d], P_cpu)
+        cost, state = orc.unet_step(x, state, P_cpu)
+        costs.append(cost)
+    prob_c = torch.softmax(torch.stack(costs, 1).squeeze(2), dim=1)
+    (prob_c * R).sum().backward()
+
+    imgs = torch.from_numpy(np.moveaxis(sc["features"], 0, 1).copy()).to(DEV).requires_grad_(True)
+    prob, _, _ = m(imgs, proj.to(DEV), dv.to(DEV))
+    np.testing.assert_allclose(prob.detach().cpu().numpy(), prob_c.detach().numpy(), atol=1e-5)
+    (prob * R.to(DEV)).sum().backward()
+    gi = imgs.grad.cpu().numpy()
+    gref = np.moveaxis(fc.grad.numpy(), 0, 1)
+    np.testing.assert_allclose(gi, gref, atol=1e-4 * np.abs(gref).max())
+    for k, p in m.named_parameters():
+        if k in P_cpu:
+            gr = P_cpu[k].grad.numpy()
+            np.testing.assert_allclose(p.grad.cpu().numpy(), gr, atol=1e-4 * max(np.abs(gr).max(), 1e-12),
+                                       err_msg=k)
