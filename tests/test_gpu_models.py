@@ -142,8 +142,11 @@ def test_training_backward_matches_cpu_autograd():
     gi = imgs.grad.cpu().numpy()
     gref = np.moveaxis(fc.grad.numpy(), 0, 1)
     np.testing.assert_allclose(gi, gref, atol=1e-4 * np.abs(gref).max())
+    # conv_0.bias's true gradient is 0 (softmax over D sums the cost gradients to zero),
+    # so each parameter is compared at 1e-4 of max(its own scale, 1e-3 x the largest)
+    gmax = max(float(p.grad.abs().max()) for p in P_cpu.values())
     for k, p in m.named_parameters():
         if k in P_cpu:
             gr = P_cpu[k].grad.numpy()
-            np.testing.assert_allclose(p.grad.cpu().numpy(), gr, atol=1e-4 * max(np.abs(gr).max(), 1e-12),
-                                       err_msg=k)
+            tol = 1e-4 * max(np.abs(gr).max(), 1e-3 * gmax)
+            np.testing.assert_allclose(p.grad.cpu().numpy(), gr, atol=tol, err_msg=k)
