@@ -38,6 +38,7 @@ for _p in (ROOT, os.path.join(ROOT, "aa-rmvsnet_amd")):
         sys.path.insert(0, _p)
 
 from aarmvs import ops, synthetic as syn  # noqa: E402
+from aarmvs.dist import env, init_process_group, max_over_ranks  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= vector) dense peak
@@ -64,7 +65,7 @@ def algorithmic_work(name: str, B: int, N: int, H: int, W: int, launches_per_pla
                    the 32-ch cost slice written once (fp32);
       cost_t1      same source/ref reads + the 16-B/px/view omega conv output;
       lstm_cell k  2*9*Cin*Cout FLOP per cell pixel;
-      deconv       2*16*16*9 FLOP per output pixel / 4 (stride 2 -> 9 taps per 4 outputs... exact: 2*16*16*9 per input px);
+      deconv       2*16*16*9 FLOP per deconv input pixel (each input pixel meets the 3x3 kernel once);
       head_wta     8*9*2 FLOP per pixel.
     """
     HW = H * W
@@ -159,14 +160,10 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, local, world = env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+    init_process_group(dev)
 
     cfg = CONFIGS[args.config]
     N, H, W, D, B = cfg["N"], cfg["H"], cfg["W"], cfg["D"], args.batch
@@ -199,10 +196,7 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = ops.profile_read() if timing else {}
     ops.profile_enable(False)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dev)
 
     hyp = world * B * H * W * D * args.steps
     value = hyp / elapsed
@@ -216,11 +210,16 @@ def main():
                         peak=HBM_PEAK_GBS if r["bound"] == "hbm" else FP32_PEAK_TFLOPS,
                         unit=r["unit"], frac=r["frac"], traffic=traffic,
                         per_launch=r["per_launch"], avg_us=r["avg_us"])
-        if "cost_final" in kernels:
-            c = kernels["cost_final"]
-            roofline["warp_aggregation"] = dict(kernel="cost_final", achieved=c["achieved"],
-                                                unit="GB/s", frac=c["frac"],
-                                                traffic=load_traffic(args.config, "cost_final"))
+        # the warp + aggregation path as a whole (every launch that produces the cost
+        # slice): 128*(N+1) algorithmic B/hyp over the summed device time of its kernels
+        group = [k for k in ("cost_t1", "omega_stats1", "omega_stats2", "cost_final") if k in prof]
+        if group:
+            ms = sum(prof[k][1] for k in group)
+            planes = D * args.steps
+            ach = 128.0 * (N + 1) * B * H * W * planes / (ms / 1e3) / 1e9
+            roofline["warp_aggregation"] = dict(kernels=group, achieved=round(ach, 1), unit="GB/s",
+                                                peak=HBM_PEAK_GBS, frac=round(ach / HBM_PEAK_GBS, 4),
+                                                us_per_plane=round(ms / planes * 1e3, 2))
 
     cpu = None
     parity = None

@@ -1,0 +1,3 @@
+#!/bin/bash
+source tools/gpu_round.sh
+run pytest_gpu 900 python -m pytest tests -m gpu -q -x
