@@ -49,27 +49,30 @@ constexpr int kCellScale[5] = {1, 2, 4, 2, 1};
 // Workspace layout.
 // ---------------------------------------------------------------------------
 struct Workspace {
-  double* stats;        // [B][nstat][kSlots][2]
-  float* max_prob;      // [B,HW]
-  float* exp_sum;       // [B,HW]
-  float* depth;         // [B,HW]
-  float* x;             // [B,32,H,W] cost slice
-  float* t1;            // [B][nsrc][HW][4] omega conv3x3 output
-  float* u0;            // [B,16,H/2,W/2] deconv_0 output (pre-GN)
-  float* u1;            // [B,16,H,W]     deconv_1 output (pre-GN)
-  float* h[5][2];       // ping-pong hidden states
-  float* c[5];          // cell states (updated in place)
+  double* omega_stats[2]; // per plane parity: [B][nsrc][3][kSlots][2] omega GN statistics
+  double* reg_stats;      // [B][2 deconvs][2 groups][kSlots][2] U-Net GN statistics
+  float* max_prob;        // [B,HW]
+  float* exp_sum;         // [B,HW]
+  float* depth;           // [B,HW]
+  float* x;               // [B,32,H,W] cost slice
+  float* t1[2];           // per plane parity: [B][nsrc][HW][4] omega conv3x3 output
+  float* u0;              // [B,16,H/2,W/2] deconv_0 output (pre-GN)
+  float* u1;              // [B,16,H,W]     deconv_1 output (pre-GN)
+  float* h[5][2];         // ping-pong hidden states
+  float* c[5];            // cell states (updated in place)
   size_t bytes;
-  size_t stats_bytes;
-  size_t state_bytes;   // h[*][*], c[*] region (contiguous) for zero-init
+  size_t omega_stats_bytes;  // one parity
+  size_t reg_stats_bytes;
+  size_t stats_bytes;        // both omega parities + reg (contiguous, for the initial clear)
+  size_t state_bytes;        // h[*][*], c[*] region (contiguous) for zero-init
   void* state_begin;
-  size_t wta_bytes;     // max_prob/exp_sum/depth region
+  size_t wta_bytes;          // max_prob/exp_sum/depth region
 };
 Workspace carve_workspace(void* base, int B, int H, int W, int nsrc);
-__host__ __device__ inline int nstat(int nsrc) { return 3 * nsrc + 4; }
-// statistic ids within a batch element
-__host__ __device__ inline int stat_omega(int v, int k) { return 3 * v + k; }
-__host__ __device__ inline int stat_deconv(int nsrc, int j, int g) { return 3 * nsrc + 2 * j + g; }
+// U-Net statistic (deconv j, group g) of batch element b within reg_stats
+__host__ __device__ inline size_t reg_stat_index(int b, int j, int g) {
+  return ((size_t)(b * 2 + j) * 2 + g) * kSlots * 2;
+}
 
 // ---------------------------------------------------------------------------
 // Kernel launchers (defined in the .hip units).
@@ -90,11 +93,12 @@ struct CostArgs {
   const float* src[AARMVS_MAX_SRC];
   const float* rel;       // [nsrc][B][12]
   const float* depth_values;  // [B,D]
-  int d;
   const float* params;    // packed
 };
-hipError_t launch_cost_slice(const CostArgs& a, const SweepGeom& g, const Workspace& ws,
-                             float* omega_out, hipStream_t s);
+// One step of the cost-slice pipeline: cost slice x of plane d_prev (if >= 0) and the
+// omega conv output + GroupNorm statistics of plane d_next (if >= 0).
+hipError_t launch_cost_pipe(const CostArgs& a, const SweepGeom& g, const Workspace& ws,
+                            int d_prev, int d_next, float* omega_out, hipStream_t s);
 
 hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
                             const Workspace& ws, int parity, hipStream_t s);
@@ -113,7 +117,7 @@ int cu_count();
 // stream around each kernel.  Off by default; costs nothing when off.
 // ---------------------------------------------------------------------------
 enum KernelId : int {
-  K_COST_T1, K_OMEGA1, K_OMEGA2, K_COST_FINAL,
+  K_COST_PIPE, K_OMEGA1, K_OMEGA2,
   K_CELL0, K_CELL1, K_CELL2, K_CELL3, K_CELL4,
   K_DECONV0, K_DECONV1, K_HEAD_WTA, K_FINALIZE, K_SOFTMAX, K_WARP,
   K_COUNT

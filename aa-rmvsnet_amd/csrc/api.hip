@@ -59,7 +59,7 @@ static double g_prof_ms[K_COUNT];
 static long long g_prof_n[K_COUNT];
 
 static const char* kKernelNames[K_COUNT] = {
-    "cost_t1", "omega_stats1", "omega_stats2", "cost_final",
+    "cost_pipe", "omega_stats1", "omega_stats2",
     "lstm_cell0", "lstm_cell1", "lstm_cell2", "lstm_cell3", "lstm_cell4",
     "deconv0", "deconv1", "head_wta", "finalize", "softmax_depth", "homo_warp"};
 
@@ -120,15 +120,21 @@ Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
     return r;
   };
   const size_t HW = (size_t)H * W, HW2 = HW / 4, HW4 = HW / 16;
-  ws.stats_bytes = (size_t)B * nstat(nsrc) * kSlots * 2 * sizeof(double);
-  ws.stats = reinterpret_cast<double*>(take(ws.stats_bytes));
+  ws.omega_stats_bytes = (size_t)B * nsrc * 3 * kSlots * 2 * sizeof(double);
+  ws.reg_stats_bytes = (size_t)B * 4 * kSlots * 2 * sizeof(double);
+  const size_t stats_begin = off;
+  ws.omega_stats[0] = reinterpret_cast<double*>(take(ws.omega_stats_bytes));
+  ws.omega_stats[1] = reinterpret_cast<double*>(take(ws.omega_stats_bytes));
+  ws.reg_stats = reinterpret_cast<double*>(take(ws.reg_stats_bytes));
+  ws.stats_bytes = off - stats_begin;
   const size_t wta_begin = off;
   ws.max_prob = reinterpret_cast<float*>(take(B * HW * 4));
   ws.exp_sum = reinterpret_cast<float*>(take(B * HW * 4));
   ws.depth = reinterpret_cast<float*>(take(B * HW * 4));
   ws.wta_bytes = off - wta_begin;
   ws.x = reinterpret_cast<float*>(take(B * kC * HW * 4));
-  ws.t1 = reinterpret_cast<float*>(take((size_t)B * nsrc * HW * 16));
+  ws.t1[0] = reinterpret_cast<float*>(take((size_t)B * nsrc * HW * 16));
+  ws.t1[1] = reinterpret_cast<float*>(take((size_t)B * nsrc * HW * 16));
   ws.u0 = reinterpret_cast<float*>(take(B * 16 * HW2 * 4));
   ws.u1 = reinterpret_cast<float*>(take(B * 16 * HW * 4));
   const size_t state_begin = off;
@@ -287,28 +293,32 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   Workspace ws = carve_workspace(a->workspace, a->B, a->H, a->W, a->nsrc);
   const float* params = static_cast<const float*>(a->packed_params);
   hipError_t e;
-  if (a->d_begin == 0) {
-    // UNetConvLSTM._init_hidden (drmvsnet.py:133-134, 202-206) and the WTA images
-    // (drmvsnet.py:302-304)
-    if ((e = hipMemsetAsync(ws.state_begin, 0, ws.state_bytes, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: state init");
-    if ((e = hipMemsetAsync(ws.max_prob, 0, ws.wta_bytes, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: wta init");
-  }
   CostArgs ca{};
   ca.ref = a->ref_fea;
   for (int v = 0; v < a->nsrc; ++v) ca.src[v] = a->src_fea[v];
   ca.rel = a->rel_proj;
   ca.depth_values = a->depth_values;
   ca.params = params;
+  if (a->d_begin == 0) {
+    // UNetConvLSTM._init_hidden (drmvsnet.py:133-134, 202-206) and the WTA images
+    // (drmvsnet.py:302-304); then prime the cost-slice pipeline with plane 0's omega
+    // conv output and statistics
+    if ((e = hipMemsetAsync(ws.state_begin, 0, ws.state_bytes, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: state init");
+    if ((e = hipMemsetAsync(ws.max_prob, 0, ws.wta_bytes, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: wta init");
+    if ((e = hipMemsetAsync(ws.omega_stats[0], 0, ws.stats_bytes, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: stats init");
+    if ((e = launch_cost_pipe(ca, g, ws, -1, 0, nullptr, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: cost pipeline prologue");
+  }
   const bool wta = a->depth_out || a->conf_out;
   for (int d = a->d_begin; d < a->d_end; ++d) {
-    ca.d = d;
     const bool last = d == a->d_end - 1;
-    if ((e = hipMemsetAsync(ws.stats, 0, ws.stats_bytes, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: stats reset");
-    if ((e = launch_cost_slice(ca, g, ws, last ? a->omega_out : nullptr, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: cost slice");
+    const int d_next = d + 1 < a->D ? d + 1 : -1;
+    if ((e = launch_cost_pipe(ca, g, ws, d, d_next, last ? a->omega_out : nullptr, stream)) !=
+        hipSuccess)
+      return hip_fail(e, "sweep: cost pipeline");
     if (last && a->slice_out) {
       e = hipMemcpyAsync(a->slice_out, ws.x, (size_t)a->B * kC * a->H * a->W * 4,
                          hipMemcpyDeviceToDevice, stream);
@@ -340,7 +350,7 @@ int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
   hipError_t e;
   if (step == 0 && (e = hipMemsetAsync(ws.state_begin, 0, ws.state_bytes, stream)) != hipSuccess)
     return hip_fail(e, "unet_step: state init");
-  if ((e = hipMemsetAsync(ws.stats, 0, ws.stats_bytes, stream)) != hipSuccess)
+  if ((e = hipMemsetAsync(ws.reg_stats, 0, ws.reg_stats_bytes, stream)) != hipSuccess)
     return hip_fail(e, "unet_step: stats reset");
   if ((e = launch_unet_step(x, params, g, ws, step & 1, stream)) != hipSuccess)
     return hip_fail(e, "unet_step");

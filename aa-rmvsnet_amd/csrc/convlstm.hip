@@ -258,8 +258,13 @@ __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__
                                                        int d, int D, float* __restrict__ cost_out,
                                                        int wta, float* __restrict__ max_prob,
                                                        float* __restrict__ exp_sum,
-                                                       float* __restrict__ depth) {
+                                                       float* __restrict__ depth,
+                                                       double* __restrict__ zero_stats,
+                                                       int zero_n) {
 #pragma clang fp contract(off)
+  // the plane's U-Net GroupNorm statistics are consumed: clear them for the next plane
+  if (zero_stats && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = threadIdx.x; i < zero_n; i += blockDim.x) zero_stats[i] = 0.0;
   // the select arithmetic of drmvsnet.py:328-333 is reproduced op for op
   const int b = blockIdx.y, HW = H * W;
   const float* hb = h4 + (size_t)b * 8 * HW;
@@ -353,13 +358,12 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   if ((e = run_cell<32, 16, 8>(a2, cu, K_CELL2, s)) != hipSuccess) return e;
   // GroupNorm statistics are per batch element, so the deconvs and the two cells that
   // consume their normalised output are launched per batch element.
-  const size_t sstride = (size_t)nstat(g.nsrc) * kSlots * 2;
   // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
   {
     const int Hi = H / 4, Wi = W / 4;
     const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 2 * cu / std::max(1, B)));
     for (int b = 0; b < B; ++b) {
-      double* st = ws.stats + b * sstride + (size_t)stat_deconv(g.nsrc, 0, 0) * kSlots * 2;
+      double* st = ws.reg_stats + reg_stat_index(b, 0, 0);
       ProfScope ps(s, K_DECONV0);
       hipLaunchKernelGGL(deconv_kernel, dim3(blocks, 1), dim3(256), 0, s,
                          ws.h[2][nxt] + (size_t)b * 16 * Hi * Wi, params + L.pk_off[P_D0W],
@@ -370,7 +374,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   }
   // cell 3: [gnrelu(u0), h1', h3] @ H/2
   for (int b = 0; b < B; ++b) {
-    const double* st = ws.stats + b * sstride + (size_t)stat_deconv(g.nsrc, 0, 0) * kSlots * 2;
+    const double* st = ws.reg_stats + reg_stat_index(b, 0, 0);
     const size_t hq = (size_t)(H / 2) * (W / 2);
     CellArgs a3 = cell(3, {{ws.u0 + b * 16 * hq, 16, SRC_GNRELU, st, params + L.pk_off[P_D0GW],
                             params + L.pk_off[P_D0GB]},
@@ -387,7 +391,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     const int Hi = H / 2, Wi = W / 2;
     const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 2 * cu / std::max(1, B)));
     for (int b = 0; b < B; ++b) {
-      double* st = ws.stats + b * sstride + (size_t)stat_deconv(g.nsrc, 1, 0) * kSlots * 2;
+      double* st = ws.reg_stats + reg_stat_index(b, 1, 0);
       ProfScope ps(s, K_DECONV1);
       hipLaunchKernelGGL(deconv_kernel, dim3(blocks, 1), dim3(256), 0, s,
                          ws.h[3][nxt] + (size_t)b * 16 * Hi * Wi, params + L.pk_off[P_D1W],
@@ -398,7 +402,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   }
   // cell 4: [gnrelu(u1), h0', h4] @ H
   for (int b = 0; b < B; ++b) {
-    const double* st = ws.stats + b * sstride + (size_t)stat_deconv(g.nsrc, 1, 0) * kSlots * 2;
+    const double* st = ws.reg_stats + reg_stat_index(b, 1, 0);
     const size_t hw = (size_t)H * W;
     CellArgs a4 = cell(4, {{ws.u1 + b * 16 * hw, 16, SRC_GNRELU, st, params + L.pk_off[P_D1GW],
                             params + L.pk_off[P_D1GB]},
@@ -423,7 +427,8 @@ hipError_t launch_head_wta(const float* params, const SweepGeom& g, const Worksp
   ProfScope ps(s, K_HEAD_WTA);
   hipLaunchKernelGGL(head_wta_kernel, dim3(blocks, g.B), dim3(256), 0, s, ws.h[4][nxt],
                      params + L.pk_off[P_HW], params + L.pk_off[P_HB], g.H, g.W, depth_values, d,
-                     g.D, cost_out, wta ? 1 : 0, ws.max_prob, ws.exp_sum, ws.depth);
+                     g.D, cost_out, wta ? 1 : 0, ws.max_prob, ws.exp_sum, ws.depth, ws.reg_stats,
+                     (int)(ws.reg_stats_bytes / sizeof(double)));
   return hipGetLastError();
 }
 

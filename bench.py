@@ -61,19 +61,18 @@ def algorithmic_work(name: str, B: int, N: int, H: int, W: int, launches_per_pla
     """(kind, amount per launch) of a sweep kernel; kind 'bytes' (HBM) or 'flops' (MFMA).
 
     Per-unit figures:
-      cost_final   128*(N+1) B per hypothesis: ref + N-1 source features read once,
-                   the 32-ch cost slice written once (fp32);
-      cost_t1      same source/ref reads + the 16-B/px/view omega conv output;
+      cost_pipe    128*(N+1) B per hypothesis: ref + N-1 source features read once,
+                   the 32-ch cost slice written once (fp32) -- one plane's cost slice
+                   per launch (the launch also produces the next plane's omega conv);
+      omega_stats  16*(N-1) B per hypothesis (the omega conv output, 4 ch per view);
       lstm_cell k  2*9*Cin*Cout FLOP per cell pixel;
       deconv       2*16*16*9 FLOP per deconv input pixel (each input pixel meets the 3x3 kernel once);
       head_wta     8*9*2 FLOP per pixel.
     """
     HW = H * W
     nsrc = N - 1
-    if name == "cost_final":
+    if name == "cost_pipe":
         return "bytes", 128.0 * (N + 1) * B * HW / launches_per_plane
-    if name == "cost_t1":
-        return "bytes", (128.0 * N + 16.0 * nsrc) * B * HW / launches_per_plane
     if name in ("omega_stats1", "omega_stats2"):
         return "bytes", 16.0 * nsrc * B * HW / launches_per_plane
     if name.startswith("lstm_cell"):
@@ -212,7 +211,7 @@ def main():
                         per_launch=r["per_launch"], avg_us=r["avg_us"])
         # the warp + aggregation path as a whole (every launch that produces the cost
         # slice): 128*(N+1) algorithmic B/hyp over the summed device time of its kernels
-        group = [k for k in ("cost_t1", "omega_stats1", "omega_stats2", "cost_final") if k in prof]
+        group = [k for k in ("cost_pipe", "omega_stats1", "omega_stats2") if k in prof]
         if group:
             ms = sum(prof[k][1] for k in group)
             planes = D * args.steps
