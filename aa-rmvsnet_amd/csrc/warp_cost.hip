@@ -236,8 +236,8 @@ struct OmegaP {
   float g0w[4], g0b[4], g1w[4], g1b[4], g2w[4], g2b[4];
 };
 
-__device__ __forceinline__ void load_omega(const PipeArgs& a, OmegaP& o) {
-  const float* P = a.params;
+__device__ __forceinline__ void load_omega(const PipeArgs& a, const float* __restrict__ P,
+                                           OmegaP& o) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     o.w1[i] = P[a.off_ow1 + i];
@@ -282,9 +282,10 @@ __device__ __forceinline__ void conv1x1_4(const float (&x)[4], const float* w, c
 
 // omega weight of one (pixel, view) from its conv3x3 output t and the three GN stats
 // (drmvsnet.py:30-35 after the first conv)
-__device__ __forceinline__ float omega_weight(const float4 q, const GnStat* gs, const PipeArgs& a) {
+__device__ __forceinline__ float omega_weight(const float4 q, const GnStat* gs, const PipeArgs& a,
+                                              const float* __restrict__ P) {
   OmegaP o;
-  load_omega(a, o);
+  load_omega(a, P, o);
   const float t[4] = {q.x, q.y, q.z, q.w};
   float aa[4], t2[4], bb[4], t3[4], g3[4];
   gn_relu4(t, gs[0], o.g0w, o.g0b, true, aa);
@@ -325,7 +326,8 @@ __device__ __forceinline__ void tile_range(int ntiles, int& t0, int& t1) {
 }
 
 template <int TH>
-__global__ void __launch_bounds__(TH * kPipeTW) cost_pipe_kernel(PipeArgs a) {
+__global__ void __launch_bounds__(TH * kPipeTW) cost_pipe_kernel(PipeArgs a,
+                                                                 const float* __restrict__ P) {
   using Cfg = PipeCfg<TH>;
   __shared__ float sq[kC * Cfg::NPIX];
   __shared__ float wsum[Cfg::WAVES][AARMVS_MAX_SRC][2];
@@ -341,8 +343,10 @@ __global__ void __launch_bounds__(TH * kPipeTW) cost_pipe_kernel(PipeArgs a) {
     gs[v][k] = stat_read(a.st_prev + st_index(b, v, k, nsrc), 4.0 * HW);
   }
   __syncthreads();
-  const float* w0 = a.params + a.off_ow0;   // [4][32][9]
-  const float* b0 = a.params + a.off_ob0;
+  // parameters come through a __restrict__ argument so that their uniform loads can be
+  // scalar (s_load) despite the kernel's vector stores
+  const float* __restrict__ w0 = P + a.off_ow0;   // [4][32][9]
+  const float* __restrict__ b0 = P + a.off_ob0;
   const float dprev = prev ? a.dvals[b * a.D + a.d_prev] : 0.f;
   const float dnext = next ? a.dvals[b * a.D + a.d_next] : 0.f;
   const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's [32,H,W] map
@@ -380,7 +384,7 @@ __global__ void __launch_bounds__(TH * kPipeTW) cost_pipe_kernel(PipeArgs a) {
       const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
       if (prev && inside) {
         const float wv =
-            omega_weight(a.t1_prev[((size_t)b * nsrc + v) * HW + p], gs[v], a);
+            omega_weight(a.t1_prev[((size_t)b * nsrc + v) * HW + p], gs[v], a, P);
         if (a.omega_out) a.omega_out[((size_t)v * a.B + b) * HW + p] = wv;
         const float wp1 = __fadd_rn(wv, 1.0f);
         float ix, iy;
@@ -482,7 +486,8 @@ __global__ void __launch_bounds__(TH * kPipeTW) cost_pipe_kernel(PipeArgs a) {
 // GN #STAGE (1 or 2) partial sums of the omega chain on t1 (plane d_next).  Stage 1
 // also clears the statistics of the plane before (their last reader has finished).
 template <int STAGE>
-__global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a) {
+__global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
+                                                          const float* __restrict__ P) {
   __shared__ float red[2 * 4];
   __shared__ GnStat gs[2];
   const int v = blockIdx.y, b = blockIdx.z;
@@ -494,7 +499,7 @@ __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a) {
     gs[threadIdx.x] = stat_read(a.st_next + st_index(b, v, threadIdx.x, a.nsrc), 4.0 * HW);
   __syncthreads();
   OmegaP o;
-  load_omega(a, o);
+  load_omega(a, P, o);
   const float4* t1 = a.t1_next + ((size_t)b * a.nsrc + v) * HW;
   float part[2] = {0.f, 0.f};
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
@@ -573,7 +578,8 @@ hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Worksp
   hipError_t e;
   {
     ProfScope ps(s, K_COST_PIPE);
-    hipLaunchKernelGGL(cost_pipe_kernel<kPipeTH>, dim3(blocks, g.B), dim3(Cfg::THREADS), 0, s, a);
+    hipLaunchKernelGGL(cost_pipe_kernel<kPipeTH>, dim3(blocks, g.B), dim3(Cfg::THREADS), 0, s, a,
+                       a.params);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (d_next < 0) return hipSuccess;
@@ -587,12 +593,12 @@ hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Worksp
       std::max(1, std::min((HW + 255) / 256, 2 * g.cu_count / std::max(1, g.B * g.nsrc) + 1));
   {
     ProfScope ps(s, K_OMEGA1);
-    hipLaunchKernelGGL(omega_stats_kernel<1>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(omega_stats_kernel<1>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a, a.params);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   {
     ProfScope ps(s, K_OMEGA2);
-    hipLaunchKernelGGL(omega_stats_kernel<2>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(omega_stats_kernel<2>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a, a.params);
   }
   return hipGetLastError();
 }
