@@ -142,11 +142,16 @@ def test_training_backward_matches_cpu_autograd():
     gi = imgs.grad.cpu().numpy()
     gref = np.moveaxis(fc.grad.numpy(), 0, 1)
     np.testing.assert_allclose(gi, gref, atol=1e-4 * np.abs(gref).max())
-    # conv_0.bias's true gradient is 0 (softmax over D sums the cost gradients to zero),
-    # so each parameter is compared at 1e-4 of max(its own scale, 1e-3 x the largest)
+    # conv_0.bias's true gradient is exactly 0 (softmax over D sums the cost gradients to
+    # zero): both sides hold only fp32 cancellation noise, so it is checked for smallness;
+    # every other parameter at 1e-4 of max(its own scale, 1e-3 x the largest)
     gmax = max(float(p.grad.abs().max()) for p in P_cpu.values())
     for k, p in m.named_parameters():
-        if k in P_cpu:
-            gr = P_cpu[k].grad.numpy()
-            tol = 1e-4 * max(np.abs(gr).max(), 1e-3 * gmax)
-            np.testing.assert_allclose(p.grad.cpu().numpy(), gr, atol=tol, err_msg=k)
+        if k not in P_cpu:
+            continue
+        gr = P_cpu[k].grad.numpy()
+        if k == "cost_regularization.conv_0.bias":
+            assert abs(float(p.grad)) < 1e-4 * gmax and abs(float(gr)) < 1e-4 * gmax
+            continue
+        tol = 1e-4 * max(np.abs(gr).max(), 1e-3 * gmax)
+        np.testing.assert_allclose(p.grad.cpu().numpy(), gr, atol=tol, err_msg=k)
