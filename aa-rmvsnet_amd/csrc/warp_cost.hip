@@ -303,44 +303,81 @@ __device__ __forceinline__ size_t st_index(int b, int v, int k, int nsrc) {
   return (((size_t)b * nsrc + v) * 3 + k) * kSlots * 2;
 }
 
+// NHWC gathers: a tap of one pixel is 32 contiguous channels (128 B); lane k of an
+// 8-lane pixel group loads channels 4k..4k+3 with one dwordx4 (the per-CU address rate,
+// not HBM, limits dword gathers).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                     __uint_as_float(v.w));
+}
+
+// byte offsets of the 4 taps (pixel * 128 B, or `oob`) + weights
+__device__ __forceinline__ BTaps make_ntaps(float ix, float iy, int H, int W, uint32_t oob) {
+  BTaps t = make_btaps(ix, iy, H, W, oob);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (t.off[k] != oob) t.off[k] *= 32u;   // dword offset of the pixel * 4 B -> * 128 B
+  return t;
+}
+
+// bilinear sample of 4 channels (byte offset `coff` within the pixel), same fma chain
+__device__ __forceinline__ float4 bilinear4(__amdgpu_buffer_rsrc_t r, const BTaps& t, uint32_t coff) {
+  const float4 v0 = ld4(r, t.off[0] + coff), v1 = ld4(r, t.off[1] + coff);
+  const float4 v2 = ld4(r, t.off[2] + coff), v3 = ld4(r, t.off[3] + coff);
+  auto one = [&](float a0, float a1, float a2, float a3) {
+    return __fmaf_rn(a3, t.wt[3], __fmaf_rn(a2, t.wt[2], __fmaf_rn(a1, t.wt[1], __fmul_rn(a0, t.wt[0]))));
+  };
+  return make_float4(one(v0.x, v1.x, v2.x, v3.x), one(v0.y, v1.y, v2.y, v3.y),
+                     one(v0.z, v1.z, v2.z, v3.z), one(v0.w, v1.w, v2.w, v3.w));
+}
+
+struct RingTap {
+  BTaps t;
+  uint32_t qofs;   // reference pixel byte offset (or out of range)
+  int hidx;        // position in the halo tile
+};
+
 constexpr int kPipeTW = 32;
+constexpr int kPipeThreads = 256;   // 32 pixel columns x 8 lanes
+constexpr int kSqStride = 36;       // floats per pixel in the LDS tile: conflict-free b128 reads
 
 template <int TH>
 struct PipeCfg {
-  static constexpr int THREADS = TH * kPipeTW;
   static constexpr int HH = TH + 2, HW = kPipeTW + 2, NPIX = HH * HW;
   static constexpr int RING = 2 * HW + 2 * TH;
-  static constexpr int WAVES = THREADS / 64;
+  static constexpr int PIX = TH * kPipeTW;
+  static constexpr int WAVES = kPipeThreads / 64;
+  static constexpr int SQ_FLOATS = NPIX * kSqStride;
+  static constexpr int WT_FLOATS = AARMVS_MAX_SRC * PIX;
+  static constexpr int LDS_FLOATS = SQ_FLOATS > WT_FLOATS ? SQ_FLOATS : WT_FLOATS;
 };
 
-// XCD-aware contiguous tile range of this block: blocks are dealt round-robin over the
-// 8 XCDs, so logical block l = xcd * (G/8) + slot gives every XCD one contiguous band of
-// tiles (neighbouring tiles share source rows in that XCD's L2).  Speed only.
-__device__ __forceinline__ void tile_range(int ntiles, int& t0, int& t1) {
-  const int G = gridDim.x;
-  int l = blockIdx.x;
-  if ((G & 7) == 0) l = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  const int chunk = (ntiles + G - 1) / G;
-  t0 = min(ntiles, l * chunk);
-  t1 = min(ntiles, t0 + chunk);
-}
-
-template <int TH>
-__global__ void __launch_bounds__(TH * kPipeTW) cost_pipe_kernel(PipeArgs a,
+// ABL: ablation bits for the diagnostic harness (tools/microbench/pipe_bench.cpp); the
+// library only instantiates ABL = 0.  1: no prev part, 2: no next-part own gathers,
+// 4: no ring gathers, 8: no conv.
+template <int TH, int ABL = 0>
+__global__ void __launch_bounds__(kPipeThreads) cost_pipe_kernel(PipeArgs a,
                                                                  const float* __restrict__ P) {
   using Cfg = PipeCfg<TH>;
-  __shared__ float sq[kC * Cfg::NPIX];
+  // sq tile (next part) and the omega-weight table (prev part) share the LDS
+  __shared__ __attribute__((aligned(16))) float lds[Cfg::LDS_FLOATS];
+  __shared__ RingTap ring[Cfg::RING];
   __shared__ float wsum[Cfg::WAVES][AARMVS_MAX_SRC][2];
   __shared__ GnStat gs[AARMVS_MAX_SRC][3];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = tid >> 3, k = tid & 7;        // 8-lane pixel groups
+  const uint32_t koff = 16u * k;                // this lane's 4 channels within a pixel
   const int b = blockIdx.y;
   const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
-  const bool prev = a.d_prev >= 0, next = a.d_next >= 0;
-  for (int i = tid; i < Cfg::WAVES * AARMVS_MAX_SRC * 2; i += Cfg::THREADS)
+  const bool prev = a.d_prev >= 0 && !(ABL & 1), next = a.d_next >= 0;
+  for (int i = tid; i < Cfg::WAVES * AARMVS_MAX_SRC * 2; i += kPipeThreads)
     (&wsum[0][0][0])[i] = 0.f;
   if (prev && tid < 3 * nsrc) {
-    const int v = tid / 3, k = tid % 3;
-    gs[v][k] = stat_read(a.st_prev + st_index(b, v, k, nsrc), 4.0 * HW);
+    const int v = tid / 3, kk = tid % 3;
+    gs[v][kk] = stat_read(a.st_prev + st_index(b, v, kk, nsrc), 4.0 * HW);
   }
   __syncthreads();
   // parameters come through a __restrict__ argument so that their uniform loads can be
@@ -349,129 +386,201 @@ __global__ void __launch_bounds__(TH * kPipeTW) cost_pipe_kernel(PipeArgs a,
   const float* __restrict__ b0 = P + a.off_ob0;
   const float dprev = prev ? a.dvals[b * a.D + a.d_prev] : 0.f;
   const float dnext = next ? a.dvals[b * a.D + a.d_next] : 0.f;
-  const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's [32,H,W] map
+  const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's [H,W,32] map
   const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(a.ref + (size_t)b * kC * HW, fbytes);
-  const uint32_t cstride = (uint32_t)HW * 4u;
   const float inv_n = (float)nsrc;
+  const int tiles_x = (W + kPipeTW - 1) / kPipeTW;
+  const int tile = blockIdx.x;
+  const int y0 = (tile / tiles_x) * TH, x0 = (tile % tiles_x) * kPipeTW;
 
-  // ring (halo-only) pixel of this thread, in halo-tile coordinates
-  int rhy = -1, rhx = -1;
-  if (tid < Cfg::RING) {
-    const int i = tid;
-    if (i < Cfg::HW) { rhy = 0; rhx = i; }
-    else if (i < 2 * Cfg::HW) { rhy = TH + 1; rhx = i - Cfg::HW; }
-    else if (i < 2 * Cfg::HW + TH) { rhy = 1 + i - 2 * Cfg::HW; rhx = 0; }
-    else { rhy = 1 + i - 2 * Cfg::HW - TH; rhx = Cfg::HW - 1; }
-  }
-  const int ty = tid / kPipeTW, tx = tid % kPipeTW;
-
-  const int tiles_x = (W + kPipeTW - 1) / kPipeTW, tiles_y = (H + TH - 1) / TH;
-  int tb, te;
-  tile_range(tiles_x * tiles_y, tb, te);
-  for (int tile = tb; tile < te; ++tile) {
-    const int y0 = (tile / tiles_x) * TH, x0 = (tile % tiles_x) * kPipeTW;
-    const int gy = y0 + ty, gx = x0 + tx;
-    const bool inside = gy < H && gx < W;
-    const int p = gy * W + gx;
-    const uint32_t pofs = inside ? (uint32_t)p * 4u : fbytes;   // reference pixel (re-read: L1/L2)
-    float acc[kC];
+  if (prev) {
+    // omega weights w_v of the tile's pixels (one pixel per thread) -> LDS; two views
+    // per step so that two t1 loads are in flight
+    float* wtab = lds;
+    for (int i = tid; i < Cfg::PIX; i += kPipeThreads) {
+      const int gy = y0 + i / kPipeTW, gx = x0 + i % kPipeTW;
+      const bool inside = gy < H && gx < W;
+      const size_t p = inside ? (size_t)gy * W + gx : 0;
+      for (int v = 0; v < nsrc; v += 2) {
+        const bool two = v + 1 < nsrc;
+        const float4 q0 = a.t1_prev[((size_t)b * nsrc + v) * HW + p];
+        const float4 q1 = two ? a.t1_prev[((size_t)b * nsrc + v + 1) * HW + p] : q0;
+        const float w0v = inside ? omega_weight(q0, gs[v], a, P) : 0.f;
+        wtab[v * Cfg::PIX + i] = __fadd_rn(w0v, 1.0f);
+        if (inside && a.omega_out) a.omega_out[((size_t)v * a.B + b) * HW + p] = w0v;
+        if (two) {
+          const float w1v = inside ? omega_weight(q1, gs[v + 1], a, P) : 0.f;
+          wtab[(v + 1) * Cfg::PIX + i] = __fadd_rn(w1v, 1.0f);
+          if (inside && a.omega_out) a.omega_out[((size_t)(v + 1) * a.B + b) * HW + p] = w1v;
+        }
+      }
+    }
+    __syncthreads();
+    // x = -(sum_v (1 + w_v) (warp_v - ref)^2) / nsrc, 4 channels per lane; RB rows and
+    // two views per step keep 2 x RB x 4 tap loads in flight (the view order of the
+    // accumulation is kept)
+    constexpr int RB = 2;
+    static_assert(TH % RB == 0, "rows per step must divide the tile height");
+    for (int r0 = 0; r0 < TH; r0 += RB) {
+      int gy[RB], gx = x0 + col, p[RB];
+      bool inside[RB];
+      float4 rf[RB], acc[RB];
 #pragma unroll
-    for (int c = 0; c < kC; ++c) acc[c] = 0.f;
-    const int ry = y0 - 1 + rhy, rx = x0 - 1 + rhx;
-    const bool ring_in = rhy >= 0 && ry >= 0 && ry < H && rx >= 0 && rx < W;
+      for (int j = 0; j < RB; ++j) {
+        gy[j] = y0 + r0 + j;
+        inside[j] = gy[j] < H && gx < W;
+        p[j] = gy[j] * W + gx;
+        rf[j] = ld4(rref, (inside[j] ? (uint32_t)p[j] * 128u : fbytes) + koff);
+        acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      for (int v = 0; v < nsrc; v += 2) {
+        const int nv = v + 1 < nsrc ? 2 : 1;
+        float4 g[2][RB];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (u < nv) {
+            const __amdgpu_buffer_rsrc_t rsrc =
+                uniform_rsrc(a.src[v + u] + (size_t)b * kC * HW, fbytes);
+#pragma unroll
+            for (int j = 0; j < RB; ++j) {
+              float ix, iy;
+              sample_pos(a.rel + 12 * ((v + u) * a.B + b), dprev, (float)gx, (float)gy[j], H, W,
+                         ix, iy);
+              const BTaps t = make_ntaps(ix, iy, H, W, fbytes);
+              g[u][j] = bilinear4(rsrc, t, koff);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (u < nv) {
+#pragma unroll
+            for (int j = 0; j < RB; ++j) {
+              const float wp1 = wtab[(v + u) * Cfg::PIX + (r0 + j) * kPipeTW + col];
+              const float dx = __fsub_rn(g[u][j].x, rf[j].x), dy = __fsub_rn(g[u][j].y, rf[j].y);
+              const float dz = __fsub_rn(g[u][j].z, rf[j].z), dw = __fsub_rn(g[u][j].w, rf[j].w);
+              acc[j].x = __fadd_rn(acc[j].x, __fmul_rn(wp1, __fmul_rn(dx, dx)));
+              acc[j].y = __fadd_rn(acc[j].y, __fmul_rn(wp1, __fmul_rn(dy, dy)));
+              acc[j].z = __fadd_rn(acc[j].z, __fmul_rn(wp1, __fmul_rn(dz, dz)));
+              acc[j].w = __fadd_rn(acc[j].w, __fmul_rn(wp1, __fmul_rn(dw, dw)));
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < RB; ++j) {
+        if (inside[j]) {
+          float* xo = a.x + (size_t)b * kC * HW + (size_t)(4 * k) * HW + p[j];   // NCHW
+          xo[0] = -1.0f * __fdiv_rn(acc[j].x, inv_n);
+          xo[(size_t)HW] = -1.0f * __fdiv_rn(acc[j].y, inv_n);
+          xo[(size_t)2 * HW] = -1.0f * __fdiv_rn(acc[j].z, inv_n);
+          xo[(size_t)3 * HW] = -1.0f * __fdiv_rn(acc[j].w, inv_n);
+        }
+      }
+    }
+    __syncthreads();   // the weight table's LDS becomes the sq tile
+  }
+
+  if (next) {
+    float* sq = lds;
     for (int v = 0; v < nsrc; ++v) {
       const float* m = a.rel + 12 * (v * a.B + b);
       const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
-      if (prev && inside) {
-        const float wv =
-            omega_weight(a.t1_prev[((size_t)b * nsrc + v) * HW + p], gs[v], a, P);
-        if (a.omega_out) a.omega_out[((size_t)v * a.B + b) * HW + p] = wv;
-        const float wp1 = __fadd_rn(wv, 1.0f);
-        float ix, iy;
-        sample_pos(m, dprev, (float)gx, (float)gy, H, W, ix, iy);
-        const BTaps t = make_btaps(ix, iy, H, W, fbytes);
-#pragma unroll 8
-        for (int c = 0; c < kC; ++c) {
-          const float d = __fsub_rn(bilinear_b(rsrc, t, c * cstride), load_b(rref, pofs, c * cstride));
-          acc[c] = __fadd_rn(acc[c], __fmul_rn(wp1, __fmul_rn(d, d)));
+      if (tid < Cfg::RING) {
+        // taps of this thread's ring (halo-only) pixel, shared through LDS
+        int hy, hx;
+        if (tid < Cfg::HW) { hy = 0; hx = tid; }
+        else if (tid < 2 * Cfg::HW) { hy = TH + 1; hx = tid - Cfg::HW; }
+        else if (tid < 2 * Cfg::HW + TH) { hy = 1 + tid - 2 * Cfg::HW; hx = 0; }
+        else { hy = 1 + tid - 2 * Cfg::HW - TH; hx = Cfg::HW - 1; }
+        const int ry = y0 - 1 + hy, rx = x0 - 1 + hx;
+        RingTap rt;
+        rt.hidx = hy * Cfg::HW + hx;
+        if (ry >= 0 && ry < H && rx >= 0 && rx < W && !(ABL & 4)) {
+          float ix, iy;
+          sample_pos(m, dnext, (float)rx, (float)ry, H, W, ix, iy);
+          rt.t = make_ntaps(ix, iy, H, W, fbytes);
+          rt.qofs = (uint32_t)(ry * W + rx) * 128u;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            rt.t.off[q] = fbytes;
+            rt.t.wt[q] = 0.f;
+          }
+          rt.qofs = fbytes;
         }
+        ring[tid] = rt;
       }
-      if (next) {
-        // own (interior) pixel
-        {
-          const int hidx = (ty + 1) * Cfg::HW + tx + 1;
-          if (inside) {
-            float ix, iy;
-            sample_pos(m, dnext, (float)gx, (float)gy, H, W, ix, iy);
-            const BTaps t = make_btaps(ix, iy, H, W, fbytes);
-#pragma unroll 8
-            for (int c = 0; c < kC; ++c) {
-              const float d = __fsub_rn(bilinear_b(rsrc, t, c * cstride), load_b(rref, pofs, c * cstride));
-              sq[c * Cfg::NPIX + hidx] = __fmul_rn(d, d);
-            }
-          } else {
+      // own rows: squared difference at d_next -> LDS tile (zero outside the image)
+      for (int r = 0; r < TH; ++r) {
+        const int gy = y0 + r, gx = x0 + col;
+        const bool inside = gy < H && gx < W && !(ABL & 2);
+        float ix, iy;
+        sample_pos(m, dnext, (float)gx, (float)gy, H, W, ix, iy);
+        BTaps t = make_ntaps(ix, iy, H, W, fbytes);
+        if (!inside)
 #pragma unroll
-            for (int c = 0; c < kC; ++c) sq[c * Cfg::NPIX + hidx] = 0.f;
-          }
-        }
-        // ring pixel (zero outside the image: the conv's zero padding)
-        if (rhy >= 0) {
-          const int hidx = rhy * Cfg::HW + rhx;
-          if (ring_in) {
-            float ix, iy;
-            sample_pos(m, dnext, (float)rx, (float)ry, H, W, ix, iy);
-            const BTaps t = make_btaps(ix, iy, H, W, fbytes);
-            const uint32_t qofs = (uint32_t)(ry * W + rx) * 4u;
-#pragma unroll 8
-            for (int c = 0; c < kC; ++c) {
-              const float d = __fsub_rn(bilinear_b(rsrc, t, c * cstride), load_b(rref, qofs, c * cstride));
-              sq[c * Cfg::NPIX + hidx] = __fmul_rn(d, d);
-            }
-          } else {
-#pragma unroll
-            for (int c = 0; c < kC; ++c) sq[c * Cfg::NPIX + hidx] = 0.f;
-          }
-        }
-        __syncthreads();
-        // omega.reweight_network.0.0: conv3x3 32->4, pad 1
+          for (int q = 0; q < 4; ++q) t.off[q] = fbytes;
+        const float4 g = bilinear4(rsrc, t, koff);
+        const float4 rf = ld4(rref, (inside ? (uint32_t)(gy * W + gx) * 128u : fbytes) + koff);
+        const float dx = __fsub_rn(g.x, rf.x), dy = __fsub_rn(g.y, rf.y);
+        const float dz = __fsub_rn(g.z, rf.z), dw = __fsub_rn(g.w, rf.w);
+        *reinterpret_cast<float4*>(&sq[((r + 1) * Cfg::HW + col + 1) * kSqStride + 4 * k]) =
+            make_float4(__fmul_rn(dx, dx), __fmul_rn(dy, dy), __fmul_rn(dz, dz), __fmul_rn(dw, dw));
+      }
+      __syncthreads();   // ring tap table ready
+      for (int i = tid; i < Cfg::RING * 8; i += kPipeThreads) {
+        const RingTap& rt = ring[i >> 3];   // (i & 7) == k
+        const float4 g = bilinear4(rsrc, rt.t, koff);
+        const float4 rf = ld4(rref, rt.qofs + koff);
+        const float dx = __fsub_rn(g.x, rf.x), dy = __fsub_rn(g.y, rf.y);
+        const float dz = __fsub_rn(g.z, rf.z), dw = __fsub_rn(g.w, rf.w);
+        *reinterpret_cast<float4*>(&sq[rt.hidx * kSqStride + 4 * k]) =
+            make_float4(__fmul_rn(dx, dx), __fmul_rn(dy, dy), __fmul_rn(dz, dz), __fmul_rn(dw, dw));
+      }
+      __syncthreads();
+      // omega.reweight_network.0.0: conv3x3 32->4, pad 1; one output pixel per thread
+      float ps = 0.f, pss = 0.f;
+      for (int i = tid; i < Cfg::PIX; i += kPipeThreads) {
+        const int py = i / kPipeTW, px = i % kPipeTW;
         float o4[4] = {0.f, 0.f, 0.f, 0.f};
+        if (!(ABL & 8)) {
 #pragma unroll 1
-        for (int ci = 0; ci < kC; ++ci) {
-#pragma unroll
           for (int tap = 0; tap < 9; ++tap) {
-            const float s = sq[ci * Cfg::NPIX + (ty + tap / 3) * Cfg::HW + tx + tap % 3];
+            const float4* s4 = reinterpret_cast<const float4*>(
+                &sq[((py + tap / 3) * Cfg::HW + px + tap % 3) * kSqStride]);
+#pragma unroll 2
+            for (int c4 = 0; c4 < 8; ++c4) {
+              const float4 q = s4[c4];
+              const float qq[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-            for (int co = 0; co < 4; ++co) o4[co] = fmaf(s, w0[(co * kC + ci) * 9 + tap], o4[co]);
+              for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int co = 0; co < 4; ++co)
+                  o4[co] = fmaf(qq[j], w0[(co * kC + 4 * c4 + j) * 9 + tap], o4[co]);
+            }
           }
         }
-        float ps = 0.f, pss = 0.f;
-        if (inside) {
+        const int gy = y0 + py, gx = x0 + px;
+        if (gy < H && gx < W) {
           float4 out;
           out.x = o4[0] + b0[0];
           out.y = o4[1] + b0[1];
           out.z = o4[2] + b0[2];
           out.w = o4[3] + b0[3];
-          a.t1_next[((size_t)b * nsrc + v) * HW + p] = out;
-          ps = (out.x + out.y) + (out.z + out.w);
-          pss = (out.x * out.x + out.y * out.y) + (out.z * out.z + out.w * out.w);
+          a.t1_next[((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
+          ps += (out.x + out.y) + (out.z + out.w);
+          pss += (out.x * out.x + out.y * out.y) + (out.z * out.z + out.w * out.w);
         }
-        ps = wave_sum(ps);
-        pss = wave_sum(pss);
-        if (lane == 0) {
-          wsum[wave][v][0] += ps;
-          wsum[wave][v][1] += pss;
-        }
-        __syncthreads();   // sq is rewritten by the next view
       }
+      ps = wave_sum(ps);
+      pss = wave_sum(pss);
+      if (lane == 0) {
+        wsum[wave][v][0] = ps;
+        wsum[wave][v][1] = pss;
+      }
+      __syncthreads();   // sq and the ring table are rewritten for the next view
     }
-    if (prev && inside) {
-      float* xo = a.x + (size_t)b * kC * HW + p;
-#pragma unroll
-      for (int c = 0; c < kC; ++c) xo[(size_t)c * HW] = -1.0f * __fdiv_rn(acc[c], inv_n);
-    }
-  }
-  if (next) {
-    __syncthreads();
     if (tid < nsrc) {
       double s = 0.0, ss = 0.0;
       for (int w = 0; w < Cfg::WAVES; ++w) {
@@ -560,6 +669,9 @@ constexpr int kPipeTH = 8;
 hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Workspace& ws,
                             int d_prev, int d_next, float* omega_out, hipStream_t s) {
   PipeArgs a = pipe_args(ca, g, ws);
+  // the pipeline gathers from the NHWC copies of the features in the workspace
+  a.ref = ws.nhwc[0];
+  for (int v = 0; v < g.nsrc; ++v) a.src[v] = ws.nhwc[1 + v];
   a.d_prev = d_prev;
   a.d_next = d_next;
   if (d_prev >= 0) {
@@ -571,14 +683,11 @@ hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Worksp
     a.st_next = ws.omega_stats[d_next & 1];
   }
   a.omega_out = omega_out;
-  using Cfg = PipeCfg<kPipeTH>;
   const int ntiles = ((g.W + kPipeTW - 1) / kPipeTW) * ((g.H + kPipeTH - 1) / kPipeTH);
-  int blocks = std::max(1, std::min(ntiles, 4 * g.cu_count / std::max(1, g.B)));
-  if (blocks >= 64) blocks &= ~7;   // multiple of 8 for the XCD-aware tile mapping
   hipError_t e;
   {
     ProfScope ps(s, K_COST_PIPE);
-    hipLaunchKernelGGL(cost_pipe_kernel<kPipeTH>, dim3(blocks, g.B), dim3(Cfg::THREADS), 0, s, a,
+    hipLaunchKernelGGL(cost_pipe_kernel<kPipeTH>, dim3(ntiles, g.B), dim3(kPipeThreads), 0, s, a,
                        a.params);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -600,6 +709,36 @@ hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Worksp
     ProfScope ps(s, K_OMEGA2);
     hipLaunchKernelGGL(omega_stats_kernel<2>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a, a.params);
   }
+  return hipGetLastError();
+}
+
+// NCHW [B][32][HW] -> NHWC [B][HW][32] (once per sweep, so that a bilinear tap is one
+// 128-B line).  64 pixels per block through LDS: coalesced reads and 16-B writes.
+__global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* __restrict__ src,
+                                                           float* __restrict__ dst, int HW) {
+  __shared__ float t[kC][65];
+  const int b = blockIdx.y, p0 = blockIdx.x * 64;
+  const float* s = src + (size_t)b * kC * HW;
+  float* d = dst + (size_t)b * kC * HW;
+  const int px = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = (threadIdx.x >> 6) + 4 * j;
+    t[c][px] = p0 + px < HW ? s[(size_t)c * HW + p0 + px] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = threadIdx.x + 256 * j, q = idx >> 3, c4 = idx & 7;
+    if (p0 + q < HW)
+      reinterpret_cast<float4*>(d)[(size_t)(p0 + q) * 8 + c4] =
+          make_float4(t[4 * c4][q], t[4 * c4 + 1][q], t[4 * c4 + 2][q], t[4 * c4 + 3][q]);
+  }
+}
+
+hipError_t launch_to_nhwc(const float* src, float* dst, int B, int HW, hipStream_t s) {
+  ProfScope ps(s, K_TO_NHWC);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3((HW + 63) / 64, B), dim3(256), 0, s, src, dst, HW);
   return hipGetLastError();
 }
 

@@ -1,0 +1,99 @@
+// Diagnostic harness: times cost_pipe_kernel ablations at the headline geometry
+// (1600x1184, 6 source views).  Includes the kernel source; links libaarmvs.so for the
+// parameter layout / workspace carve.  Not shipped; numbers are for design decisions.
+#include "../../aa-rmvsnet_amd/csrc/warp_cost.hip"
+
+#include <cstdio>
+#include <vector>
+
+using namespace aarmvs;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+int main(int argc, char** argv) {
+  const int B = 1, H = 1184, W = 1600, nsrc = 6, D = 4;
+  const size_t HW = (size_t)H * W, fn = (size_t)kC * HW;
+  std::vector<float> h(fn);
+  uint32_t st = 1;
+  auto rnd = [&] { st = st * 1664525u + 1013904223u; return ((st >> 8) & 0xFFFF) / 65536.0f - 0.5f; };
+  float* feats[7];
+  for (int v = 0; v < 7; ++v) {
+    for (size_t i = 0; i < fn; ++i) h[i] = rnd();
+    CK(hipMalloc(&feats[v], fn * 4));
+    CK(hipMemcpy(feats[v], h.data(), fn * 4, hipMemcpyHostToDevice));
+  }
+  // cameras as in aarmvs.synthetic: f = W, baseline -20 mm * v, small yaw
+  std::vector<float> rel(nsrc * B * 12);
+  for (int v = 0; v < nsrc; ++v) {
+    float th = 0.02f * (v + 1) * ((v + 1) % 2 ? 1 : -1);
+    float f = W, cx = W / 2.f, cy = H / 2.f;
+    // rel = K [R|t] K^-1 (ref = identity), rows 0..2
+    float R[3][3] = {{cosf(th), 0, sinf(th)}, {0, 1, 0}, {-sinf(th), 0, cosf(th)}};
+    float t[3] = {-20.f * (v + 1), 0.3f * (v + 1), 0};
+    float Ki[3][3] = {{1 / f, 0, -cx / f}, {0, 1 / f, -cy / f}, {0, 0, 1}};
+    float K[3][3] = {{f, 0, cx}, {0, f, cy}, {0, 0, 1}};
+    float KR[3][3], M[3][3], Kt[3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) { KR[i][j] = 0; for (int k = 0; k < 3; ++k) KR[i][j] += K[i][k] * R[k][j]; }
+    for (int i = 0; i < 3; ++i) {
+      Kt[i] = 0; for (int k = 0; k < 3; ++k) Kt[i] += K[i][k] * t[k];
+      for (int j = 0; j < 3; ++j) { M[i][j] = 0; for (int k = 0; k < 3; ++k) M[i][j] += KR[i][k] * Ki[k][j]; }
+    }
+    for (int i = 0; i < 3; ++i) { for (int j = 0; j < 3; ++j) rel[v * 12 + i * 4 + j] = M[i][j]; rel[v * 12 + i * 4 + 3] = Kt[i]; }
+  }
+  float *drel, *ddv, *dpar;
+  CK(hipMalloc(&drel, rel.size() * 4)); CK(hipMemcpy(drel, rel.data(), rel.size() * 4, hipMemcpyHostToDevice));
+  float dvh[D] = {600.f, 601.f, 602.f, 603.f};
+  CK(hipMalloc(&ddv, sizeof(dvh))); CK(hipMemcpy(ddv, dvh, sizeof(dvh), hipMemcpyHostToDevice));
+  size_t pb = aarmvs_packed_param_bytes();
+  std::vector<float> ph(pb / 4);
+  for (auto& x : ph) x = 0.1f * rnd();
+  CK(hipMalloc(&dpar, pb)); CK(hipMemcpy(dpar, ph.data(), pb, hipMemcpyHostToDevice));
+  size_t wsb = aarmvs_sweep_workspace_bytes(B, H, W, nsrc);
+  void* wsp; CK(hipMalloc(&wsp, wsb)); CK(hipMemset(wsp, 0, wsb));
+  Workspace ws = carve_workspace(wsp, B, H, W, nsrc);
+  SweepGeom g{B, H, W, nsrc, D, 256};
+  CostArgs ca{};
+  ca.ref = feats[0];
+  for (int v = 0; v < nsrc; ++v) ca.src[v] = feats[v + 1];
+  ca.rel = drel; ca.depth_values = ddv; ca.params = dpar;
+  CK(launch_to_nhwc(feats[0], ws.nhwc[0], B, (int)HW, 0));
+  for (int v = 0; v < nsrc; ++v) CK(launch_to_nhwc(feats[v + 1], ws.nhwc[v + 1], B, (int)HW, 0));
+  CK(launch_cost_pipe(ca, g, ws, -1, 0, nullptr, 0));
+  CK(hipDeviceSynchronize());
+  PipeArgs a = pipe_args(ca, g, ws);
+  a.d_prev = 0; a.d_next = 1;
+  a.ref = ws.nhwc[0];
+  for (int v = 0; v < nsrc; ++v) a.src[v] = ws.nhwc[v + 1];
+  a.t1_prev = reinterpret_cast<const float4*>(ws.t1[0]); a.st_prev = ws.omega_stats[0];
+  a.t1_next = reinterpret_cast<float4*>(ws.t1[1]); a.st_next = ws.omega_stats[1];
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const int ntiles = ((W + 31) / 32) * ((H + 7) / 8);
+  auto run = [&](const char* name, auto kern, int blocks) {
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, dim3(blocks, B), dim3(256), 0, 0, a, dpar);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    const int R = 10;
+    for (int i = 0; i < R; ++i) hipLaunchKernelGGL(kern, dim3(blocks, B), dim3(256), 0, 0, a, dpar);
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("%-44s blocks %5d  %8.3f ms\n", name, blocks, ms / R);
+  };
+  run("full", cost_pipe_kernel<8, 0>, ntiles);
+  run("no prev part (1)", cost_pipe_kernel<8, 1>, ntiles);
+  run("no next own gathers (2)", cost_pipe_kernel<8, 2>, ntiles);
+  run("no ring gathers (4)", cost_pipe_kernel<8, 4>, ntiles);
+  run("no conv (8)", cost_pipe_kernel<8, 8>, ntiles);
+  run("only prev part (2|4|8)", cost_pipe_kernel<8, 14>, ntiles);
+  run("only next part gathers (1|8)", cost_pipe_kernel<8, 9>, ntiles);
+  run("nothing but launch/ring/conv-free (1|2|4|8)", cost_pipe_kernel<8, 15>, ntiles);
+  {
+    // NHWC transpose of one view
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 10; ++i) CK(launch_to_nhwc(feats[0], ws.nhwc[0], B, (int)HW, 0));
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("%-44s %8.3f ms (%.0f GB/s)\n", "to_nhwc one view", ms / 10, 2.0 * fn * 4 / (ms / 10) / 1e6);
+  }
+  CK(hipGetLastError());
+  return 0;
+}
