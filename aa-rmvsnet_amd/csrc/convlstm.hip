@@ -44,142 +44,302 @@ struct CellArgs {
   int B, H, W;          // cell resolution
 };
 
-constexpr int kLDW = 34;   // 32-pixel tile row + 1-px halo each side
+constexpr int kMaxParts = 3;
 
-template <int CIN, int HID, int TH>
-struct CellCfg {
-  static constexpr int MT = HID / 8;
-  static constexpr int COUT = 4 * HID;
-  static constexpr int K = 9 * CIN;
-  static constexpr int TROWS = TH + 2;
-  static constexpr int IN_FLOATS = CIN * TROWS * kLDW;
-  static constexpr int W_FLOATS = COUT * K;
-  static constexpr int GN_FLOATS = 2 * 16;
-  static constexpr size_t LDS_BYTES = (size_t)(W_FLOATS + IN_FLOATS + GN_FLOATS) * 4;
-  static constexpr int THREADS = TH * 64;
+// The five cells of the U-Net (drmvsnet.py:141-161): input parts in concatenation
+// order (channels, how they are staged), hidden channels, and the tile shape
+// (TH rows of NT x 32 pixels; one wave per row).
+template <int KIND>
+struct CellDef;
+template <>
+struct CellDef<0> {   // [x, h0] @ H
+  static constexpr int NP = 2, CH[kMaxParts] = {32, 16, 0};
+  static constexpr int MODE[kMaxParts] = {SRC_PLAIN, SRC_PLAIN, SRC_PLAIN};
+  static constexpr int HID = 16, TH = 4, NT = 1;
+};
+template <>
+struct CellDef<1> {   // [maxpool(h0'), h1] @ H/2
+  static constexpr int NP = 2, CH[kMaxParts] = {16, 16, 0};
+  static constexpr int MODE[kMaxParts] = {SRC_POOL, SRC_PLAIN, SRC_PLAIN};
+  static constexpr int HID = 16, TH = 8, NT = 1;
+};
+template <>
+struct CellDef<2> : CellDef<1> {};   // [maxpool(h1'), h2] @ H/4
+template <>
+struct CellDef<3> {   // [gnrelu(u0), h1', h3] @ H/2
+  static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 16};
+  static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
+  static constexpr int HID = 16, TH = 4, NT = 1;
+};
+template <>
+struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
+  static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 8};
+  static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
+  static constexpr int HID = 8, TH = 4, NT = 2;
 };
 
-template <int CIN, int HID, int TH>
-__global__ void __launch_bounds__(TH * 64) lstm_cell_kernel(CellArgs a) {
-  using Cfg = CellCfg<CIN, HID, TH>;
-  constexpr int MT = Cfg::MT;
+template <int KIND>
+struct CellCfg {
+  using D = CellDef<KIND>;
+  static constexpr int CIN = D::CH[0] + D::CH[1] + D::CH[2];
+  static constexpr int HID = D::HID, TH = D::TH, NT = D::NT;
+  static constexpr int MT = HID / 8;
+  static constexpr int COUT = 4 * HID;
+  static constexpr int CP = CIN / 2;            // k-steps per tap
+  static constexpr int TW = 32 * NT;            // tile width (pixels)
+  static constexpr int W2 = TW + 2, TROWS = TH + 2;
+  static constexpr int PLANE = TROWS * W2;      // one channel of the haloed tile
+  static constexpr int IN_FLOATS = CIN * PLANE;
+  static constexpr int W_FLOATS = COUT * 9 * CIN;
+  static constexpr int THREADS = TH * 64;
+  static constexpr size_t LDS_BYTES = (size_t)(W_FLOATS + IN_FLOATS + 32) * 4;
+  static constexpr int c0(int p) { return p == 0 ? 0 : (p == 1 ? D::CH[0] : D::CH[0] + D::CH[1]); }
+};
+
+// Input staging through registers: the next tile's loads are issued before the current
+// tile's MFMA loop and land in LDS after it (one tile of prefetch, no second LDS buffer).
+// One register block per input part, sized exactly (POOL parts hold the 2x2 window).
+template <int KIND, int P>
+struct PartRegs {
+  using C = CellCfg<KIND>;
+  using D = typename C::D;
+  static constexpr int MODE = D::MODE[P < D::NP ? P : 0];
+  static constexpr int NCH = P < D::NP ? D::CH[P] : 0;
+  static constexpr int ELEMS = NCH * C::PLANE;
+  static constexpr int NE = (ELEMS + C::THREADS - 1) / C::THREADS;
+  static constexpr int WIN = MODE == SRC_POOL ? 4 : 1;
+  float v[NE > 0 ? NE : 1][WIN];
+  uint32_t inb;   // bit j: element j lies inside the image (else zero padding)
+
+  __device__ __forceinline__ void load(const ChanSrc& s, int b, int y0, int x0, int H, int W,
+                                       int tid) {
+    inb = 0u;
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int e = tid + j * C::THREADS;
+      const int lc = e / C::PLANE, rem = e % C::PLANE;
+      const int gy = y0 - 1 + rem / C::W2, gx = x0 - 1 + rem % C::W2;
+      if (e < ELEMS && gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        inb |= 1u << j;
+        if (MODE == SRC_POOL) {
+          const int Ws = 2 * W;
+          const float* q = s.ptr + (((size_t)b * NCH + lc) * (2 * H) + 2 * gy) * Ws + 2 * gx;
+          v[j][0] = q[0];
+          v[j][WIN > 1 ? 1 : 0] = q[1];
+          v[j][WIN > 2 ? 2 : 0] = q[Ws];
+          v[j][WIN > 3 ? 3 : 0] = q[Ws + 1];
+        } else {
+          v[j][0] = s.ptr[(((size_t)b * NCH + lc) * H + gy) * W + gx];
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(float* in, const float* gn, int tid) const {
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int e = tid + j * C::THREADS;
+      if (e < ELEMS) {
+        const int lc = e / C::PLANE;
+        float x = 0.0f;
+        if (inb & (1u << j)) {
+          if (MODE == SRC_POOL)
+            x = fmaxf(fmaxf(v[j][0], v[j][WIN > 1 ? 1 : 0]),
+                      fmaxf(v[j][WIN > 2 ? 2 : 0], v[j][WIN > 3 ? 3 : 0]));
+          else if (MODE == SRC_GNRELU)
+            x = fmaxf(v[j][0] * gn[lc] + gn[16 + lc], 0.0f);
+          else
+            x = v[j][0];
+        }
+        in[(C::c0(P) + lc) * C::PLANE + e % C::PLANE] = x;
+      }
+    }
+  }
+};
+
+template <int KIND>
+struct Stager {
+  using D = CellDef<KIND>;
+  PartRegs<KIND, 0> p0;
+  PartRegs<KIND, 1> p1;
+  PartRegs<KIND, 2> p2;
+  __device__ __forceinline__ void load(const CellArgs& a, int b, int y0, int x0, int tid) {
+    p0.load(a.part[0], b, y0, x0, a.H, a.W, tid);
+    p1.load(a.part[1], b, y0, x0, a.H, a.W, tid);
+    if (D::NP > 2) p2.load(a.part[2], b, y0, x0, a.H, a.W, tid);
+  }
+  __device__ __forceinline__ void store(float* in, const float* gn, int tid) const {
+    p0.store(in, gn, tid);
+    p1.store(in, gn, tid);
+    if (D::NP > 2) p2.store(in, gn, tid);
+  }
+};
+
+template <int KIND>
+__global__ void __launch_bounds__(CellCfg<KIND>::THREADS) lstm_cell_kernel(CellArgs a) {
+  using C = CellCfg<KIND>;
+  using D = typename C::D;
+  constexpr int MT = C::MT, NT = C::NT, HID = C::HID;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* wl = lds;
-  float* in = lds + Cfg::W_FLOATS;
-  float* gn = in + Cfg::IN_FLOATS;   // [16] scale, [16] shift for a SRC_GNRELU part
+  float* in = lds + C::W_FLOATS;
+  float* gn = in + C::IN_FLOATS;   // [16] scale, [16] shift of the GN+ReLU part
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, W = a.W;
 
-  // weights -> LDS once per block (persistent over tiles)
+  // weights -> LDS once per block (persistent over tiles); 8 float4 loads in flight
   {
     const float4* s = reinterpret_cast<const float4*>(a.wpk);
     float4* d = reinterpret_cast<float4*>(wl);
-    for (int i = tid; i < Cfg::W_FLOATS / 4; i += Cfg::THREADS) d[i] = s[i];
+    constexpr int N4 = C::W_FLOATS / 4, CH8 = 8 * C::THREADS;
+    int i0 = 0;
+    for (; i0 + CH8 <= N4; i0 += CH8) {
+      float4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = s[i0 + u * C::THREADS + tid];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) d[i0 + u * C::THREADS + tid] = t[u];
+    }
+    for (int i = i0 + tid; i < N4; i += C::THREADS) d[i] = s[i];
   }
-  // fused GroupNorm(2,16) parameters of the (single) normalised part
-  for (int p = 0; p < a.nparts; ++p) {
-    if (a.part[p].mode == SRC_GNRELU && tid < 16) {
-      const double n = 8.0 * H * W;
-      const GnStat st = stat_read(a.part[p].stats + (tid >> 3) * kSlots * 2, n);
+  // fused GroupNorm(2,16) scale/shift of the normalised part (module.py:284-287)
+#pragma unroll
+  for (int p = 0; p < D::NP; ++p) {
+    if (D::MODE[p] == SRC_GNRELU && tid < 16) {
+      const GnStat st = stat_read(a.part[p].stats + (tid >> 3) * kSlots * 2, 8.0 * H * W);
       const float sc = st.rstd * a.part[p].gamma[tid];
       gn[tid] = sc;
       gn[16 + tid] = a.part[p].beta[tid] - st.mean * sc;
     }
   }
 
-  const int tiles_x = (W + 31) / 32, tiles_y = (H + TH - 1) / TH;
+  const int tiles_x = (W + C::TW - 1) / C::TW, tiles_y = (H + C::TH - 1) / C::TH;
   const int ntiles = a.B * tiles_x * tiles_y;
-  const int n0 = a.part[0].nch, n1 = n0 + (a.nparts > 1 ? a.part[1].nch : 0);
-
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int b = tile / (tiles_x * tiles_y);
+  auto tile_coords = [&](int tile, int& b, int& y0, int& x0) {
+    b = tile / (tiles_x * tiles_y);
     const int rem = tile % (tiles_x * tiles_y);
-    const int y0 = (rem / tiles_x) * TH, x0 = (rem % tiles_x) * 32;
-    __syncthreads();   // previous tile's LDS reads complete (and gn/weights visible)
-    for (int i = tid; i < Cfg::IN_FLOATS; i += Cfg::THREADS) {
-      const int ci = i / (Cfg::TROWS * kLDW);
-      const int r = (i / kLDW) % Cfg::TROWS, cc = i % kLDW;
-      const int gy = y0 - 1 + r, gx = x0 - 1 + cc;
-      float v = 0.0f;
-      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        const int p = ci < n0 ? 0 : (ci < n1 ? 1 : 2);
-        const int lc = ci - (p == 0 ? 0 : (p == 1 ? n0 : n1));
-        const ChanSrc& s = a.part[p];
-        if (s.mode == SRC_POOL) {
-          const int Ws = 2 * W, Hs = 2 * H;
-          const float* q = s.ptr + (((size_t)b * s.nch + lc) * Hs + 2 * gy) * Ws + 2 * gx;
-          v = fmaxf(fmaxf(q[0], q[1]), fmaxf(q[Ws], q[Ws + 1]));
-        } else {
-          v = s.ptr[(((size_t)b * s.nch + lc) * H + gy) * W + gx];
-          if (s.mode == SRC_GNRELU) v = fmaxf(v * gn[lc] + gn[16 + lc], 0.0f);
-        }
-      }
-      in[i] = v;
-    }
-    __syncthreads();
+    y0 = (rem / tiles_x) * C::TH;
+    x0 = (rem % tiles_x) * C::TW;
+  };
 
-    floatx16 acc[MT];
+  Stager<KIND> st;
+  int tile = blockIdx.x;
+  if (tile < ntiles) {
+    int b, y0, x0;
+    tile_coords(tile, b, y0, x0);
+    st.load(a, b, y0, x0, tid);
+  }
+  const int hi = lane >> 5, col = lane & 31;
+  for (; tile < ntiles; tile += gridDim.x) {
+    int b, y0, x0;
+    tile_coords(tile, b, y0, x0);
+    __syncthreads();   // previous tile's MFMA reads done (and weights / gn visible)
+    st.store(in, gn, tid);
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) {   // prefetch the next tile during the MFMAs
+      int nb, ny0, nx0;
+      tile_coords(tile + gridDim.x, nb, ny0, nx0);
+      st.load(a, nb, ny0, nx0, tid);
+    }
+    // cell state of this lane's outputs, needed by the epilogue
+    const int y = y0 + wave;
+    float cst[MT][NT][4];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) acc[m][j] = 0.0f;
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int x = x0 + nt * 32 + col;
+          const int ch = m * 8 + 4 * hi + q;
+          cst[m][nt][q] = (y < H && x < W) ? a.c[(((size_t)b * HID + ch) * H + y) * W + x] : 0.f;
+        }
 
-    const int hi = lane >> 5, col = lane & 31;
-    const float* inb = in + hi * Cfg::TROWS * kLDW + wave * kLDW + col;
+    floatx16 acc[MT][NT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[m][nt][j] = 0.0f;
+
+    // implicit GEMM: k = tap * CIN + ci; operands of step cp+1 are read while the
+    // MFMAs of step cp issue
+    const float* inb = in + hi * C::PLANE + wave * C::W2 + col;
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       const int dy = tap / 3, dx = tap % 3;
-      const float* bt = inb + dy * kLDW + dx;
-      const float* at = wl + (tap * (CIN / 2)) * MT * 64 + lane;
+      const float* bt = inb + dy * C::W2 + dx;
+      const float* at = wl + (tap * C::CP) * MT * 64 + lane;
+      float av[2][MT], bv[2][NT];
 #pragma unroll
-      for (int cp = 0; cp < CIN / 2; ++cp) {
-        const float bv = bt[2 * cp * Cfg::TROWS * kLDW];
+      for (int m = 0; m < MT; ++m) av[0][m] = at[m * 64];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bv[0][nt] = bt[nt * 32];
+#pragma unroll
+      for (int cp = 0; cp < C::CP; ++cp) {
+        const int cur = cp & 1, nxt = cur ^ 1;
+        if (cp + 1 < C::CP) {
+#pragma unroll
+          for (int m = 0; m < MT; ++m) av[nxt][m] = at[((cp + 1) * MT + m) * 64];
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) bv[nxt][nt] = bt[2 * (cp + 1) * C::PLANE + nt * 32];
+        }
 #pragma unroll
         for (int m = 0; m < MT; ++m)
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(at[(cp * MT + m) * 64], bv, acc[m], 0, 0, 0);
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[m][nt] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][m], bv[cur][nt], acc[m][nt], 0, 0, 0);
       }
     }
 
     // epilogue: LSTM gates (module.py:83-90)
-    const int y = y0 + wave, x = x0 + col;
-    if (y < H && x < W) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
+    for (int nt = 0; nt < NT; ++nt) {
+      const int x = x0 + nt * 32 + col;
+      if (y < H && x < W) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int ch = m * 8 + 4 * hi + q;
-          const float gi = acc[m][q] + a.bias[ch];
-          const float gf = acc[m][4 + q] + a.bias[HID + ch];
-          const float go = acc[m][8 + q] + a.bias[2 * HID + ch];
-          const float gg = acc[m][12 + q] + a.bias[3 * HID + ch];
-          const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
-          const float cn = sigmoidf_(gf) * a.c[idx] + sigmoidf_(gi) * tanhf(gg);
-          a.c[idx] = cn;
-          a.h_new[idx] = sigmoidf_(go) * tanhf(cn);
+        for (int m = 0; m < MT; ++m) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int ch = m * 8 + 4 * hi + q;
+            const float gi = acc[m][nt][q] + a.bias[ch];
+            const float gf = acc[m][nt][4 + q] + a.bias[HID + ch];
+            const float go = acc[m][nt][8 + q] + a.bias[2 * HID + ch];
+            const float gg = acc[m][nt][12 + q] + a.bias[3 * HID + ch];
+            const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
+            const float cn = sigmoidf_(gf) * cst[m][nt][q] + sigmoidf_(gi) * tanhf(gg);
+            a.c[idx] = cn;
+            a.h_new[idx] = sigmoidf_(go) * tanhf(cn);
+          }
         }
       }
     }
   }
 }
 
-template <int CIN, int HID, int TH>
+template <int KIND>
 static hipError_t run_cell(const CellArgs& a, int cu, int kid, hipStream_t s) {
-  using Cfg = CellCfg<CIN, HID, TH>;
-  static_assert(Cfg::LDS_BYTES <= 160 * 1024, "cell tile exceeds LDS");
+  using C = CellCfg<KIND>;
+  static_assert(C::LDS_BYTES <= 160 * 1024, "cell tile exceeds LDS");
+  static_assert(PartRegs<KIND, 0>::NE <= 32 && PartRegs<KIND, 1>::NE <= 32 &&
+                    PartRegs<KIND, 2>::NE <= 32,
+                "staging mask holds 32 elements per part");
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_kernel<CIN, HID, TH>,
+    hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_kernel<KIND>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)Cfg::LDS_BYTES);
+                                       (int)C::LDS_BYTES);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  const int ntiles = a.B * ((a.W + 31) / 32) * ((a.H + TH - 1) / TH);
-  const int grid = std::max(1, std::min(ntiles, cu));
+  const int ntiles = a.B * ((a.W + C::TW - 1) / C::TW) * ((a.H + C::TH - 1) / C::TH);
+  const int per_cu = (int)((160 * 1024) / C::LDS_BYTES);
+  const int grid = std::max(1, std::min(ntiles, cu * std::max(1, per_cu)));
   ProfScope ps(s, kid);
-  hipLaunchKernelGGL((lstm_cell_kernel<CIN, HID, TH>), dim3(grid), dim3(Cfg::THREADS),
-                     Cfg::LDS_BYTES, s, a);
+  hipLaunchKernelGGL(lstm_cell_kernel<KIND>, dim3(grid), dim3(C::THREADS), C::LDS_BYTES, s, a);
   return hipGetLastError();
 }
 
@@ -347,15 +507,15 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // cell 0: [x, h0] @ H
   CellArgs a0 = cell(0, {{x, 32, SRC_PLAIN, nullptr, nullptr, nullptr},
                          {ws.h[0][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
-  if ((e = run_cell<48, 16, 4>(a0, cu, K_CELL0, s)) != hipSuccess) return e;
+  if ((e = run_cell<0>(a0, cu, K_CELL0, s)) != hipSuccess) return e;
   // cell 1: [maxpool(h0'), h1] @ H/2
   CellArgs a1 = cell(1, {{ws.h[0][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {ws.h[1][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 2);
-  if ((e = run_cell<32, 16, 8>(a1, cu, K_CELL1, s)) != hipSuccess) return e;
+  if ((e = run_cell<1>(a1, cu, K_CELL1, s)) != hipSuccess) return e;
   // cell 2: [maxpool(h1'), h2] @ H/4
   CellArgs a2 = cell(2, {{ws.h[1][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {ws.h[2][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
-  if ((e = run_cell<32, 16, 8>(a2, cu, K_CELL2, s)) != hipSuccess) return e;
+  if ((e = run_cell<2>(a2, cu, K_CELL2, s)) != hipSuccess) return e;
   // GroupNorm statistics are per batch element, so the deconvs and the two cells that
   // consume their normalised output are launched per batch element.
   // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
@@ -384,7 +544,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a3.B = 1;
     a3.h_new += b * 16 * hq;
     a3.c += b * 16 * hq;
-    if ((e = run_cell<48, 16, 4>(a3, cu, K_CELL3, s)) != hipSuccess) return e;
+    if ((e = run_cell<3>(a3, cu, K_CELL3, s)) != hipSuccess) return e;
   }
   // deconv_1: h3' (H/2) -> u1 (H) + GN stats
   {
@@ -412,7 +572,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a4.B = 1;
     a4.h_new += b * 8 * hw;
     a4.c += b * 8 * hw;
-    if ((e = run_cell<40, 8, 8>(a4, cu, K_CELL4, s)) != hipSuccess) return e;
+    if ((e = run_cell<4>(a4, cu, K_CELL4, s)) != hipSuccess) return e;
   }
   return hipSuccess;
 }
