@@ -75,7 +75,7 @@ template <>
 struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 8};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
-  static constexpr int HID = 8, TH = 4, NT = 2;
+  static constexpr int HID = 8, TH = 8, NT = 1;
 };
 
 template <int KIND>
@@ -87,8 +87,11 @@ struct CellCfg {
   static constexpr int COUT = 4 * HID;
   static constexpr int CP = CIN / 2;            // k-steps per tap
   static constexpr int TW = 32 * NT;            // tile width (pixels)
-  static constexpr int W2 = TW + 2, TROWS = TH + 2;
-  static constexpr int PLANE = TROWS * W2;      // one channel of the haloed tile
+  // LDS row: [pad pad pad halo | TW interior (16-B aligned) | halo pad pad pad]
+  static constexpr int LEFT = 4;                 // interior starts at column 4
+  static constexpr int W2 = TW + 8, TROWS = TH + 2;
+  static constexpr int SEGS = TW / 4;            // float4 segments of an interior row
+  static constexpr int PLANE = TROWS * W2;       // one channel of the haloed tile
   static constexpr int IN_FLOATS = CIN * PLANE;
   static constexpr int W_FLOATS = COUT * 9 * CIN;
   static constexpr int THREADS = TH * 64;
@@ -98,60 +101,131 @@ struct CellCfg {
 
 // Input staging through registers: the next tile's loads are issued before the current
 // tile's MFMA loop and land in LDS after it (one tile of prefetch, no second LDS buffer).
-// One register block per input part, sized exactly (POOL parts hold the 2x2 window).
+// The interior of each (channel, row) is moved as float4 segments (x0 is a multiple of
+// 32 and W of 4, so they are 16-B aligned; POOL reads two float4 per fine row), the two
+// halo columns as scalars.  One register block per input part, sized exactly.
 template <int KIND, int P>
 struct PartRegs {
   using C = CellCfg<KIND>;
   using D = typename C::D;
   static constexpr int MODE = D::MODE[P < D::NP ? P : 0];
   static constexpr int NCH = P < D::NP ? D::CH[P] : 0;
-  static constexpr int ELEMS = NCH * C::PLANE;
-  static constexpr int NE = (ELEMS + C::THREADS - 1) / C::THREADS;
-  static constexpr int WIN = MODE == SRC_POOL ? 4 : 1;
-  float v[NE > 0 ? NE : 1][WIN];
-  uint32_t inb;   // bit j: element j lies inside the image (else zero padding)
+  static constexpr int SEG_ITEMS = NCH * C::TROWS * C::SEGS;   // float4 items
+  static constexpr int HALO_ITEMS = NCH * C::TROWS * 2;        // scalar items
+  static constexpr int NS = (SEG_ITEMS + C::THREADS - 1) / C::THREADS;
+  static constexpr int NH = (HALO_ITEMS + C::THREADS - 1) / C::THREADS;
+  static constexpr int WIN = MODE == SRC_POOL ? 4 : 1;   // fine-row float4 pairs x 2 rows
+  float4 seg[NS > 0 ? NS : 1][WIN];
+  float halo[NH > 0 ? NH : 1][WIN];
+  uint32_t seg_in, halo_in;   // bit j: item j lies inside the image (else zero padding)
+
+  // 4 consecutive floats at p (x .. x+3 of a row of width w): one aligned float4 when
+  // the row width is a multiple of 4, else guarded scalars (zero past the row end)
+  __device__ __forceinline__ static float4 row4(const float* p, int x, int w, bool vec) {
+    if (vec) return *reinterpret_cast<const float4*>(p);
+    float4 r;
+    r.x = p[0];
+    r.y = x + 1 < w ? p[1] : 0.f;
+    r.z = x + 2 < w ? p[2] : 0.f;
+    r.w = x + 3 < w ? p[3] : 0.f;
+    return r;
+  }
 
   __device__ __forceinline__ void load(const ChanSrc& s, int b, int y0, int x0, int H, int W,
                                        int tid) {
-    inb = 0u;
+    seg_in = halo_in = 0u;
+    const bool vec = (W & 3) == 0;   // the full-resolution W is; W/4 of a small image may not be
 #pragma unroll
-    for (int j = 0; j < NE; ++j) {
+    for (int j = 0; j < NS; ++j) {
       const int e = tid + j * C::THREADS;
-      const int lc = e / C::PLANE, rem = e % C::PLANE;
-      const int gy = y0 - 1 + rem / C::W2, gx = x0 - 1 + rem % C::W2;
-      if (e < ELEMS && gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        inb |= 1u << j;
+      const int lc = e / (C::TROWS * C::SEGS), rem = e % (C::TROWS * C::SEGS);
+      const int gy = y0 - 1 + rem / C::SEGS, gx = x0 + 4 * (rem % C::SEGS);
+      if (e < SEG_ITEMS && gy >= 0 && gy < H && gx < W) {
+        seg_in |= 1u << j;
         if (MODE == SRC_POOL) {
           const int Ws = 2 * W;
           const float* q = s.ptr + (((size_t)b * NCH + lc) * (2 * H) + 2 * gy) * Ws + 2 * gx;
-          v[j][0] = q[0];
-          v[j][WIN > 1 ? 1 : 0] = q[1];
-          v[j][WIN > 2 ? 2 : 0] = q[Ws];
-          v[j][WIN > 3 ? 3 : 0] = q[Ws + 1];
+          seg[j][0] = row4(q, 2 * gx, Ws, vec);
+          seg[j][WIN > 1 ? 1 : 0] = row4(q + 4, 2 * gx + 4, Ws, vec);
+          seg[j][WIN > 2 ? 2 : 0] = row4(q + Ws, 2 * gx, Ws, vec);
+          seg[j][WIN > 3 ? 3 : 0] = row4(q + Ws + 4, 2 * gx + 4, Ws, vec);
         } else {
-          v[j][0] = s.ptr[(((size_t)b * NCH + lc) * H + gy) * W + gx];
+          seg[j][0] = row4(s.ptr + (((size_t)b * NCH + lc) * H + gy) * W + gx, gx, W, vec);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      const int e = tid + j * C::THREADS;
+      const int lc = e / (C::TROWS * 2), rem = e % (C::TROWS * 2);
+      const int gy = y0 - 1 + rem / 2, gx = (rem & 1) ? x0 + C::TW : x0 - 1;
+      if (e < HALO_ITEMS && gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        halo_in |= 1u << j;
+        if (MODE == SRC_POOL) {
+          const int Ws = 2 * W;
+          const float* q = s.ptr + (((size_t)b * NCH + lc) * (2 * H) + 2 * gy) * Ws + 2 * gx;
+          halo[j][0] = q[0];
+          halo[j][WIN > 1 ? 1 : 0] = q[1];
+          halo[j][WIN > 2 ? 2 : 0] = q[Ws];
+          halo[j][WIN > 3 ? 3 : 0] = q[Ws + 1];
+        } else {
+          halo[j][0] = s.ptr[(((size_t)b * NCH + lc) * H + gy) * W + gx];
         }
       }
     }
   }
 
-  __device__ __forceinline__ void store(float* in, const float* gn, int tid) const {
+  __device__ __forceinline__ static float post(float v, int lc, const float* gn) {
+    return MODE == SRC_GNRELU ? fmaxf(v * gn[lc] + gn[16 + lc], 0.0f) : v;
+  }
+
+  __device__ __forceinline__ void store(float* in, const float* gn, int tid, int x0,
+                                        int W) const {
 #pragma unroll
-    for (int j = 0; j < NE; ++j) {
+    for (int j = 0; j < NS; ++j) {
       const int e = tid + j * C::THREADS;
-      if (e < ELEMS) {
-        const int lc = e / C::PLANE;
-        float x = 0.0f;
-        if (inb & (1u << j)) {
-          if (MODE == SRC_POOL)
-            x = fmaxf(fmaxf(v[j][0], v[j][WIN > 1 ? 1 : 0]),
-                      fmaxf(v[j][WIN > 2 ? 2 : 0], v[j][WIN > 3 ? 3 : 0]));
-          else if (MODE == SRC_GNRELU)
-            x = fmaxf(v[j][0] * gn[lc] + gn[16 + lc], 0.0f);
-          else
-            x = v[j][0];
+      if (e < SEG_ITEMS) {
+        const int lc = e / (C::TROWS * C::SEGS), rem = e % (C::TROWS * C::SEGS);
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (seg_in & (1u << j)) {
+          if (MODE == SRC_POOL) {
+            // 2x2 max-pool: fine rows 2gy, 2gy+1, fine columns 2gx .. 2gx+7
+            const float4 a0 = seg[j][0], a1 = seg[j][WIN > 1 ? 1 : 0];
+            const float4 c0 = seg[j][WIN > 2 ? 2 : 0], c1 = seg[j][WIN > 3 ? 3 : 0];
+            x.x = fmaxf(fmaxf(a0.x, a0.y), fmaxf(c0.x, c0.y));
+            x.y = fmaxf(fmaxf(a0.z, a0.w), fmaxf(c0.z, c0.w));
+            x.z = fmaxf(fmaxf(a1.x, a1.y), fmaxf(c1.x, c1.y));
+            x.w = fmaxf(fmaxf(a1.z, a1.w), fmaxf(c1.z, c1.w));
+          } else {
+            const float4 v = seg[j][0];
+            x = make_float4(post(v.x, lc, gn), post(v.y, lc, gn), post(v.z, lc, gn),
+                            post(v.w, lc, gn));
+          }
+          // columns past the image edge are the conv's zero padding (W % 4 != 0 only)
+          const int gx = x0 + 4 * (rem % C::SEGS);
+          if (gx + 1 >= W) x.y = 0.f;
+          if (gx + 2 >= W) x.z = 0.f;
+          if (gx + 3 >= W) x.w = 0.f;
         }
-        in[(C::c0(P) + lc) * C::PLANE + e % C::PLANE] = x;
+        *reinterpret_cast<float4*>(&in[(C::c0(P) + lc) * C::PLANE + (rem / C::SEGS) * C::W2 +
+                                       C::LEFT + 4 * (rem % C::SEGS)]) = x;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      const int e = tid + j * C::THREADS;
+      if (e < HALO_ITEMS) {
+        const int lc = e / (C::TROWS * 2), rem = e % (C::TROWS * 2);
+        float x = 0.0f;
+        if (halo_in & (1u << j)) {
+          if (MODE == SRC_POOL)
+            x = fmaxf(fmaxf(halo[j][0], halo[j][WIN > 1 ? 1 : 0]),
+                      fmaxf(halo[j][WIN > 2 ? 2 : 0], halo[j][WIN > 3 ? 3 : 0]));
+          else
+            x = post(halo[j][0], lc, gn);
+        }
+        in[(C::c0(P) + lc) * C::PLANE + (rem / 2) * C::W2 +
+           ((rem & 1) ? C::LEFT + C::TW : C::LEFT - 1)] = x;
       }
     }
   }
@@ -168,10 +242,11 @@ struct Stager {
     p1.load(a.part[1], b, y0, x0, a.H, a.W, tid);
     if (D::NP > 2) p2.load(a.part[2], b, y0, x0, a.H, a.W, tid);
   }
-  __device__ __forceinline__ void store(float* in, const float* gn, int tid) const {
-    p0.store(in, gn, tid);
-    p1.store(in, gn, tid);
-    if (D::NP > 2) p2.store(in, gn, tid);
+  __device__ __forceinline__ void store(float* in, const float* gn, int tid, int x0,
+                                        int W) const {
+    p0.store(in, gn, tid, x0, W);
+    p1.store(in, gn, tid, x0, W);
+    if (D::NP > 2) p2.store(in, gn, tid, x0, W);
   }
 };
 
@@ -235,7 +310,7 @@ __global__ void __launch_bounds__(CellCfg<KIND>::THREADS) lstm_cell_kernel(CellA
     int b, y0, x0;
     tile_coords(tile, b, y0, x0);
     __syncthreads();   // previous tile's MFMA reads done (and weights / gn visible)
-    st.store(in, gn, tid);
+    st.store(in, gn, tid, x0, W);
     __syncthreads();
     if (tile + (int)gridDim.x < ntiles) {   // prefetch the next tile during the MFMAs
       int nb, ny0, nx0;
@@ -266,7 +341,7 @@ __global__ void __launch_bounds__(CellCfg<KIND>::THREADS) lstm_cell_kernel(CellA
 
     // implicit GEMM: k = tap * CIN + ci; operands of step cp+1 are read while the
     // MFMAs of step cp issue
-    const float* inb = in + hi * C::PLANE + wave * C::W2 + col;
+    const float* inb = in + hi * C::PLANE + wave * C::W2 + (C::LEFT - 1) + col;
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       const int dy = tap / 3, dx = tap % 3;
@@ -310,9 +385,9 @@ __global__ void __launch_bounds__(CellCfg<KIND>::THREADS) lstm_cell_kernel(CellA
             const float go = acc[m][nt][8 + q] + a.bias[2 * HID + ch];
             const float gg = acc[m][nt][12 + q] + a.bias[3 * HID + ch];
             const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
-            const float cn = sigmoidf_(gf) * cst[m][nt][q] + sigmoidf_(gi) * tanhf(gg);
+            const float cn = fast_sigmoid(gf) * cst[m][nt][q] + fast_sigmoid(gi) * fast_tanh(gg);
             a.c[idx] = cn;
-            a.h_new[idx] = sigmoidf_(go) * tanhf(cn);
+            a.h_new[idx] = fast_sigmoid(go) * fast_tanh(cn);
           }
         }
       }
@@ -324,9 +399,10 @@ template <int KIND>
 static hipError_t run_cell(const CellArgs& a, int cu, int kid, hipStream_t s) {
   using C = CellCfg<KIND>;
   static_assert(C::LDS_BYTES <= 160 * 1024, "cell tile exceeds LDS");
-  static_assert(PartRegs<KIND, 0>::NE <= 32 && PartRegs<KIND, 1>::NE <= 32 &&
-                    PartRegs<KIND, 2>::NE <= 32,
-                "staging mask holds 32 elements per part");
+  static_assert(PartRegs<KIND, 0>::NS <= 32 && PartRegs<KIND, 1>::NS <= 32 &&
+                    PartRegs<KIND, 2>::NS <= 32 && PartRegs<KIND, 0>::NH <= 32,
+                "staging masks hold 32 items per part");
+  static_assert(C::TW % 32 == 0, "tile width is a multiple of 32 (16-B aligned interior)");
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_kernel<KIND>,

@@ -10,6 +10,17 @@ namespace aarmvs {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Gate activations of the LSTM epilogue on the hardware exp/rcp (v_exp_f32, v_rcp_f32:
+// ~1 ulp each, a few 1e-7 relative overall; the reference's own vectorised CPU
+// sigmoid/tanh are approximations of the same order).
+__device__ __forceinline__ float fast_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float fast_tanh(float x) {
+  // tanh(x) = 1 - 2 / (exp(2x) + 1); saturates cleanly for large |x| (exp -> inf / 0)
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
