@@ -32,18 +32,29 @@ constexpr int kParamSize[P_COUNT] = {
     16 * 16 * 9, 16, 16, 16, 16 * 16 * 9, 16, 16, 16,
     8 * 9, 1};
 
-struct ParamLayout {
-  size_t raw_off[P_COUNT];
-  size_t pk_off[P_COUNT];   // packed offsets (floats), 64-float aligned
-  size_t raw_total;
-  size_t pk_total;
-};
-const ParamLayout& param_layout();
-
 // LSTM cell geometry (drmvsnet.py:241-244): input x-channels, hidden channels, scale.
 constexpr int kCellCX[5] = {32, 16, 16, 32, 32};
 constexpr int kCellHid[5] = {16, 16, 16, 16, 8};
 constexpr int kCellScale[5] = {1, 2, 4, 2, 1};
+
+// Split-fp16 MFMA operands of a cell's conv weights (see convlstm.hip): input channels
+// padded to a multiple of 16 (one 16-channel chunk per k-group), A fragments ordered
+// [chunk][tap][m-tile][lane][8 halves], hi then lo.
+__host__ __device__ constexpr int cell_cin(int k) { return kCellCX[k] + kCellHid[k]; }
+__host__ __device__ constexpr int cell_chunks(int k) { return (cell_cin(k) + 15) / 16; }
+__host__ __device__ constexpr int cell_a_halves(int k) {   // per hi / lo
+  return cell_chunks(k) * 9 * (kCellHid[k] / 8) * 64 * 8;
+}
+
+struct ParamLayout {
+  size_t raw_off[P_COUNT];
+  size_t pk_off[P_COUNT];   // packed offsets (floats), 64-float aligned
+  size_t h3_off[5];         // split-fp16 cell weights (hi then lo halves), in floats
+  size_t h3_scale_off;      // 5 floats: 1 / (power-of-two weight scale) per cell
+  size_t raw_total;
+  size_t pk_total;
+};
+const ParamLayout& param_layout();
 
 // ---------------------------------------------------------------------------
 // Workspace layout.

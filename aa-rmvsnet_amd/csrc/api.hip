@@ -34,6 +34,12 @@ const ParamLayout& param_layout() {
       raw += kParamSize[i];
       pk += ((size_t)kParamSize[i] + 63) / 64 * 64;
     }
+    for (int k = 0; k < 5; ++k) {
+      l.h3_off[k] = pk;
+      pk += ((size_t)cell_a_halves(k) + 63) / 64 * 64;   // 2 x halves = halves floats
+    }
+    l.h3_scale_off = pk;
+    pk += 64;
     l.raw_total = raw;
     l.pk_total = pk;
     return l;
@@ -180,11 +186,52 @@ __global__ void pack_params_kernel(const float* __restrict__ raw, float* __restr
   }
 }
 
+// Split-fp16 cell weights: w * 2^e = hi + lo (both fp16, hi = fp16(w 2^e),
+// lo = fp16(w 2^e - hi)), e chosen per cell so that max|w| 2^e <= 2^14 (lo stays in
+// fp16's normal range for all but tiny weights).  One block per cell.
+__global__ void __launch_bounds__(256) pack_cell_h3_kernel(const float* __restrict__ raw,
+                                                           float* __restrict__ pk, ParamLayout L) {
+  __shared__ float red[4];
+  const int k = blockIdx.x;
+  const int hid = kCellHid[k], cin = cell_cin(k), cout = 4 * hid, mt_n = hid / 8;
+  const float* w = raw + L.raw_off[P_C0W + 2 * k];   // [cout][cin][3][3]
+  const int n = cout * cin * 9;
+  float mx = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) mx = fmaxf(mx, fabsf(w[i]));
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  int e = 0;
+  if (mx > 0.f) {
+    e = (int)floorf(log2f(16384.0f / mx));
+    e = e < -20 ? -20 : (e > 20 ? 20 : e);
+  }
+  const float sc = ldexpf(1.0f, e);
+  if (threadIdx.x == 0) pk[L.h3_scale_off + k] = ldexpf(1.0f, -e);
+  const int halves = cell_a_halves(k);
+  _Float16* hi = reinterpret_cast<_Float16*>(pk + L.h3_off[k]);
+  _Float16* lo = hi + halves;
+  for (int i = threadIdx.x; i < halves; i += blockDim.x) {
+    const int j = i & 7, l = (i >> 3) & 63, rest = i >> 9;   // [chunk][tap][mt][lane][j]
+    const int mt = rest % mt_n, tap = (rest / mt_n) % 9, c = rest / (mt_n * 9);
+    const int r = l & 31, h = l >> 5;
+    const int co = (r >> 3) * hid + 8 * mt + (r & 7);
+    const int ci = 16 * c + 8 * h + j;
+    const float v = ci < cin ? w[(co * cin + ci) * 9 + tap] * sc : 0.f;
+    const _Float16 vh = (_Float16)v;
+    hi[i] = vh;
+    lo[i] = (_Float16)(v - (float)vh);
+  }
+}
+
 hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s) {
   const ParamLayout& L = param_layout();
   hipError_t e = hipMemsetAsync(packed, 0, L.pk_total * sizeof(float), s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pack_params_kernel, dim3(32, P_COUNT), dim3(256), 0, s, raw, packed, L);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(pack_cell_h3_kernel, dim3(5), dim3(256), 0, s, raw, packed, L);
   return hipGetLastError();
 }
 

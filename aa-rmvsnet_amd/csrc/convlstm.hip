@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "device_common.h"
 
@@ -267,16 +268,9 @@ __global__ void __launch_bounds__(CellCfg<KIND>::THREADS) lstm_cell_kernel(CellA
   {
     const float4* s = reinterpret_cast<const float4*>(a.wpk);
     float4* d = reinterpret_cast<float4*>(wl);
-    constexpr int N4 = C::W_FLOATS / 4, CH8 = 8 * C::THREADS;
-    int i0 = 0;
-    for (; i0 + CH8 <= N4; i0 += CH8) {
-      float4 t[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = s[i0 + u * C::THREADS + tid];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) d[i0 + u * C::THREADS + tid] = t[u];
-    }
-    for (int i = i0 + tid; i < N4; i += C::THREADS) d[i] = s[i];
+    constexpr int N4 = C::W_FLOATS / 4;
+#pragma unroll 8
+    for (int i = tid; i < N4; i += C::THREADS) d[i] = s[i];
   }
   // fused GroupNorm(2,16) scale/shift of the normalised part (module.py:284-287)
 #pragma unroll
@@ -416,6 +410,364 @@ static hipError_t run_cell(const CellArgs& a, int cu, int kid, hipStream_t s) {
   const int grid = std::max(1, std::min(ntiles, cu * std::max(1, per_cu)));
   ProfScope ps(s, kid);
   hipLaunchKernelGGL(lstm_cell_kernel<KIND>, dim3(grid), dim3(C::THREADS), C::LDS_BYTES, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Split-fp16 ConvLSTM cell ("h3"): the same implicit GEMM on v_mfma_f32_32x32x16_f16
+// with each fp32 operand split into fp16 hi + lo and three products per k-step,
+//   w x = w_hi x_hi + w_hi x_lo + w_lo x_hi   (+ w_lo x_lo, dropped: ~2^-22 relative),
+// accumulated in fp32.  The weights carry a power-of-two scale (pack_cell_h3_kernel)
+// undone in the epilogue.  Per product the error is ~2^-21 relative, i.e. within a few
+// fp32 roundings; the depth/confidence parity is that of the fp32 path.
+// Rate: 3 x 16 K per 3 x 32 cycles vs 2 K per 64 cycles for the f32 MFMA, 5.3x.
+//
+// Input channels are processed in 16-channel chunks (one k-group of every tap); a
+// chunk of the haloed tile sits in LDS as [pixel][16 ch] fp16 (hi and lo planes, the
+// two 16-B halves of a pixel swapped on every other group of 8 pixels: conflict-free
+// ds_read_b128 B fragments).  The next chunk (or the next tile's first chunk) is
+// prefetched into registers while the MFMAs of the current one run.
+// ---------------------------------------------------------------------------
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
+template <int KIND>
+struct H3Cfg {
+  using D = CellDef<KIND>;
+  static constexpr int CIN = D::CH[0] + D::CH[1] + D::CH[2];
+  static constexpr int NCHK = (CIN + 15) / 16;
+  static constexpr int HID = D::HID, MT = HID / 8, COUT = 4 * HID;
+  static constexpr int TH = 8, THREADS = TH * 64, TW = 32, W2 = TW + 2, TROWS = TH + 2;
+  static constexpr int NPIX = TROWS * W2;
+  static constexpr int A_HALVES = NCHK * 9 * MT * 64 * 8;   // per hi / lo
+  static constexpr int SEGS = TW / 4;
+  static constexpr int SEG_ITEMS = 8 * TROWS * SEGS;         // (channel pair, row, float4 segment)
+  static constexpr int HALO_ITEMS = 8 * TROWS * 2;
+  static constexpr int NS = (SEG_ITEMS + THREADS - 1) / THREADS;
+  static constexpr int NH = (HALO_ITEMS + THREADS - 1) / THREADS;
+  static constexpr size_t LDS_BYTES = (size_t)A_HALVES * 2 * 2 + (size_t)NPIX * 32 * 2 + 32 * 4;
+  static constexpr int c0(int p) { return p == 0 ? 0 : (p == 1 ? D::CH[0] : D::CH[0] + D::CH[1]); }
+  static constexpr int chunk_part(int c) {
+    return 16 * c < c0(1) ? 0 : (16 * c < c0(2) || D::NP < 3 ? 1 : 2);
+  }
+  static constexpr int chunk_lc0(int c) { return 16 * c - c0(chunk_part(c)); }
+  static constexpr int chunk_nv(int c) {
+    return D::CH[chunk_part(c)] - chunk_lc0(c) < 16 ? D::CH[chunk_part(c)] - chunk_lc0(c) : 16;
+  }
+};
+
+// byte offset of (pixel p, 16-B half h) in a chunk plane
+__device__ __forceinline__ int h3_pix(int p, int h) { return p * 32 + ((h ^ ((p >> 3) & 1)) << 4); }
+
+__device__ __forceinline__ uint32_t h3_split2(float a, float b, uint32_t& lo_bits) {
+  const _Float16 ah = (_Float16)a, bh = (_Float16)b;
+  const half2_t hi = {ah, bh};
+  const half2_t lo = {(_Float16)(a - (float)ah), (_Float16)(b - (float)bh)};
+  lo_bits = __builtin_bit_cast(uint32_t, lo);
+  return __builtin_bit_cast(uint32_t, hi);
+}
+
+template <int KIND>
+struct H3Stager {
+  using C = H3Cfg<KIND>;
+  using D = typename C::D;
+  float4 seg[C::NS][2][4];   // [item][channel of the pair][POOL window]
+  float halo[C::NH][2][4];
+  uint32_t seg_in, halo_in;
+
+  template <int CH>
+  __device__ __forceinline__ void load(const CellArgs& a, int b, int y0, int x0, int tid) {
+    constexpr int P = C::chunk_part(CH), MODE = D::MODE[P], NCH = D::CH[P];
+    constexpr int LC0 = C::chunk_lc0(CH), NV = C::chunk_nv(CH);
+    const ChanSrc& s = a.part[P];
+    const int H = a.H, W = a.W;
+    const bool vec = (W & 3) == 0;
+    seg_in = halo_in = 0u;
+#pragma unroll
+    for (int j = 0; j < C::NS; ++j) {
+      const int e = tid + j * C::THREADS;
+      const int q = e / (C::TROWS * C::SEGS), rem = e % (C::TROWS * C::SEGS);
+      const int gy = y0 - 1 + rem / C::SEGS, gx = x0 + 4 * (rem % C::SEGS);
+      if (e < C::SEG_ITEMS && 2 * q < NV && gy >= 0 && gy < H && gx < W) {
+        seg_in |= 1u << j;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int lc = LC0 + 2 * q + u;
+          if (MODE == SRC_POOL) {
+            const int Ws = 2 * W;
+            const float* p = s.ptr + (((size_t)b * NCH + lc) * (2 * H) + 2 * gy) * Ws + 2 * gx;
+            seg[j][u][0] = PartRegs<0, 0>::row4(p, 2 * gx, Ws, vec);
+            seg[j][u][1] = PartRegs<0, 0>::row4(p + 4, 2 * gx + 4, Ws, vec);
+            seg[j][u][2] = PartRegs<0, 0>::row4(p + Ws, 2 * gx, Ws, vec);
+            seg[j][u][3] = PartRegs<0, 0>::row4(p + Ws + 4, 2 * gx + 4, Ws, vec);
+          } else {
+            seg[j][u][0] =
+                PartRegs<0, 0>::row4(s.ptr + (((size_t)b * NCH + lc) * H + gy) * W + gx, gx, W, vec);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < C::NH; ++j) {
+      const int e = tid + j * C::THREADS;
+      const int q = e / (C::TROWS * 2), rem = e % (C::TROWS * 2);
+      const int gy = y0 - 1 + rem / 2, gx = (rem & 1) ? x0 + C::TW : x0 - 1;
+      if (e < C::HALO_ITEMS && 2 * q < NV && gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        halo_in |= 1u << j;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int lc = LC0 + 2 * q + u;
+          if (MODE == SRC_POOL) {
+            const int Ws = 2 * W;
+            const float* p = s.ptr + (((size_t)b * NCH + lc) * (2 * H) + 2 * gy) * Ws + 2 * gx;
+            halo[j][u][0] = p[0];
+            halo[j][u][1] = p[1];
+            halo[j][u][2] = p[Ws];
+            halo[j][u][3] = p[Ws + 1];
+          } else {
+            halo[j][u][0] = s.ptr[(((size_t)b * NCH + lc) * H + gy) * W + gx];
+          }
+        }
+      }
+    }
+  }
+
+  template <int CH>
+  __device__ __forceinline__ float value(float4 v0, float4 v1, float4 v2, float4 v3, int e4,
+                                         int lc, const float* gn) const {
+    constexpr int MODE = D::MODE[C::chunk_part(CH)];
+    auto comp = [](float4 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w)); };
+    if (MODE == SRC_POOL) {
+      // coarse column e4 of the segment <- fine columns 2 e4, 2 e4 + 1 of rows 2gy, 2gy + 1
+      const float4 a = e4 < 2 ? v0 : v1, c = e4 < 2 ? v2 : v3;
+      const int i0 = 2 * (e4 & 1);
+      return fmaxf(fmaxf(comp(a, i0), comp(a, i0 + 1)), fmaxf(comp(c, i0), comp(c, i0 + 1)));
+    }
+    const float x = comp(v0, e4);
+    return MODE == SRC_GNRELU ? fmaxf(x * gn[lc] + gn[16 + lc], 0.0f) : x;
+  }
+
+  template <int CH>
+  __device__ __forceinline__ void store(char* hi_plane, char* lo_plane, const float* gn, int tid,
+                                        int x0, int W) const {
+    constexpr int MODE = D::MODE[C::chunk_part(CH)];
+    constexpr int LC0 = C::chunk_lc0(CH);
+#pragma unroll
+    for (int j = 0; j < C::NS; ++j) {
+      const int e = tid + j * C::THREADS;
+      if (e < C::SEG_ITEMS) {
+        const int q = e / (C::TROWS * C::SEGS), rem = e % (C::TROWS * C::SEGS);
+        const int row = rem / C::SEGS, sg = rem % C::SEGS;
+        const bool in = seg_in & (1u << j);
+        const int gx = x0 + 4 * sg;
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          float v[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            v[u] = (in && gx + e4 < W)
+                       ? value<CH>(seg[j][u][0], seg[j][u][MODE == SRC_POOL ? 1 : 0],
+                                   seg[j][u][MODE == SRC_POOL ? 2 : 0],
+                                   seg[j][u][MODE == SRC_POOL ? 3 : 0], e4, LC0 + 2 * q + u, gn)
+                       : 0.0f;
+          uint32_t lo;
+          const uint32_t hi = h3_split2(v[0], v[1], lo);
+          const int p = row * C::W2 + 1 + 4 * sg + e4;
+          const int off = h3_pix(p, q >> 2) + 4 * (q & 3);
+          *reinterpret_cast<uint32_t*>(hi_plane + off) = hi;
+          *reinterpret_cast<uint32_t*>(lo_plane + off) = lo;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < C::NH; ++j) {
+      const int e = tid + j * C::THREADS;
+      if (e < C::HALO_ITEMS) {
+        const int q = e / (C::TROWS * 2), rem = e % (C::TROWS * 2);
+        const int row = rem / 2;
+        const bool in = halo_in & (1u << j);
+        float v[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float x = 0.0f;
+          if (in) {
+            if (MODE == SRC_POOL)
+              x = fmaxf(fmaxf(halo[j][u][0], halo[j][u][1]), fmaxf(halo[j][u][2], halo[j][u][3]));
+            else if (MODE == SRC_GNRELU)
+              x = fmaxf(halo[j][u][0] * gn[LC0 + 2 * q + u] + gn[16 + LC0 + 2 * q + u], 0.0f);
+            else
+              x = halo[j][u][0];
+          }
+          v[u] = x;
+        }
+        uint32_t lo;
+        const uint32_t hi = h3_split2(v[0], v[1], lo);
+        const int p = row * C::W2 + ((rem & 1) ? C::W2 - 1 : 0);
+        const int off = h3_pix(p, q >> 2) + 4 * (q & 3);
+        *reinterpret_cast<uint32_t*>(hi_plane + off) = hi;
+        *reinterpret_cast<uint32_t*>(lo_plane + off) = lo;
+      }
+    }
+  }
+};
+
+template <int KIND, int CH>
+__device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[H3Cfg<KIND>::MT],
+                                              const char* wl_hi, const char* wl_lo,
+                                              const char* in_hi, const char* in_lo, int wave,
+                                              int lane) {
+  using C = H3Cfg<KIND>;
+  constexpr int MT = C::MT;
+  const int col = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int p = (wave + tap / 3) * C::W2 + col + tap % 3;
+    const int boff = h3_pix(p, h);
+    const half8 bh = *reinterpret_cast<const half8*>(in_hi + boff);
+    const half8 bl = *reinterpret_cast<const half8*>(in_lo + boff);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int aoff = ((((CH * 9 + tap) * MT + m) * 64) + lane) * 16;
+      const half8 ah = *reinterpret_cast<const half8*>(wl_hi + aoff);
+      const half8 al = *reinterpret_cast<const half8*>(wl_lo + aoff);
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[m], 0, 0, 0);
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[m], 0, 0, 0);
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[m], 0, 0, 0);
+    }
+  }
+}
+
+template <int KIND>
+__global__ void __launch_bounds__(H3Cfg<KIND>::THREADS) lstm_cell_h3_kernel(
+    CellArgs a, const float* __restrict__ inv_scale_ptr) {
+  using C = H3Cfg<KIND>;
+  using D = typename C::D;
+  constexpr int MT = C::MT, HID = C::HID, NCHK = C::NCHK;
+  extern __shared__ __attribute__((aligned(16))) char lds_h3[];
+  char* wl_hi = lds_h3;
+  char* wl_lo = wl_hi + C::A_HALVES * 2;
+  char* in_hi = wl_lo + C::A_HALVES * 2;
+  char* in_lo = in_hi + C::NPIX * 32;
+  float* gn = reinterpret_cast<float*>(in_lo + C::NPIX * 32);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, W = a.W;
+  const float inv_scale = *inv_scale_ptr;
+  // split-fp16 weights -> LDS once per block
+  {
+    const float4* s = reinterpret_cast<const float4*>(a.wpk);
+    float4* d = reinterpret_cast<float4*>(wl_hi);
+    constexpr int N4 = C::A_HALVES * 2 * 2 / 16;
+#pragma unroll 8
+    for (int i = tid; i < N4; i += C::THREADS) d[i] = s[i];
+  }
+#pragma unroll
+  for (int p = 0; p < D::NP; ++p) {
+    if (D::MODE[p] == SRC_GNRELU && tid < 16) {
+      const GnStat st = stat_read(a.part[p].stats + (tid >> 3) * kSlots * 2, 8.0 * H * W);
+      const float sc = st.rstd * a.part[p].gamma[tid];
+      gn[tid] = sc;
+      gn[16 + tid] = a.part[p].beta[tid] - st.mean * sc;
+    }
+  }
+
+  const int tiles_x = (W + C::TW - 1) / C::TW, tiles_y = (H + C::TH - 1) / C::TH;
+  const int ntiles = a.B * tiles_x * tiles_y;
+  auto coords = [&](int tile, int& b, int& y0, int& x0) {
+    b = tile / (tiles_x * tiles_y);
+    const int rem = tile % (tiles_x * tiles_y);
+    y0 = (rem / tiles_x) * C::TH;
+    x0 = (rem % tiles_x) * C::TW;
+  };
+  H3Stager<KIND> st;
+  int tile = blockIdx.x;
+  if (tile < ntiles) {
+    int b, y0, x0;
+    coords(tile, b, y0, x0);
+    st.template load<0>(a, b, y0, x0, tid);
+  }
+  const int hi = lane >> 5, col = lane & 31;
+  for (; tile < ntiles; tile += gridDim.x) {
+    int b, y0, x0;
+    coords(tile, b, y0, x0);
+    const int next = tile + (int)gridDim.x;
+    int nb = 0, ny0 = 0, nx0 = 0;
+    if (next < ntiles) coords(next, nb, ny0, nx0);
+    const int y = y0 + wave;
+    floatx16 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[m][j] = 0.0f;
+    float cst[MT][4];
+    // chunk loop, fully unrolled so that every chunk's staging mode is compile-time
+    auto chunk = [&](auto CHc) {
+      constexpr int CH = decltype(CHc)::value;
+      __syncthreads();   // previous chunk's B reads done (weights / gn visible the first time)
+      st.template store<CH>(in_hi, in_lo, gn, tid, x0, W);
+      __syncthreads();
+      if (CH + 1 < NCHK) {
+        st.template load<(CH + 1 < NCHK ? CH + 1 : 0)>(a, b, y0, x0, tid);
+      } else if (next < ntiles) {
+        st.template load<0>(a, nb, ny0, nx0, tid);
+      }
+      if (CH == 0) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int x = x0 + col, ch = m * 8 + 4 * hi + q;
+            cst[m][q] = (y < H && x < W) ? a.c[(((size_t)b * HID + ch) * H + y) * W + x] : 0.f;
+          }
+      }
+      h3_mfma_chunk<KIND, CH>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
+    };
+    chunk(std::integral_constant<int, 0>{});
+    if constexpr (NCHK > 1) chunk(std::integral_constant<int, 1>{});
+    if constexpr (NCHK > 2) chunk(std::integral_constant<int, 2>{});
+
+    // epilogue: LSTM gates (module.py:83-90); undo the weight scale, add the bias
+    const int x = x0 + col;
+    if (y < H && x < W) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ch = m * 8 + 4 * hi + q;
+          const float gi = fmaf(acc[m][q], inv_scale, a.bias[ch]);
+          const float gf = fmaf(acc[m][4 + q], inv_scale, a.bias[HID + ch]);
+          const float go = fmaf(acc[m][8 + q], inv_scale, a.bias[2 * HID + ch]);
+          const float gg = fmaf(acc[m][12 + q], inv_scale, a.bias[3 * HID + ch]);
+          const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
+          const float cn = fast_sigmoid(gf) * cst[m][q] + fast_sigmoid(gi) * fast_tanh(gg);
+          a.c[idx] = cn;
+          a.h_new[idx] = fast_sigmoid(go) * fast_tanh(cn);
+        }
+      }
+    }
+  }
+}
+
+template <int KIND>
+static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu, int kid,
+                              hipStream_t s) {
+  using C = H3Cfg<KIND>;
+  static_assert(C::LDS_BYTES <= 160 * 1024, "h3 cell tile exceeds LDS");
+  static_assert(C::NS <= 32 && C::NH <= 32, "staging masks hold 32 items");
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_h3_kernel<KIND>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)C::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int ntiles = a.B * ((a.W + C::TW - 1) / C::TW) * ((a.H + C::TH - 1) / C::TH);
+  const int per_cu = std::max(1, (int)((160 * 1024) / C::LDS_BYTES));
+  const int grid = std::max(1, std::min(ntiles, cu * per_cu));
+  ProfScope ps(s, kid);
+  hipLaunchKernelGGL(lstm_cell_h3_kernel<KIND>, dim3(grid), dim3(C::THREADS), C::LDS_BYTES, s, a,
+                     inv_scale);
   return hipGetLastError();
 }
 
@@ -573,7 +925,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a.nparts = i;
     a.h_new = ws.h[k][nxt];
     a.c = ws.c[k];
-    a.wpk = params + L.pk_off[P_C0W + 2 * k];
+    a.wpk = params + L.h3_off[k];   // split-fp16 A fragments
     a.bias = params + L.pk_off[P_C0B + 2 * k];
     a.B = B;
     a.H = H / scale;
@@ -583,15 +935,15 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // cell 0: [x, h0] @ H
   CellArgs a0 = cell(0, {{x, 32, SRC_PLAIN, nullptr, nullptr, nullptr},
                          {ws.h[0][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
-  if ((e = run_cell<0>(a0, cu, K_CELL0, s)) != hipSuccess) return e;
+  if ((e = run_cell_h3<0>(a0, params + L.h3_scale_off + 0, cu, K_CELL0, s)) != hipSuccess) return e;
   // cell 1: [maxpool(h0'), h1] @ H/2
   CellArgs a1 = cell(1, {{ws.h[0][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {ws.h[1][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 2);
-  if ((e = run_cell<1>(a1, cu, K_CELL1, s)) != hipSuccess) return e;
+  if ((e = run_cell_h3<1>(a1, params + L.h3_scale_off + 1, cu, K_CELL1, s)) != hipSuccess) return e;
   // cell 2: [maxpool(h1'), h2] @ H/4
   CellArgs a2 = cell(2, {{ws.h[1][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {ws.h[2][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
-  if ((e = run_cell<2>(a2, cu, K_CELL2, s)) != hipSuccess) return e;
+  if ((e = run_cell_h3<2>(a2, params + L.h3_scale_off + 2, cu, K_CELL2, s)) != hipSuccess) return e;
   // GroupNorm statistics are per batch element, so the deconvs and the two cells that
   // consume their normalised output are launched per batch element.
   // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
@@ -620,7 +972,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a3.B = 1;
     a3.h_new += b * 16 * hq;
     a3.c += b * 16 * hq;
-    if ((e = run_cell<3>(a3, cu, K_CELL3, s)) != hipSuccess) return e;
+    if ((e = run_cell_h3<3>(a3, params + L.h3_scale_off + 3, cu, K_CELL3, s)) != hipSuccess) return e;
   }
   // deconv_1: h3' (H/2) -> u1 (H) + GN stats
   {
@@ -648,7 +1000,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a4.B = 1;
     a4.h_new += b * 8 * hw;
     a4.c += b * 8 * hw;
-    if ((e = run_cell<4>(a4, cu, K_CELL4, s)) != hipSuccess) return e;
+    if ((e = run_cell_h3<4>(a4, params + L.h3_scale_off + 4, cu, K_CELL4, s)) != hipSuccess) return e;
   }
   return hipSuccess;
 }

@@ -6,14 +6,6 @@
 #include <cstdio>
 #include <vector>
 
-namespace aarmvs {
-// variants: same parts as the base kind, other tile shapes
-template <> struct CellDef<10> : CellDef<0> { static constexpr int TH = 4, NT = 1; };
-template <> struct CellDef<14> : CellDef<4> { static constexpr int TH = 4, NT = 1; };
-template <> struct CellDef<24> : CellDef<4> { static constexpr int TH = 16, NT = 1; };
-template <> struct CellDef<34> : CellDef<4> { static constexpr int TH = 8, NT = 2; };
-template <> struct CellDef<11> : CellDef<1> { static constexpr int TH = 4, NT = 1; };
-}  // namespace aarmvs
 
 using namespace aarmvs;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -36,6 +28,18 @@ int main() {
   float* hout = rnd_buf(16 * HW, 1.f);
   float* cst = rnd_buf(16 * HW, 1.f);
   float* wts = rnd_buf(64 * 48 * 9, 0.1f);
+  // split-fp16 weights (valid halves) for the h3 kernels + a scale
+  _Float16* wh;
+  {
+    std::vector<_Float16> hh(2 * 3 * 9 * 2 * 64 * 8);
+    uint32_t st = 99;
+    for (auto& x : hh) { st = st * 1664525u + 1013904223u; x = (_Float16)(((st >> 8) & 0xFFFF) / 65536.0f * 20.f - 10.f); }
+    CK(hipMalloc(&wh, hh.size() * 2)); CK(hipMemcpy(wh, hh.data(), hh.size() * 2, hipMemcpyHostToDevice));
+  }
+  float* invs = rnd_buf(1, 0.f);
+  {
+    float v = 1.0f / 1024; CK(hipMemcpy(invs, &v, 4, hipMemcpyHostToDevice));
+  }
   float* bias = rnd_buf(64, 0.1f);
   float* gamma = rnd_buf(16, 1.f);
   double* stats; CK(hipMalloc(&stats, 4 * kSlots * 2 * 8)); CK(hipMemset(stats, 0, 4 * kSlots * 2 * 8));
@@ -66,13 +70,11 @@ int main() {
   };
   const double fl0 = 2.0 * 9 * 48 * 64 * HW, fl1 = 2.0 * 9 * 32 * 64 * HW / 4, fl3 = 2.0 * 9 * 48 * 64 * HW / 4,
                fl4 = 2.0 * 9 * 40 * 32 * HW;
-  run("cell0 (TH4 NT1)", [&] { return run_cell<0>(args(0, 1), 256, K_CELL0, 0); }, fl0);
-  run("cell1 (TH8 NT1)", [&] { return run_cell<1>(args(1, 2), 256, K_CELL1, 0); }, fl1);
-  run("cell1 var TH4", [&] { return run_cell<11>(args(1, 2), 256, K_CELL1, 0); }, fl1);
-  run("cell3 (TH4 NT1)", [&] { return run_cell<3>(args(3, 2), 256, K_CELL3, 0); }, fl3);
-  run("cell4 (TH8 NT1)", [&] { return run_cell<4>(args(4, 1), 256, K_CELL4, 0); }, fl4);
-  run("cell4 var TH4 NT1", [&] { return run_cell<14>(args(4, 1), 256, K_CELL4, 0); }, fl4);
-  run("cell4 var TH16 NT1", [&] { return run_cell<24>(args(4, 1), 256, K_CELL4, 0); }, fl4);
-  run("cell4 var TH8 NT2", [&] { return run_cell<34>(args(4, 1), 256, K_CELL4, 0); }, fl4);
+  run("cell0 f32 (TH4 NT1)", [&] { return run_cell<0>(args(0, 1), 256, K_CELL0, 0); }, fl0);
+  auto h3 = [&](CellArgs a) { a.wpk = reinterpret_cast<const float*>(wh); return a; };
+  run("cell0 h3", [&] { return run_cell_h3<0>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell1 h3", [&] { return run_cell_h3<1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell3 h3", [&] { return run_cell_h3<3>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+  run("cell4 h3", [&] { return run_cell_h3<4>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
   return 0;
 }
