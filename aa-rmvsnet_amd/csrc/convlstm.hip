@@ -816,15 +816,16 @@ __global__ void __launch_bounds__(256) deconv_kernel(const float* __restrict__ i
         o[3][co] = fmaf(v00, k[8], fmaf(v01, k[6], fmaf(v10, k[2], fmaf(v11, k[0], o[3][co]))));
       }
     }
+    // the two output columns 2ix, 2ix+1 of a row are adjacent: one float2 store each
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int oy = 2 * iy + (q >> 1), ox = 2 * ix + (q & 1);
+    for (int ry = 0; ry < 2; ++ry) {
+      const int oy = 2 * iy + ry;
 #pragma unroll
       for (int co = 0; co < 16; ++co) {
-        const float r = o[q][co] + bias[co];
-        ob[((size_t)co * Ho + oy) * Wo + ox] = r;
-        part[(co >> 3) * 2] += r;
-        part[(co >> 3) * 2 + 1] += r * r;
+        const float r0 = o[2 * ry][co] + bias[co], r1 = o[2 * ry + 1][co] + bias[co];
+        *reinterpret_cast<float2*>(&ob[((size_t)co * Ho + oy) * Wo + 2 * ix]) = make_float2(r0, r1);
+        part[(co >> 3) * 2] += r0 + r1;
+        part[(co >> 3) * 2 + 1] += r0 * r0 + r1 * r1;
       }
     }
   }
@@ -839,6 +840,8 @@ __global__ void __launch_bounds__(256) deconv_kernel(const float* __restrict__ i
 // conv_0 head (drmvsnet.py:117,165: Conv2d(8,1,3,pad 1)) fused with the online
 // winner-take-all update (drmvsnet.py:324-334) and the optional cost-volume store.
 // ---------------------------------------------------------------------------
+constexpr int kHeadTH = 8, kHeadTW = 32;
+
 __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__ h4,
                                                        const float* __restrict__ w,
                                                        const float* __restrict__ bias, int H,
@@ -850,35 +853,42 @@ __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__
                                                        double* __restrict__ zero_stats,
                                                        int zero_n) {
 #pragma clang fp contract(off)
+  // the select arithmetic of drmvsnet.py:328-333 is reproduced op for op
+  __shared__ float t[8][kHeadTH + 2][kHeadTW + 2];
   // the plane's U-Net GroupNorm statistics are consumed: clear them for the next plane
   if (zero_stats && blockIdx.x == 0 && blockIdx.y == 0)
     for (int i = threadIdx.x; i < zero_n; i += blockDim.x) zero_stats[i] = 0.0;
-  // the select arithmetic of drmvsnet.py:328-333 is reproduced op for op
   const int b = blockIdx.y, HW = H * W;
+  const int tiles_x = (W + kHeadTW - 1) / kHeadTW;
+  const int y0 = (blockIdx.x / tiles_x) * kHeadTH, x0 = (blockIdx.x % tiles_x) * kHeadTW;
   const float* hb = h4 + (size_t)b * 8 * HW;
-  const float dv = wta ? dvals[b * D + d] : 0.0f;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
-    const int y = p / W, x = p % W;
-    float acc = 0.f;
-    for (int ci = 0; ci < 8; ++ci) {
+  // h4 tile with a 1-px zero-padded halo -> LDS (coalesced along x)
+  for (int i = threadIdx.x; i < 8 * (kHeadTH + 2) * (kHeadTW + 2); i += 256) {
+    const int ci = i / ((kHeadTH + 2) * (kHeadTW + 2)), rem = i % ((kHeadTH + 2) * (kHeadTW + 2));
+    const int yy = y0 - 1 + rem / (kHeadTW + 2), xx = x0 - 1 + rem % (kHeadTW + 2);
+    (&t[ci][0][0])[rem] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? hb[(size_t)ci * HW + yy * W + xx]
+                                                                     : 0.0f;
+  }
+  __syncthreads();
+  const int ty = threadIdx.x / kHeadTW, tx = threadIdx.x % kHeadTW;
+  const int y = y0 + ty, x = x0 + tx;
+  if (y >= H || x >= W) return;
+  const int p = y * W + x;
+  float acc = 0.f;
+  for (int ci = 0; ci < 8; ++ci)
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
-        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-          acc = fmaf(hb[(size_t)ci * HW + yy * W + xx], w[ci * 9 + tap], acc);
-      }
-    }
-    const float cost = acc + bias[0];
-    if (cost_out) cost_out[((size_t)b * D + d) * HW + p] = cost;
-    if (wta) {
-      const size_t q = (size_t)b * HW + p;
-      const float pr = expf(cost);
-      const float mp = max_prob[q];
-      const float f = (mp < pr) ? 1.0f : 0.0f;
-      max_prob[q] = __fadd_rn(__fmul_rn(f, pr), __fmul_rn(1.0f - f, mp));
-      depth[q] = __fadd_rn(__fmul_rn(f, dv), __fmul_rn(1.0f - f, depth[q]));
-      exp_sum[q] = __fadd_rn(exp_sum[q], pr);
-    }
+    for (int tap = 0; tap < 9; ++tap) acc = fmaf(t[ci][ty + tap / 3][tx + tap % 3], w[ci * 9 + tap], acc);
+  const float cost = acc + bias[0];
+  if (cost_out) cost_out[((size_t)b * D + d) * HW + p] = cost;
+  if (wta) {
+    const float dv = dvals[b * D + d];
+    const size_t q = (size_t)b * HW + p;
+    const float pr = expf(cost);
+    const float mp = max_prob[q];
+    const float f = (mp < pr) ? 1.0f : 0.0f;
+    max_prob[q] = __fadd_rn(__fmul_rn(f, pr), __fmul_rn(1.0f - f, mp));
+    depth[q] = __fadd_rn(__fmul_rn(f, dv), __fmul_rn(1.0f - f, depth[q]));
+    exp_sum[q] = __fadd_rn(exp_sum[q], pr);
   }
 }
 
@@ -949,7 +959,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
   {
     const int Hi = H / 4, Wi = W / 4;
-    const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 2 * cu / std::max(1, B)));
+    const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 8 * cu));
     for (int b = 0; b < B; ++b) {
       double* st = ws.reg_stats + reg_stat_index(b, 0, 0);
       ProfScope ps(s, K_DECONV0);
@@ -977,7 +987,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // deconv_1: h3' (H/2) -> u1 (H) + GN stats
   {
     const int Hi = H / 2, Wi = W / 2;
-    const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 2 * cu / std::max(1, B)));
+    const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 8 * cu));
     for (int b = 0; b < B; ++b) {
       double* st = ws.reg_stats + reg_stat_index(b, 1, 0);
       ProfScope ps(s, K_DECONV1);
@@ -1010,8 +1020,7 @@ hipError_t launch_head_wta(const float* params, const SweepGeom& g, const Worksp
                            bool wta, hipStream_t s) {
   const ParamLayout& L = param_layout();
   const int nxt = (parity & 1) ^ 1;
-  const int HW = g.H * g.W;
-  const int blocks = std::max(1, std::min((HW + 255) / 256, 8 * g.cu_count / std::max(1, g.B)));
+  const int blocks = ((g.W + kHeadTW - 1) / kHeadTW) * ((g.H + kHeadTH - 1) / kHeadTH);
   ProfScope ps(s, K_HEAD_WTA);
   hipLaunchKernelGGL(head_wta_kernel, dim3(blocks, g.B), dim3(256), 0, s, ws.h[4][nxt],
                      params + L.pk_off[P_HW], params + L.pk_off[P_HB], g.H, g.W, depth_values, d,

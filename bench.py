@@ -42,6 +42,10 @@ from aarmvs.dist import env, init_process_group, max_over_ranks  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= vector) dense peak
+F16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA peak
+# The ConvLSTM cells run each fp32 product as three f16 MFMA products (split-fp16,
+# DESIGN.md §7): their fp32-equivalent ceiling is the f16 peak / 3.
+CELL_PEAK_TFLOPS = F16_PEAK_TFLOPS / 3
 
 # BASELINE.json configs (name -> views N, H, W, D)
 CONFIGS = {
@@ -102,9 +106,10 @@ def kernel_table(prof: dict, planes: int, B: int, N: int, H: int, W: int):
                               frac=round(ach / HBM_PEAK_GBS, 4), per_launch=amount)
         else:
             ach = amount / avg_s / 1e12
+            peak = CELL_PEAK_TFLOPS if name.startswith("lstm_cell") else FP32_PEAK_TFLOPS
             rows[name] = dict(launches=n, avg_us=round(avg_s * 1e6, 2), share=round(ms / total, 4),
                               bound="mfma", achieved=round(ach, 2), unit="TFLOP/s",
-                              frac=round(ach / FP32_PEAK_TFLOPS, 4), per_launch=amount)
+                              peak=round(peak, 1), frac=round(ach / peak, 4), per_launch=amount)
     return rows
 
 
@@ -206,7 +211,7 @@ def main():
         r = kernels[dom]
         traffic = load_traffic(args.config, dom)
         roofline = dict(kernel=dom, bound=r["bound"], achieved=r["achieved"],
-                        peak=HBM_PEAK_GBS if r["bound"] == "hbm" else FP32_PEAK_TFLOPS,
+                        peak=HBM_PEAK_GBS if r["bound"] == "hbm" else r["peak"],
                         unit=r["unit"], frac=r["frac"], traffic=traffic,
                         per_launch=r["per_launch"], avg_us=r["avg_us"])
         # the warp + aggregation path as a whole (every launch that produces the cost
