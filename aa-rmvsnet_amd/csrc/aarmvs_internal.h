@@ -51,6 +51,7 @@ struct ParamLayout {
   size_t pk_off[P_COUNT];   // packed offsets (floats), 64-float aligned
   size_t h3_off[5];         // split-fp16 cell weights (hi then lo halves), in floats
   size_t h3_scale_off;      // 5 floats: 1 / (power-of-two weight scale) per cell
+  size_t ow0t_off;          // omega conv3x3 weights as [tap][ci][co] (1,152 floats)
   size_t raw_total;
   size_t pk_total;
 };

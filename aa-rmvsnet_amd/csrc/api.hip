@@ -40,6 +40,8 @@ const ParamLayout& param_layout() {
     }
     l.h3_scale_off = pk;
     pk += 64;
+    l.ow0t_off = pk;
+    pk += 4 * 32 * 9;
     l.raw_total = raw;
     l.pk_total = pk;
     return l;
@@ -225,6 +227,18 @@ __global__ void __launch_bounds__(256) pack_cell_h3_kernel(const float* __restri
   }
 }
 
+// omega conv3x3 32->4 weights [co][ci][tap] -> [tap][ci][co]: the 16 weights of one
+// (tap, 4-channel group) are contiguous (one s_load_dwordx16 in the pipeline's conv)
+__global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __restrict__ pk,
+                                       ParamLayout L) {
+  const float* w = raw + L.raw_off[P_OW0];
+  float* d = pk + L.ow0t_off;
+  for (int i = threadIdx.x; i < 4 * 32 * 9; i += blockDim.x) {
+    const int co = i % 4, ci = (i / 4) % 32, tap = i / 128;
+    d[i] = w[(co * 32 + ci) * 9 + tap];
+  }
+}
+
 hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s) {
   const ParamLayout& L = param_layout();
   hipError_t e = hipMemsetAsync(packed, 0, L.pk_total * sizeof(float), s);
@@ -232,6 +246,8 @@ hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s) {
   hipLaunchKernelGGL(pack_params_kernel, dim3(32, P_COUNT), dim3(256), 0, s, raw, packed, L);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(pack_cell_h3_kernel, dim3(5), dim3(256), 0, s, raw, packed, L);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(pack_omega_conv_kernel, dim3(1), dim3(256), 0, s, raw, packed, L);
   return hipGetLastError();
 }
 

@@ -223,7 +223,7 @@ struct PipeArgs {
   float* x;                   // [B,32,H,W]
   float* omega_out;           // [nsrc,B,H,W] (prev plane) or null
   const float* params;
-  size_t off_ow0, off_ob0, off_og0w, off_og0b, off_ow1, off_ob1, off_og1w, off_og1b, off_ow2,
+  size_t off_ow0t, off_ow0, off_ob0, off_og0w, off_og0b, off_ow1, off_ob1, off_og1w, off_og1b, off_ow2,
       off_ob2, off_og2w, off_og2b, off_owo, off_obo;
   int B, H, W, nsrc;
   double* zero_ptr;           // omega_stats<1>: stale statistics to clear (or null)
@@ -360,7 +360,8 @@ struct PipeCfg {
 // 4: no ring gathers, 8: no conv.
 template <int TH, int ABL = 0>
 __global__ void __launch_bounds__(kPipeThreads) cost_pipe_kernel(PipeArgs a,
-                                                                 const float* __restrict__ P) {
+                                                                 const float* __restrict__ P,
+                                                                 const float* __restrict__ Rel) {
   using Cfg = PipeCfg<TH>;
   // sq tile (next part) and the omega-weight table (prev part) share the LDS
   __shared__ __attribute__((aligned(16))) float lds[Cfg::LDS_FLOATS];
@@ -382,7 +383,7 @@ __global__ void __launch_bounds__(kPipeThreads) cost_pipe_kernel(PipeArgs a,
   __syncthreads();
   // parameters come through a __restrict__ argument so that their uniform loads can be
   // scalar (s_load) despite the kernel's vector stores
-  const float* __restrict__ w0 = P + a.off_ow0;   // [4][32][9]
+  const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]
   const float* __restrict__ b0 = P + a.off_ob0;
   const float dprev = prev ? a.dvals[b * a.D + a.d_prev] : 0.f;
   const float dnext = next ? a.dvals[b * a.D + a.d_next] : 0.f;
@@ -444,7 +445,7 @@ __global__ void __launch_bounds__(kPipeThreads) cost_pipe_kernel(PipeArgs a,
 #pragma unroll
             for (int j = 0; j < RB; ++j) {
               float ix, iy;
-              sample_pos(a.rel + 12 * ((v + u) * a.B + b), dprev, (float)gx, (float)gy[j], H, W,
+              sample_pos(Rel + 12 * ((v + u) * a.B + b), dprev, (float)gx, (float)gy[j], H, W,
                          ix, iy);
               const BTaps t = make_ntaps(ix, iy, H, W, fbytes);
               g[u][j] = bilinear4(rsrc, t, koff);
@@ -484,7 +485,7 @@ __global__ void __launch_bounds__(kPipeThreads) cost_pipe_kernel(PipeArgs a,
   if (next) {
     float* sq = lds;
     for (int v = 0; v < nsrc; ++v) {
-      const float* m = a.rel + 12 * (v * a.B + b);
+      const float* m = Rel + 12 * (v * a.B + b);
       const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
       if (tid < Cfg::RING) {
         // taps of this thread's ring (halo-only) pixel, shared through LDS
@@ -553,11 +554,11 @@ __global__ void __launch_bounds__(kPipeThreads) cost_pipe_kernel(PipeArgs a,
             for (int c4 = 0; c4 < 8; ++c4) {
               const float4 q = s4[c4];
               const float qq[4] = {q.x, q.y, q.z, q.w};
+              const float* wt = w0t + (tap * kC + 4 * c4) * 4;   // [j][co], contiguous
 #pragma unroll
               for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int co = 0; co < 4; ++co)
-                  o4[co] = fmaf(qq[j], w0[(co * kC + 4 * c4 + j) * 9 + tap], o4[co]);
+                for (int co = 0; co < 4; ++co) o4[co] = fmaf(qq[j], wt[j * 4 + co], o4[co]);
             }
           }
         }
@@ -648,6 +649,7 @@ static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspac
   a.W = g.W;
   a.nsrc = g.nsrc;
   a.off_ow0 = L.pk_off[P_OW0];
+  a.off_ow0t = L.ow0t_off;
   a.off_ob0 = L.pk_off[P_OB0];
   a.off_og0w = L.pk_off[P_OG0W];
   a.off_og0b = L.pk_off[P_OG0B];
@@ -688,7 +690,7 @@ hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Worksp
   {
     ProfScope ps(s, K_COST_PIPE);
     hipLaunchKernelGGL(cost_pipe_kernel<kPipeTH>, dim3(ntiles, g.B), dim3(kPipeThreads), 0, s, a,
-                       a.params);
+                       a.params, a.rel);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (d_next < 0) return hipSuccess;

@@ -69,16 +69,18 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int ntiles = ((W + 31) / 32) * ((H + 7) / 8);
   auto run = [&](const char* name, auto kern, int blocks) {
-    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, dim3(blocks, B), dim3(256), 0, 0, a, dpar);
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, dim3(blocks, B), dim3(256), 0, 0, a, dpar, drel);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
     const int R = 10;
-    for (int i = 0; i < R; ++i) hipLaunchKernelGGL(kern, dim3(blocks, B), dim3(256), 0, 0, a, dpar);
+    for (int i = 0; i < R; ++i) hipLaunchKernelGGL(kern, dim3(blocks, B), dim3(256), 0, 0, a, dpar, drel);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     printf("%-44s blocks %5d  %8.3f ms\n", name, blocks, ms / R);
   };
   run("full", cost_pipe_kernel<8, 0>, ntiles);
+  const int ntiles4 = ((W + 31) / 32) * ((H + 3) / 4);
+  run("full TH4", cost_pipe_kernel<4, 0>, ntiles4);
   run("no prev part (1)", cost_pipe_kernel<8, 1>, ntiles);
   run("no next own gathers (2)", cost_pipe_kernel<8, 2>, ntiles);
   run("no ring gathers (4)", cost_pipe_kernel<8, 4>, ntiles);
