@@ -67,7 +67,7 @@ struct Workspace {
   float* exp_sum;         // [B,HW]
   float* depth;           // [B,HW]
   float* x;               // [B,32,H,W] cost slice
-  float* nhwc[AARMVS_MAX_SRC + 1];  // [B,H,W,32] copies of ref (0) and source views
+  float* feat8[AARMVS_MAX_SRC + 1]; // [B][4][H][W][8] "c8" copies of ref (0) and source views
   float* t1[2];           // per plane parity: [B][nsrc][HW][4] omega conv3x3 output
   float* u0;              // [B,16,H/2,W/2] deconv_0 output (pre-GN)
   float* u1;              // [B,16,H,W]     deconv_1 output (pre-GN)
@@ -110,7 +110,7 @@ struct CostArgs {
 };
 // One step of the cost-slice pipeline: cost slice x of plane d_prev (if >= 0) and the
 // omega conv output + GroupNorm statistics of plane d_next (if >= 0).
-hipError_t launch_to_nhwc(const float* src, float* dst, int B, int HW, hipStream_t s);
+hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s);
 hipError_t launch_cost_pipe(const CostArgs& a, const SweepGeom& g, const Workspace& ws,
                             int d_prev, int d_next, float* omega_out, hipStream_t s);
 
@@ -131,9 +131,9 @@ int cu_count();
 // stream around each kernel.  Off by default; costs nothing when off.
 // ---------------------------------------------------------------------------
 enum KernelId : int {
-  K_COST_PIPE, K_OMEGA1, K_OMEGA2,
+  K_COST_X, K_OMEGA_CONV, K_OMEGA1, K_OMEGA2,
   K_CELL0, K_CELL1, K_CELL2, K_CELL3, K_CELL4,
-  K_DECONV0, K_DECONV1, K_HEAD_WTA, K_FINALIZE, K_SOFTMAX, K_WARP, K_TO_NHWC,
+  K_DECONV0, K_DECONV1, K_HEAD_WTA, K_FINALIZE, K_SOFTMAX, K_WARP, K_TO_C8,
   K_COUNT
 };
 extern bool g_prof_on;

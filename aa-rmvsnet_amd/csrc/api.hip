@@ -67,9 +67,9 @@ static double g_prof_ms[K_COUNT];
 static long long g_prof_n[K_COUNT];
 
 static const char* kKernelNames[K_COUNT] = {
-    "cost_pipe", "omega_stats1", "omega_stats2",
+    "cost_x", "omega_conv", "omega_stats1", "omega_stats2",
     "lstm_cell0", "lstm_cell1", "lstm_cell2", "lstm_cell3", "lstm_cell4",
-    "deconv0", "deconv1", "head_wta", "finalize", "softmax_depth", "homo_warp", "to_nhwc"};
+    "deconv0", "deconv1", "head_wta", "finalize", "softmax_depth", "homo_warp", "to_c8"};
 
 static hipEvent_t prof_event() {
   if (g_prof_used == g_prof_pool.size()) {
@@ -141,7 +141,7 @@ Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
   ws.depth = reinterpret_cast<float*>(take(B * HW * 4));
   ws.wta_bytes = off - wta_begin;
   ws.x = reinterpret_cast<float*>(take(B * kC * HW * 4));
-  for (int v = 0; v <= nsrc; ++v) ws.nhwc[v] = reinterpret_cast<float*>(take(B * kC * HW * 4));
+  for (int v = 0; v <= nsrc; ++v) ws.feat8[v] = reinterpret_cast<float*>(take(B * kC * HW * 4));
   ws.t1[0] = reinterpret_cast<float*>(take((size_t)B * nsrc * HW * 16));
   ws.t1[1] = reinterpret_cast<float*>(take((size_t)B * nsrc * HW * 16));
   ws.u0 = reinterpret_cast<float*>(take(B * 16 * HW2 * 4));
@@ -373,13 +373,13 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
       return hip_fail(e, "sweep: wta init");
     if ((e = hipMemsetAsync(ws.omega_stats[0], 0, ws.stats_bytes, stream)) != hipSuccess)
       return hip_fail(e, "sweep: stats init");
-    // NHWC copies of the features for the pipeline's 128-B tap gathers
+    // c8 copies of the features for the pipeline's LDS source boxes
     const int HW = a->H * a->W;
-    if ((e = launch_to_nhwc(a->ref_fea, ws.nhwc[0], a->B, HW, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: nhwc");
+    if ((e = launch_to_c8(a->ref_fea, ws.feat8[0], a->B, HW, stream)) != hipSuccess)
+      return hip_fail(e, "sweep: c8 copy");
     for (int v = 0; v < a->nsrc; ++v)
-      if ((e = launch_to_nhwc(a->src_fea[v], ws.nhwc[1 + v], a->B, HW, stream)) != hipSuccess)
-        return hip_fail(e, "sweep: nhwc");
+      if ((e = launch_to_c8(a->src_fea[v], ws.feat8[1 + v], a->B, HW, stream)) != hipSuccess)
+        return hip_fail(e, "sweep: c8 copy");
     if ((e = launch_cost_pipe(ca, g, ws, -1, 0, nullptr, stream)) != hipSuccess)
       return hip_fail(e, "sweep: cost pipeline prologue");
   }

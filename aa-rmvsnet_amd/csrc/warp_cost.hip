@@ -10,6 +10,9 @@
 // features plus two small statistics launches over the 16-B/px/view omega conv output.
 #include <hip/hip_runtime.h>
 
+#include <climits>
+#include <cstdlib>
+
 #include "device_common.h"
 
 namespace aarmvs {
@@ -22,10 +25,6 @@ namespace aarmvs {
 // FMA-contracted by its compiler: ix = fma(g + 1, size/2, -0.5).  This pair of
 // choices reproduces the reference's sampling positions bit for bit.
 // ---------------------------------------------------------------------------
-struct Proj12 {
-  float r[12];
-};
-
 __device__ __forceinline__ void sample_pos(const float* __restrict__ m, float depth, float x,
                                            float y, int H, int W, float& ix, float& iy) {
   float p[3];
@@ -78,9 +77,9 @@ __device__ __forceinline__ float bilinear(const float* __restrict__ plane, const
                    __fmaf_rn(v[2], t.wt[2], __fmaf_rn(v[1], t.wt[1], __fmul_rn(v[0], t.wt[0]))));
 }
 
-// Buffer-descriptor gathers for the streaming kernels: 32-bit byte offsets instead of
+// Buffer-descriptor loads for the streaming kernels: 32-bit byte offsets instead of
 // 64-bit addresses (VGPR pressure), and the hardware range check does the zero padding:
-// an out-of-range tap gets offset = num_records and loads 0.
+// an offset at or past num_records loads 0.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const float* base, uint32_t bytes) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
@@ -90,41 +89,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const float* base
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)n, 0x00020000);
 }
 
-struct BTaps {
-  uint32_t off[4];   // byte offset within one channel plane, or `oob`
-  float wt[4];
-};
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ BTaps make_btaps(float ix, float iy, int H, int W, uint32_t oob) {
-  BTaps t;
-  const float x0 = floorf(ix), y0 = floorf(iy);
-  const float wx = __fsub_rn(ix, x0), wy = __fsub_rn(iy, y0);
-  const float ex = __fsub_rn(1.0f, wx), sy = __fsub_rn(1.0f, wy);
-  t.wt[0] = __fmul_rn(sy, ex);
-  t.wt[1] = __fmul_rn(sy, wx);
-  t.wt[2] = __fmul_rn(wy, ex);
-  t.wt[3] = __fmul_rn(wy, wx);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float xf = x0 + (float)(k & 1), yf = y0 + (float)(k >> 1);
-    const bool ok = (xf > -1.0f) && (xf < (float)W) && (yf > -1.0f) && (yf < (float)H);
-    t.off[k] = ok ? (uint32_t)((int)yf * W + (int)xf) * 4u : oob;
-  }
-  return t;
-}
-
-// bilinear sample of channel plane at byte offset `coff` (same fma chain as bilinear())
-__device__ __forceinline__ float bilinear_b(__amdgpu_buffer_rsrc_t r, const BTaps& t, uint32_t coff) {
-  float v[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, t.off[k], coff, 0));
-  return __fmaf_rn(v[3], t.wt[3],
-                   __fmaf_rn(v[2], t.wt[2], __fmaf_rn(v[1], t.wt[1], __fmul_rn(v[0], t.wt[0]))));
-}
-
-__device__ __forceinline__ float load_b(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t coff) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, coff, 0));
+__device__ __forceinline__ float4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                     __uint_as_float(v.w));
 }
 
 // ---------------------------------------------------------------------------
@@ -199,15 +169,16 @@ hipError_t launch_homo_warp_bwd(const float* gout, const float* rel, const float
 // Cost-slice pipeline.
 //
 // The cost slice of plane d does not depend on the recurrence, so the sweep runs it
-// one plane ahead: launch P(d) = cost_pipe(prev = d, next = d + 1) does, per tile,
-//   prev part  x_d = -(sum_v (1 + w_v) (warp_v(d) - ref)^2) / nsrc, with w_v from the
-//              omega conv output t1_d and plane d's three GroupNorm statistics;
-//   next part  sq_v(d+1) = (warp_v(d+1) - ref)^2 on a haloed tile in LDS, the omega
-//              conv3x3 32->4 -> t1_{d+1} (16 B/px/view), GroupNorm #0 partial sums.
-// Both parts sample the same source neighbourhood (adjacent depths), so the second
-// gather of a (pixel, view) hits in L1/L2: the source features stream from HBM about
-// once per plane.  omega_stats<1>/<2> then complete plane d+1's GN #1/#2 statistics
-// from t1_{d+1} alone.
+// one plane ahead of the regulariser.  Per plane d it launches
+//   cost_x(d)          x_d = -(sum_v (1 + w_v) (warp_v(d) - ref)^2) / nsrc, with w_v from
+//                      the omega conv output t1_d and plane d's three GroupNorm statistics
+//                      (drmvsnet.py:307-319);
+//   omega_conv(d + 1)  sq_v(d+1) = (warp_v(d+1) - ref)^2 on a haloed tile in LDS, the
+//                      omega conv3x3 32->4 -> t1_{d+1} (16 B/px/view), GN #0 partial sums;
+//   omega_stats<1>/<2>(d + 1)  GN #1/#2 statistics from t1_{d+1} alone.
+// Both gather their bilinear taps straight from the "c8" feature copies
+// ([B][4][H][W][8], to_c8_kernel): one tap of one 8-channel chunk is a 32-B segment,
+// and neighbouring output pixels share taps in L1/L2.
 // ---------------------------------------------------------------------------
 struct PipeArgs {
   const float* ref;
@@ -226,6 +197,7 @@ struct PipeArgs {
   size_t off_ow0t, off_ow0, off_ob0, off_og0w, off_og0b, off_ow1, off_ob1, off_og1w, off_og1b, off_ow2,
       off_ob2, off_og2w, off_og2b, off_owo, off_obo;
   int B, H, W, nsrc;
+  int box_cap;                // LDS source-box capacity in pixels (diagnostic override, <= the kernel's)
   double* zero_ptr;           // omega_stats<1>: stale statistics to clear (or null)
   int zero_n;
 };
@@ -282,10 +254,7 @@ __device__ __forceinline__ void conv1x1_4(const float (&x)[4], const float* w, c
 
 // omega weight of one (pixel, view) from its conv3x3 output t and the three GN stats
 // (drmvsnet.py:30-35 after the first conv)
-__device__ __forceinline__ float omega_weight(const float4 q, const GnStat* gs, const PipeArgs& a,
-                                              const float* __restrict__ P) {
-  OmegaP o;
-  load_omega(a, P, o);
+__device__ __forceinline__ float omega_weight(const float4 q, const GnStat* gs, const OmegaP& o) {
   const float t[4] = {q.x, q.y, q.z, q.w};
   float aa[4], t2[4], bb[4], t3[4], g3[4];
   gn_relu4(t, gs[0], o.g0w, o.g0b, true, aa);
@@ -303,293 +272,378 @@ __device__ __forceinline__ size_t st_index(int b, int v, int k, int nsrc) {
   return (((size_t)b * nsrc + v) * 3 + k) * kSlots * 2;
 }
 
-// NHWC gathers: a tap of one pixel is 32 contiguous channels (128 B); lane k of an
-// 8-lane pixel group loads channels 4k..4k+3 with one dwordx4 (the per-CU address rate,
-// not HBM, limits dword gathers).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Tiles are 32 pixels wide, 8 rows (one thread per pixel).
+constexpr int kTileW = 32, kTileH = 8, kTileThreads = kTileW * kTileH;
+constexpr int kTileWaves = kTileThreads / 64;
+constexpr int kCHH = kTileH + 2, kCHW = kTileW + 2;   // omega_conv haloed tile
+constexpr int kCRing = 2 * kCHW + 2 * kTileH;         // its halo-only (ring) pixels
+constexpr int kSqStride = 12;   // floats per halo pixel in the sq tile (8 used): conflict-free b128
+constexpr int kCBoxPx = 448;    // omega_conv LDS source box: 32-B pixels (one chunk)
+static_assert(kCRing <= kTileThreads, "one ring pixel per thread at most");
 
-__device__ __forceinline__ float4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
-                     __uint_as_float(v.w));
+// XCD-aware tile order: blocks are dealt to the 8 XCDs round-robin, so XCD k takes the
+// k-th contiguous band of tiles and neighbouring tiles (which share source rows) share
+// its L2
+__device__ __forceinline__ int xcd_tile(int bid, int nb) {
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 }
 
-// byte offsets of the 4 taps (pixel * 128 B, or `oob`) + weights
-__device__ __forceinline__ BTaps make_ntaps(float ix, float iy, int H, int W, uint32_t oob) {
-  BTaps t = make_btaps(ix, iy, H, W, oob);
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (t.off[k] != oob) t.off[k] *= 32u;   // dword offset of the pixel * 4 B -> * 128 B
+// A sampling position reduced to what the taps need: the top-left tap's floor
+// coordinates and the four bilinear weights (make_taps' arithmetic).
+struct TapF {
+  float xf, yf;
+  float wt[4];
+};
+
+__device__ __forceinline__ TapF tap_f(const float* __restrict__ m, float dep, int x, int y, int H,
+                                      int W) {
+  float ix, iy;
+  sample_pos(m, dep, (float)x, (float)y, H, W, ix, iy);
+  TapF t;
+  t.xf = floorf(ix);
+  t.yf = floorf(iy);
+  const float wx = __fsub_rn(ix, t.xf), wy = __fsub_rn(iy, t.yf);
+  const float ex = __fsub_rn(1.0f, wx), sy = __fsub_rn(1.0f, wy);
+  t.wt[0] = __fmul_rn(sy, ex);
+  t.wt[1] = __fmul_rn(sy, wx);
+  t.wt[2] = __fmul_rn(wy, ex);
+  t.wt[3] = __fmul_rn(wy, wx);
   return t;
 }
 
-// bilinear sample of 4 channels (byte offset `coff` within the pixel), same fma chain
-__device__ __forceinline__ float4 bilinear4(__amdgpu_buffer_rsrc_t r, const BTaps& t, uint32_t coff) {
-  const float4 v0 = ld4(r, t.off[0] + coff), v1 = ld4(r, t.off[1] + coff);
-  const float4 v2 = ld4(r, t.off[2] + coff), v3 = ld4(r, t.off[3] + coff);
-  auto one = [&](float a0, float a1, float a2, float a3) {
-    return __fmaf_rn(a3, t.wt[3], __fmaf_rn(a2, t.wt[2], __fmaf_rn(a1, t.wt[1], __fmul_rn(a0, t.wt[0]))));
-  };
-  return make_float4(one(v0.x, v1.x, v2.x, v3.x), one(v0.y, v1.y, v2.y, v3.y),
-                     one(v0.z, v1.z, v2.z, v3.z), one(v0.w, v1.w, v2.w, v3.w));
+// Source box of a block: the bounding box of every in-image bilinear tap its threads
+// need.  Each thread extends (lx, ly, hx, hy) by its positions, then box_reduce()
+// combines the block (one barrier) and returns the box in wave-uniform registers.
+__device__ __forceinline__ void box_extend(const TapF& t, int H, int W, int& lx, int& ly, int& hx,
+                                           int& hy) {
+  if (!(t.xf == t.xf) || !(t.yf == t.yf)) return;   // NaN position: all taps read zero
+  const float xl = fmaxf(t.xf, 0.f), xh = fminf(t.xf + 1.f, (float)(W - 1));
+  const float yl = fmaxf(t.yf, 0.f), yh = fminf(t.yf + 1.f, (float)(H - 1));
+  if (xl <= xh && yl <= yh) {
+    lx = min(lx, (int)xl);
+    hx = max(hx, (int)xh);
+    ly = min(ly, (int)yl);
+    hy = max(hy, (int)yh);
+  }
 }
 
-struct RingTap {
-  BTaps t;
-  uint32_t qofs;   // reference pixel byte offset (or out of range)
-  int hidx;        // position in the halo tile
+struct Box {
+  int x0, y0, nx, ny;
 };
 
-constexpr int kPipeTW = 32;
-constexpr int kPipeThreads = 256;   // 32 pixel columns x 8 lanes
-constexpr int kSqStride = 36;       // floats per pixel in the LDS tile: conflict-free b128 reads
-
-template <int TH>
-struct PipeCfg {
-  static constexpr int HH = TH + 2, HW = kPipeTW + 2, NPIX = HH * HW;
-  static constexpr int RING = 2 * HW + 2 * TH;
-  static constexpr int PIX = TH * kPipeTW;
-  static constexpr int WAVES = kPipeThreads / 64;
-  static constexpr int SQ_FLOATS = NPIX * kSqStride;
-  static constexpr int WT_FLOATS = AARMVS_MAX_SRC * PIX;
-  static constexpr int LDS_FLOATS = SQ_FLOATS > WT_FLOATS ? SQ_FLOATS : WT_FLOATS;
-};
-
-// ABL: ablation bits for the diagnostic harness (tools/microbench/pipe_bench.cpp); the
-// library only instantiates ABL = 0.  1: no prev part, 2: no next-part own gathers,
-// 4: no ring gathers, 8: no conv.
-template <int TH, int ABL = 0>
-__global__ void __launch_bounds__(kPipeThreads) cost_pipe_kernel(PipeArgs a,
-                                                                 const float* __restrict__ P,
-                                                                 const float* __restrict__ Rel) {
-  using Cfg = PipeCfg<TH>;
-  // sq tile (next part) and the omega-weight table (prev part) share the LDS
-  __shared__ __attribute__((aligned(16))) float lds[Cfg::LDS_FLOATS];
-  __shared__ RingTap ring[Cfg::RING];
-  __shared__ float wsum[Cfg::WAVES][AARMVS_MAX_SRC][2];
-  __shared__ GnStat gs[AARMVS_MAX_SRC][3];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int col = tid >> 3, k = tid & 7;        // 8-lane pixel groups
-  const uint32_t koff = 16u * k;                // this lane's 4 channels within a pixel
-  const int b = blockIdx.y;
-  const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
-  const bool prev = a.d_prev >= 0 && !(ABL & 1), next = a.d_next >= 0;
-  for (int i = tid; i < Cfg::WAVES * AARMVS_MAX_SRC * 2; i += kPipeThreads)
-    (&wsum[0][0][0])[i] = 0.f;
-  if (prev && tid < 3 * nsrc) {
-    const int v = tid / 3, kk = tid % 3;
-    gs[v][kk] = stat_read(a.st_prev + st_index(b, v, kk, nsrc), 4.0 * HW);
+// red: LDS scratch [kTileWaves][4]; must not be read by anyone before the barrier here
+__device__ __forceinline__ Box box_reduce(int lx, int ly, int hx, int hy, int (*red)[4]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lx = min(lx, __shfl_xor(lx, o, 64));
+    ly = min(ly, __shfl_xor(ly, o, 64));
+    hx = max(hx, __shfl_xor(hx, o, 64));
+    hy = max(hy, __shfl_xor(hy, o, 64));
+  }
+  if (lane == 0) {
+    red[wave][0] = lx;
+    red[wave][1] = ly;
+    red[wave][2] = hx;
+    red[wave][3] = hy;
   }
   __syncthreads();
-  // parameters come through a __restrict__ argument so that their uniform loads can be
+#pragma unroll
+  for (int w = 0; w < kTileWaves; ++w) {
+    lx = min(lx, red[w][0]);
+    ly = min(ly, red[w][1]);
+    hx = max(hx, red[w][2]);
+    hy = max(hy, red[w][3]);
+  }
+  Box bx;
+  bx.x0 = __builtin_amdgcn_readfirstlane(lx);
+  bx.y0 = __builtin_amdgcn_readfirstlane(ly);
+  bx.nx = __builtin_amdgcn_readfirstlane(hx >= lx ? hx - lx + 1 : 0);
+  bx.ny = __builtin_amdgcn_readfirstlane(hy >= ly ? hy - ly + 1 : 0);
+  return bx;
+}
+
+// row of box pixel p: umulhi(p, ceil(2^32 / nx)), exact for p, nx < 2^16
+__device__ __forceinline__ uint32_t box_magic(int nx) {
+  return nx > 1 ? (uint32_t)((0x100000000ull + (uint64_t)nx - 1) / (uint64_t)nx) : 0u;
+}
+__device__ __forceinline__ int box_row(int p, int nx, uint32_t mg) {
+  return nx > 1 ? (int)__umulhi((uint32_t)p, mg) : p;
+}
+
+// The four taps of a position: pixel indices (into the LDS box, or image pixels for
+// the global path) and weights; out-of-image taps get `zpix` (the box's zero pixel, or
+// a pixel index whose byte offset lies past the buffer: loads 0).
+struct TapP {
+  uint32_t pix[4];
+  float wt[4];
+};
+
+__device__ __forceinline__ TapP tap_p(const TapF& t, bool valid, int H, int W, bool lds,
+                                      const Box& bx, uint32_t zpix) {
+  TapP o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    o.wt[k] = t.wt[k];
+    const float xf = t.xf + (float)(k & 1), yf = t.yf + (float)(k >> 1);
+    const bool ok = valid && (xf > -1.0f) && (xf < (float)W) && (yf > -1.0f) && (yf < (float)H);
+    const int xi = ok ? (int)xf : bx.x0, yi = ok ? (int)yf : bx.y0;
+    const uint32_t p = lds ? (uint32_t)((yi - bx.y0) * bx.nx + (xi - bx.x0)) : (uint32_t)(yi * W + xi);
+    o.pix[k] = ok ? p : zpix;
+  }
+  return o;
+}
+
+__device__ __forceinline__ float bil1(float v0, float v1, float v2, float v3, const TapP& t) {
+  return __fmaf_rn(v3, t.wt[3], __fmaf_rn(v2, t.wt[2], __fmaf_rn(v1, t.wt[1], __fmul_rn(v0, t.wt[0]))));
+}
+
+// the fma chain of bilinear() on 4 channels
+__device__ __forceinline__ float4 bil4(float4 v0, float4 v1, float4 v2, float4 v3, const TapP& t) {
+  return make_float4(bil1(v0.x, v1.x, v2.x, v3.x, t), bil1(v0.y, v1.y, v2.y, v3.y, t),
+                     bil1(v0.z, v1.z, v2.z, v3.z, t), bil1(v0.w, v1.w, v2.w, v3.w, t));
+}
+
+__device__ __forceinline__ float4 sqdiff4(float4 g, float4 r) {
+  const float dx = __fsub_rn(g.x, r.x), dy = __fsub_rn(g.y, r.y);
+  const float dz = __fsub_rn(g.z, r.z), dw = __fsub_rn(g.w, r.w);
+  return make_float4(__fmul_rn(dx, dx), __fmul_rn(dy, dy), __fmul_rn(dz, dz), __fmul_rn(dw, dw));
+}
+
+// 16-B slot s of c8 pixel p (chunk c = s >> 1, half h = s & 1) in global memory
+__device__ __forceinline__ float4 ld_c8(__amdgpu_buffer_rsrc_t r, uint32_t p, int s, int HW) {
+  return ld4(r, (uint32_t)(s >> 1) * (uint32_t)HW * 32u + p * 32u + 16u * (uint32_t)(s & 1));
+}
+
+// cost_x: x_d on an 4 x 32 tile, two lanes per reference pixel (lane h holds channels
+// 8c + 4h .. 8c + 4h + 3 of every chunk c), so that one wave-wide tap load covers 32
+// pixels x 32 B of a chunk image: contiguous 1-KiB requests.  The views are
+// accumulated in view order in registers.
+constexpr int kXRows = 4;
+__global__ void __launch_bounds__(kTileThreads) cost_x_kernel(PipeArgs a,
+                                                              const float* __restrict__ P,
+                                                              const float* __restrict__ Rel) {
+  __shared__ GnStat gs[AARMVS_MAX_SRC][3];
+  const int tid = threadIdx.x, b = blockIdx.y;
+  const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tiles_x = (W + kTileW - 1) / kTileW;
+  const int h = tid & 1, q = tid >> 1;
+  const int gy = (tile / tiles_x) * kXRows + q / kTileW, gx = (tile % tiles_x) * kTileW + q % kTileW;
+  if (tid < 3 * nsrc) {
+    const int v = tid / 3, k = tid % 3;
+    gs[v][k] = stat_read(a.st_prev + st_index(b, v, k, nsrc), 4.0 * HW);
+  }
+  __syncthreads();
+  if (gy >= H || gx >= W) return;
+  // parameters come through a __restrict__ argument so that their uniform loads are
   // scalar (s_load) despite the kernel's vector stores
+  OmegaP o;
+  load_omega(a, P, o);
+  const float dep = a.dvals[b * a.D + a.d_prev];
+  const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's c8 image
+  const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(a.ref + (size_t)b * kC * HW, fbytes);
+  const size_t p = (size_t)gy * W + gx;
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (int v = 0; v < nsrc; ++v) {
+    const float* __restrict__ m = Rel + 12 * (v * a.B + b);
+    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
+    const float w = omega_weight(a.t1_prev[((size_t)b * nsrc + v) * HW + p], gs[v], o);
+    const float wp1 = __fadd_rn(w, 1.0f);
+    if (a.omega_out && h == 0) a.omega_out[((size_t)v * a.B + b) * HW + p] = w;
+    const Box none{0, 0, 0, 0};
+    const TapP t = tap_p(tap_f(m, dep, gx, gy, H, W), true, H, W, false, none, fbytes / 32u);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int s = 2 * c + h;
+      const float4 g = bil4(ld_c8(rsrc, t.pix[0], s, HW), ld_c8(rsrc, t.pix[1], s, HW),
+                            ld_c8(rsrc, t.pix[2], s, HW), ld_c8(rsrc, t.pix[3], s, HW), t);
+      // x accumulation in view order (drmvsnet.py:311-316)
+      const float4 sq = sqdiff4(g, ld_c8(rref, (uint32_t)p, s, HW));
+      float* ac = &acc[4 * c];
+      ac[0] = __fadd_rn(ac[0], __fmul_rn(wp1, sq.x));
+      ac[1] = __fadd_rn(ac[1], __fmul_rn(wp1, sq.y));
+      ac[2] = __fadd_rn(ac[2], __fmul_rn(wp1, sq.z));
+      ac[3] = __fadd_rn(ac[3], __fmul_rn(wp1, sq.w));
+    }
+  }
+  float* xo = a.x + (size_t)b * kC * HW + p;   // NCHW
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      xo[(size_t)(8 * c + 4 * h + j) * HW] = -1.0f * __fdiv_rn(acc[4 * c + j], (float)nsrc);
+}
+
+// omega_conv LDS box: 32-B pixels (one chunk), the two 16-B halves of pixel p swapped
+// when bit 3 of p is set (16 consecutive pixels' reads of one half cover all banks)
+__device__ __forceinline__ float4 box32(const float* box, uint32_t p, int h) {
+  return *reinterpret_cast<const float4*>(box + p * 8u + (uint32_t)((h ^ (int)((p >> 3) & 1u)) << 2));
+}
+
+// omega_conv: t1 of plane d_next for one (tile, view) per block.  The squared difference
+// on the (8+2) x 34 haloed tile goes through LDS one 8-channel chunk at a time (own
+// pixel by every thread, ring pixels by threads 0..kCRing-1); each thread accumulates
+// its pixel's conv3x3 32->4 over the chunks.  The chunk's source box is staged in LDS
+// (the next chunk's box loads are in flight during the conv); a box past kCBoxPx
+// pixels is sampled from global memory.
+__global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
+                                                                  const float* __restrict__ P,
+                                                                  const float* __restrict__ Rel) {
+  constexpr int NPF = (2 * kCBoxPx + kTileThreads - 1) / kTileThreads;   // box items per thread
+  __shared__ __attribute__((aligned(16))) float box[(kCBoxPx + 1) * 8];
+  __shared__ __attribute__((aligned(16))) float sqt[kCHH * kCHW * kSqStride];
+  __shared__ int red[kTileWaves][4];
+  __shared__ float wsum[kTileWaves][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int v = blockIdx.y, b = blockIdx.z;
+  const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tiles_x = (W + kTileW - 1) / kTileW;
+  const int y0 = (tile / tiles_x) * kTileH, x0 = (tile % tiles_x) * kTileW;
+  const int ty = tid / kTileW, tx = tid % kTileW;
+  const int gy = y0 + ty, gx = x0 + tx;
+  const bool inside = gy < H && gx < W;
+  const int own_hp = (ty + 1) * kCHW + tx + 1;
+  // this thread's ring pixel
+  const bool has_ring = tid < kCRing;
+  int hy, hx;
+  if (tid < kCHW) {
+    hy = 0;
+    hx = tid;
+  } else if (tid < 2 * kCHW) {
+    hy = kCHH - 1;
+    hx = tid - kCHW;
+  } else if (tid < 2 * kCHW + kTileH) {
+    hy = 1 + tid - 2 * kCHW;
+    hx = 0;
+  } else {
+    hy = 1 + tid - 2 * kCHW - kTileH;
+    hx = kCHW - 1;
+  }
+  const int ry = y0 - 1 + hy, rx = x0 - 1 + hx;
+  const bool ring_in = has_ring && ry >= 0 && ry < H && rx >= 0 && rx < W;
+  const int ring_hp = hy * kCHW + hx;
+  if (tid < 8) box[kCBoxPx * 8 + tid] = 0.f;   // the zero pixel
+
+  const float dep = a.dvals[b * a.D + a.d_next];
+  const float* __restrict__ m = Rel + 12 * (v * a.B + b);
+  const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's c8 image
+  const uint32_t zg = fbytes / 32u;                          // a pixel index past the buffer
+  const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(a.ref + (size_t)b * kC * HW, fbytes);
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
+  // pixels outside the image read zeros everywhere: the conv's zero padding
+  const uint32_t own_px = inside ? (uint32_t)(gy * W + gx) : zg;
+  const uint32_t ring_px = ring_in ? (uint32_t)(ry * W + rx) : zg;
+  TapF tfo{}, tfr{};
+  int lx = INT_MAX, ly = INT_MAX, bhx = INT_MIN, bhy = INT_MIN;
+  if (inside) {
+    tfo = tap_f(m, dep, gx, gy, H, W);
+    box_extend(tfo, H, W, lx, ly, bhx, bhy);
+  }
+  if (ring_in) {
+    tfr = tap_f(m, dep, rx, ry, H, W);
+    box_extend(tfr, H, W, lx, ly, bhx, bhy);
+  }
+  const Box bx = box_reduce(lx, ly, bhx, bhy, red);
+  const bool lds = bx.nx * bx.ny <= min(kCBoxPx, a.box_cap);
+  const uint32_t zp = lds ? (uint32_t)kCBoxPx : zg;
+  const TapP to = tap_p(tfo, inside, H, W, lds, bx, zp), tr = tap_p(tfr, ring_in, H, W, lds, bx, zp);
+  const uint32_t mg = box_magic(bx.nx);
+  const int items = lds ? bx.nx * bx.ny * 2 : 0;
+  // box chunk c: item i = (pixel i >> 1, half i & 1); consecutive lanes read
+  // consecutive 16-B pieces of a box row
+  float4 pf[NPF];
+  auto box_load = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int i = tid + j * kTileThreads;
+      if (i < items) {
+        const int p = i >> 1, r = box_row(p, bx.nx, mg);
+        const uint32_t gp = (uint32_t)((bx.y0 + r) * W + bx.x0 + (p - r * bx.nx));
+        pf[j] = ld_c8(rsrc, gp, 2 * c + ((i & 1) ^ ((p >> 3) & 1)), HW);
+      }
+    }
+  };
+  auto box_store = [&]() {
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int i = tid + j * kTileThreads;
+      if (i < items) *reinterpret_cast<float4*>(&box[(i >> 1) * 8 + ((i & 1) << 2)]) = pf[j];
+    }
+  };
+  auto sample = [&](const TapP& t, int c, int h) {
+    if (lds) return bil4(box32(box, t.pix[0], h), box32(box, t.pix[1], h), box32(box, t.pix[2], h),
+                         box32(box, t.pix[3], h), t);
+    const int s = 2 * c + h;
+    return bil4(ld_c8(rsrc, t.pix[0], s, HW), ld_c8(rsrc, t.pix[1], s, HW),
+                ld_c8(rsrc, t.pix[2], s, HW), ld_c8(rsrc, t.pix[3], s, HW), t);
+  };
   const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]
   const float* __restrict__ b0 = P + a.off_ob0;
-  const float dprev = prev ? a.dvals[b * a.D + a.d_prev] : 0.f;
-  const float dnext = next ? a.dvals[b * a.D + a.d_next] : 0.f;
-  const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's [H,W,32] map
-  const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(a.ref + (size_t)b * kC * HW, fbytes);
-  const float inv_n = (float)nsrc;
-  const int tiles_x = (W + kPipeTW - 1) / kPipeTW;
-  const int tile = blockIdx.x;
-  const int y0 = (tile / tiles_x) * TH, x0 = (tile % tiles_x) * kPipeTW;
 
-  if (prev) {
-    // omega weights w_v of the tile's pixels (one pixel per thread) -> LDS; two views
-    // per step so that two t1 loads are in flight
-    float* wtab = lds;
-    for (int i = tid; i < Cfg::PIX; i += kPipeThreads) {
-      const int gy = y0 + i / kPipeTW, gx = x0 + i % kPipeTW;
-      const bool inside = gy < H && gx < W;
-      const size_t p = inside ? (size_t)gy * W + gx : 0;
-      for (int v = 0; v < nsrc; v += 2) {
-        const bool two = v + 1 < nsrc;
-        const float4 q0 = a.t1_prev[((size_t)b * nsrc + v) * HW + p];
-        const float4 q1 = two ? a.t1_prev[((size_t)b * nsrc + v + 1) * HW + p] : q0;
-        const float w0v = inside ? omega_weight(q0, gs[v], a, P) : 0.f;
-        wtab[v * Cfg::PIX + i] = __fadd_rn(w0v, 1.0f);
-        if (inside && a.omega_out) a.omega_out[((size_t)v * a.B + b) * HW + p] = w0v;
-        if (two) {
-          const float w1v = inside ? omega_weight(q1, gs[v + 1], a, P) : 0.f;
-          wtab[(v + 1) * Cfg::PIX + i] = __fadd_rn(w1v, 1.0f);
-          if (inside && a.omega_out) a.omega_out[((size_t)(v + 1) * a.B + b) * HW + p] = w1v;
-        }
-      }
+  box_load(0);
+  box_store();
+  __syncthreads();
+  float o4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *reinterpret_cast<float4*>(&sqt[own_hp * kSqStride + 4 * h]) =
+          sqdiff4(sample(to, c, h), ld_c8(rref, own_px, 2 * c + h, HW));
+      if (has_ring)
+        *reinterpret_cast<float4*>(&sqt[ring_hp * kSqStride + 4 * h]) =
+            sqdiff4(sample(tr, c, h), ld_c8(rref, ring_px, 2 * c + h, HW));
     }
-    __syncthreads();
-    // x = -(sum_v (1 + w_v) (warp_v - ref)^2) / nsrc, 4 channels per lane; RB rows and
-    // two views per step keep 2 x RB x 4 tap loads in flight (the view order of the
-    // accumulation is kept)
-    constexpr int RB = 2;
-    static_assert(TH % RB == 0, "rows per step must divide the tile height");
-    for (int r0 = 0; r0 < TH; r0 += RB) {
-      int gy[RB], gx = x0 + col, p[RB];
-      bool inside[RB];
-      float4 rf[RB], acc[RB];
-#pragma unroll
-      for (int j = 0; j < RB; ++j) {
-        gy[j] = y0 + r0 + j;
-        inside[j] = gy[j] < H && gx < W;
-        p[j] = gy[j] * W + gx;
-        rf[j] = ld4(rref, (inside[j] ? (uint32_t)p[j] * 128u : fbytes) + koff);
-        acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-      for (int v = 0; v < nsrc; v += 2) {
-        const int nv = v + 1 < nsrc ? 2 : 1;
-        float4 g[2][RB];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (u < nv) {
-            const __amdgpu_buffer_rsrc_t rsrc =
-                uniform_rsrc(a.src[v + u] + (size_t)b * kC * HW, fbytes);
-#pragma unroll
-            for (int j = 0; j < RB; ++j) {
-              float ix, iy;
-              sample_pos(Rel + 12 * ((v + u) * a.B + b), dprev, (float)gx, (float)gy[j], H, W,
-                         ix, iy);
-              const BTaps t = make_ntaps(ix, iy, H, W, fbytes);
-              g[u][j] = bilinear4(rsrc, t, koff);
-            }
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (u < nv) {
-#pragma unroll
-            for (int j = 0; j < RB; ++j) {
-              const float wp1 = wtab[(v + u) * Cfg::PIX + (r0 + j) * kPipeTW + col];
-              const float dx = __fsub_rn(g[u][j].x, rf[j].x), dy = __fsub_rn(g[u][j].y, rf[j].y);
-              const float dz = __fsub_rn(g[u][j].z, rf[j].z), dw = __fsub_rn(g[u][j].w, rf[j].w);
-              acc[j].x = __fadd_rn(acc[j].x, __fmul_rn(wp1, __fmul_rn(dx, dx)));
-              acc[j].y = __fadd_rn(acc[j].y, __fmul_rn(wp1, __fmul_rn(dy, dy)));
-              acc[j].z = __fadd_rn(acc[j].z, __fmul_rn(wp1, __fmul_rn(dz, dz)));
-              acc[j].w = __fadd_rn(acc[j].w, __fmul_rn(wp1, __fmul_rn(dw, dw)));
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < RB; ++j) {
-        if (inside[j]) {
-          float* xo = a.x + (size_t)b * kC * HW + (size_t)(4 * k) * HW + p[j];   // NCHW
-          xo[0] = -1.0f * __fdiv_rn(acc[j].x, inv_n);
-          xo[(size_t)HW] = -1.0f * __fdiv_rn(acc[j].y, inv_n);
-          xo[(size_t)2 * HW] = -1.0f * __fdiv_rn(acc[j].z, inv_n);
-          xo[(size_t)3 * HW] = -1.0f * __fdiv_rn(acc[j].w, inv_n);
-        }
-      }
-    }
-    __syncthreads();   // the weight table's LDS becomes the sq tile
-  }
-
-  if (next) {
-    float* sq = lds;
-    for (int v = 0; v < nsrc; ++v) {
-      const float* m = Rel + 12 * (v * a.B + b);
-      const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
-      if (tid < Cfg::RING) {
-        // taps of this thread's ring (halo-only) pixel, shared through LDS
-        int hy, hx;
-        if (tid < Cfg::HW) { hy = 0; hx = tid; }
-        else if (tid < 2 * Cfg::HW) { hy = TH + 1; hx = tid - Cfg::HW; }
-        else if (tid < 2 * Cfg::HW + TH) { hy = 1 + tid - 2 * Cfg::HW; hx = 0; }
-        else { hy = 1 + tid - 2 * Cfg::HW - TH; hx = Cfg::HW - 1; }
-        const int ry = y0 - 1 + hy, rx = x0 - 1 + hx;
-        RingTap rt;
-        rt.hidx = hy * Cfg::HW + hx;
-        if (ry >= 0 && ry < H && rx >= 0 && rx < W && !(ABL & 4)) {
-          float ix, iy;
-          sample_pos(m, dnext, (float)rx, (float)ry, H, W, ix, iy);
-          rt.t = make_ntaps(ix, iy, H, W, fbytes);
-          rt.qofs = (uint32_t)(ry * W + rx) * 128u;
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            rt.t.off[q] = fbytes;
-            rt.t.wt[q] = 0.f;
-          }
-          rt.qofs = fbytes;
-        }
-        ring[tid] = rt;
-      }
-      // own rows: squared difference at d_next -> LDS tile (zero outside the image)
-      for (int r = 0; r < TH; ++r) {
-        const int gy = y0 + r, gx = x0 + col;
-        const bool inside = gy < H && gx < W && !(ABL & 2);
-        float ix, iy;
-        sample_pos(m, dnext, (float)gx, (float)gy, H, W, ix, iy);
-        BTaps t = make_ntaps(ix, iy, H, W, fbytes);
-        if (!inside)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) t.off[q] = fbytes;
-        const float4 g = bilinear4(rsrc, t, koff);
-        const float4 rf = ld4(rref, (inside ? (uint32_t)(gy * W + gx) * 128u : fbytes) + koff);
-        const float dx = __fsub_rn(g.x, rf.x), dy = __fsub_rn(g.y, rf.y);
-        const float dz = __fsub_rn(g.z, rf.z), dw = __fsub_rn(g.w, rf.w);
-        *reinterpret_cast<float4*>(&sq[((r + 1) * Cfg::HW + col + 1) * kSqStride + 4 * k]) =
-            make_float4(__fmul_rn(dx, dx), __fmul_rn(dy, dy), __fmul_rn(dz, dz), __fmul_rn(dw, dw));
-      }
-      __syncthreads();   // ring tap table ready
-      for (int i = tid; i < Cfg::RING * 8; i += kPipeThreads) {
-        const RingTap& rt = ring[i >> 3];   // (i & 7) == k
-        const float4 g = bilinear4(rsrc, rt.t, koff);
-        const float4 rf = ld4(rref, rt.qofs + koff);
-        const float dx = __fsub_rn(g.x, rf.x), dy = __fsub_rn(g.y, rf.y);
-        const float dz = __fsub_rn(g.z, rf.z), dw = __fsub_rn(g.w, rf.w);
-        *reinterpret_cast<float4*>(&sq[rt.hidx * kSqStride + 4 * k]) =
-            make_float4(__fmul_rn(dx, dx), __fmul_rn(dy, dy), __fmul_rn(dz, dz), __fmul_rn(dw, dw));
-      }
-      __syncthreads();
-      // omega.reweight_network.0.0: conv3x3 32->4, pad 1; one output pixel per thread
-      float ps = 0.f, pss = 0.f;
-      for (int i = tid; i < Cfg::PIX; i += kPipeThreads) {
-        const int py = i / kPipeTW, px = i % kPipeTW;
-        float o4[4] = {0.f, 0.f, 0.f, 0.f};
-        if (!(ABL & 8)) {
+    __syncthreads();   // sq visible; this chunk's box reads are done
+    if (c < 3) box_load(c + 1);
+    // omega.reweight_network.0.0: conv3x3 32->4, pad 1 (input channels 8c..8c+7)
 #pragma unroll 1
-          for (int tap = 0; tap < 9; ++tap) {
-            const float4* s4 = reinterpret_cast<const float4*>(
-                &sq[((py + tap / 3) * Cfg::HW + px + tap % 3) * kSqStride]);
-#pragma unroll 2
-            for (int c4 = 0; c4 < 8; ++c4) {
-              const float4 q = s4[c4];
-              const float qq[4] = {q.x, q.y, q.z, q.w};
-              const float* wt = w0t + (tap * kC + 4 * c4) * 4;   // [j][co], contiguous
+    for (int tap = 0; tap < 9; ++tap) {
+      const float* s8 = &sqt[(own_hp + (tap / 3 - 1) * kCHW + (tap % 3 - 1)) * kSqStride];
+      const float4 qa = *reinterpret_cast<const float4*>(s8);
+      const float4 qb = *reinterpret_cast<const float4*>(s8 + 4);
+      const float qq[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+      const float* wt = w0t + (tap * kC + 8 * c) * 4;   // [j][co], contiguous
 #pragma unroll
-              for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 8; ++j)
 #pragma unroll
-                for (int co = 0; co < 4; ++co) o4[co] = fmaf(qq[j], wt[j * 4 + co], o4[co]);
-            }
-          }
-        }
-        const int gy = y0 + py, gx = x0 + px;
-        if (gy < H && gx < W) {
-          float4 out;
-          out.x = o4[0] + b0[0];
-          out.y = o4[1] + b0[1];
-          out.z = o4[2] + b0[2];
-          out.w = o4[3] + b0[3];
-          a.t1_next[((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
-          ps += (out.x + out.y) + (out.z + out.w);
-          pss += (out.x * out.x + out.y * out.y) + (out.z * out.z + out.w * out.w);
-        }
-      }
-      ps = wave_sum(ps);
-      pss = wave_sum(pss);
-      if (lane == 0) {
-        wsum[wave][v][0] = ps;
-        wsum[wave][v][1] = pss;
-      }
-      __syncthreads();   // sq and the ring table are rewritten for the next view
+        for (int co = 0; co < 4; ++co) o4[co] = fmaf(qq[j], wt[j * 4 + co], o4[co]);
     }
-    if (tid < nsrc) {
-      double s = 0.0, ss = 0.0;
-      for (int w = 0; w < Cfg::WAVES; ++w) {
-        s += wsum[w][tid][0];
-        ss += wsum[w][tid][1];
-      }
-      stat_add(a.st_next + st_index(b, tid, 0, nsrc), s, ss);
+    if (c < 3) {
+      box_store();
+      __syncthreads();   // next box visible; the conv's sq reads are done
     }
+  }
+  float ps = 0.f, pss = 0.f;
+  if (inside) {
+    float4 out;
+    out.x = o4[0] + b0[0];
+    out.y = o4[1] + b0[1];
+    out.z = o4[2] + b0[2];
+    out.w = o4[3] + b0[3];
+    a.t1_next[((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
+    ps = (out.x + out.y) + (out.z + out.w);
+    pss = (out.x * out.x + out.y * out.y) + (out.z * out.z + out.w * out.w);
+  }
+  ps = wave_sum(ps);
+  pss = wave_sum(pss);
+  if (lane == 0) {
+    wsum[wave][0] = ps;
+    wsum[wave][1] = pss;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int w = 0; w < kTileWaves; ++w) {
+      s0 += wsum[w][0];
+      s1 += wsum[w][1];
+    }
+    stat_add(a.st_next + st_index(b, v, 0, nsrc), s0, s1);
   }
 }
 
@@ -648,6 +702,7 @@ static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspac
   a.H = g.H;
   a.W = g.W;
   a.nsrc = g.nsrc;
+  a.box_cap = INT_MAX;
   a.off_ow0 = L.pk_off[P_OW0];
   a.off_ow0t = L.ow0t_off;
   a.off_ob0 = L.pk_off[P_OB0];
@@ -666,34 +721,45 @@ static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspac
   return a;
 }
 
-constexpr int kPipeTH = 8;
+// LDS source-box capacity override: AARMVS_PIPE_BOX_CAP=n (pixels) forces smaller boxes,
+// i.e. cost_x's region subdivision and omega_conv's global-gather fallback (a diagnostic
+// for the parity tests; results are bit-identical)
+static int pipe_box_cap() {
+  const char* s = std::getenv("AARMVS_PIPE_BOX_CAP");
+  return (s && *s) ? std::max(4, std::atoi(s)) : INT_MAX;
+}
 
 hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Workspace& ws,
                             int d_prev, int d_next, float* omega_out, hipStream_t s) {
   PipeArgs a = pipe_args(ca, g, ws);
-  // the pipeline gathers from the NHWC copies of the features in the workspace
-  a.ref = ws.nhwc[0];
-  for (int v = 0; v < g.nsrc; ++v) a.src[v] = ws.nhwc[1 + v];
+  a.box_cap = pipe_box_cap();
+  // the pipeline reads the c8 copies of the features in the workspace
+  a.ref = ws.feat8[0];
+  for (int v = 0; v < g.nsrc; ++v) a.src[v] = ws.feat8[1 + v];
   a.d_prev = d_prev;
   a.d_next = d_next;
+  hipError_t e;
+  const int tiles_x = (g.W + kTileW - 1) / kTileW;
   if (d_prev >= 0) {
     a.t1_prev = reinterpret_cast<const float4*>(ws.t1[d_prev & 1]);
     a.st_prev = ws.omega_stats[d_prev & 1];
+    a.omega_out = omega_out;
+    const int ntiles = tiles_x * ((g.H + kXRows - 1) / kXRows);
+    ProfScope ps(s, K_COST_X);
+    hipLaunchKernelGGL(cost_x_kernel, dim3(ntiles, g.B), dim3(kTileThreads), 0, s, a, a.params,
+                       a.rel);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  if (d_next >= 0) {
-    a.t1_next = reinterpret_cast<float4*>(ws.t1[d_next & 1]);
-    a.st_next = ws.omega_stats[d_next & 1];
-  }
-  a.omega_out = omega_out;
-  const int ntiles = ((g.W + kPipeTW - 1) / kPipeTW) * ((g.H + kPipeTH - 1) / kPipeTH);
-  hipError_t e;
-  {
-    ProfScope ps(s, K_COST_PIPE);
-    hipLaunchKernelGGL(cost_pipe_kernel<kPipeTH>, dim3(ntiles, g.B), dim3(kPipeThreads), 0, s, a,
-                       a.params, a.rel);
-  }
-  if ((e = hipGetLastError()) != hipSuccess) return e;
   if (d_next < 0) return hipSuccess;
+  a.t1_next = reinterpret_cast<float4*>(ws.t1[d_next & 1]);
+  a.st_next = ws.omega_stats[d_next & 1];
+  {
+    const int ntiles = tiles_x * ((g.H + kTileH - 1) / kTileH);
+    ProfScope ps(s, K_OMEGA_CONV);
+    hipLaunchKernelGGL(omega_conv_kernel, dim3(ntiles, g.nsrc, g.B), dim3(kTileThreads), 0, s, a,
+                       a.params, a.rel);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   // GN #1 / #2 statistics of plane d_next; stage 1 clears plane d_prev's statistics
   if (d_prev >= 0) {
     a.zero_ptr = ws.omega_stats[d_prev & 1];
@@ -714,14 +780,14 @@ hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Worksp
   return hipGetLastError();
 }
 
-// NCHW [B][32][HW] -> NHWC [B][HW][32] (once per sweep, so that a bilinear tap is one
-// 128-B line).  64 pixels per block through LDS: coalesced reads and 16-B writes.
-__global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* __restrict__ src,
-                                                           float* __restrict__ dst, int HW) {
+// NCHW [B][32][HW] -> c8 [B][4][HW][8] (once per sweep): four 8-channel chunk images of
+// 32-B pixels.  64 pixels per block through LDS: coalesced reads and 16-B writes.
+__global__ void __launch_bounds__(256) nchw_to_c8_kernel(const float* __restrict__ src,
+                                                         float* __restrict__ dst, int HW) {
   __shared__ float t[kC][65];
   const int b = blockIdx.y, p0 = blockIdx.x * 64;
   const float* s = src + (size_t)b * kC * HW;
-  float* d = dst + (size_t)b * kC * HW;
+  float4* d = reinterpret_cast<float4*>(dst + (size_t)b * kC * HW);
   const int px = threadIdx.x & 63;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -731,16 +797,17 @@ __global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* __restri
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int idx = threadIdx.x + 256 * j, q = idx >> 3, c4 = idx & 7;
+    const int idx = threadIdx.x + 256 * j, ch = idx >> 7, q = (idx & 127) >> 1, h = idx & 1;
+    const int c0 = 8 * ch + 4 * h;
     if (p0 + q < HW)
-      reinterpret_cast<float4*>(d)[(size_t)(p0 + q) * 8 + c4] =
-          make_float4(t[4 * c4][q], t[4 * c4 + 1][q], t[4 * c4 + 2][q], t[4 * c4 + 3][q]);
+      d[((size_t)ch * HW + p0 + q) * 2 + h] =
+          make_float4(t[c0][q], t[c0 + 1][q], t[c0 + 2][q], t[c0 + 3][q]);
   }
 }
 
-hipError_t launch_to_nhwc(const float* src, float* dst, int B, int HW, hipStream_t s) {
-  ProfScope ps(s, K_TO_NHWC);
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3((HW + 63) / 64, B), dim3(256), 0, s, src, dst, HW);
+hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s) {
+  ProfScope ps(s, K_TO_C8);
+  hipLaunchKernelGGL(nchw_to_c8_kernel, dim3((HW + 63) / 64, B), dim3(256), 0, s, src, dst, HW);
   return hipGetLastError();
 }
 

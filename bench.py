@@ -65,9 +65,10 @@ def algorithmic_work(name: str, B: int, N: int, H: int, W: int, launches_per_pla
     """(kind, amount per launch) of a sweep kernel; kind 'bytes' (HBM) or 'flops' (MFMA).
 
     Per-unit figures:
-      cost_pipe    128*(N+1) B per hypothesis: ref + N-1 source features read once,
-                   the 32-ch cost slice written once (fp32) -- one plane's cost slice
-                   per launch (the launch also produces the next plane's omega conv);
+      cost_x       128*(N+1) B per hypothesis: ref + N-1 source features read once,
+                   the 32-ch cost slice written once (fp32);
+      omega_conv   128*N + 16*(N-1) B per hypothesis: ref + N-1 source features read
+                   once, the 4-ch omega conv output written once per source view;
       omega_stats  16*(N-1) B per hypothesis (the omega conv output, 4 ch per view);
       lstm_cell k  2*9*Cin*Cout FLOP per cell pixel;
       deconv       2*16*16*9 FLOP per deconv input pixel (each input pixel meets the 3x3 kernel once);
@@ -75,8 +76,10 @@ def algorithmic_work(name: str, B: int, N: int, H: int, W: int, launches_per_pla
     """
     HW = H * W
     nsrc = N - 1
-    if name == "cost_pipe":
+    if name == "cost_x":
         return "bytes", 128.0 * (N + 1) * B * HW / launches_per_plane
+    if name == "omega_conv":
+        return "bytes", (128.0 * N + 16.0 * nsrc) * B * HW / launches_per_plane
     if name in ("omega_stats1", "omega_stats2"):
         return "bytes", 16.0 * nsrc * B * HW / launches_per_plane
     if name.startswith("lstm_cell"):
@@ -216,7 +219,7 @@ def main():
                         per_launch=r["per_launch"], avg_us=r["avg_us"])
         # the warp + aggregation path as a whole (every launch that produces the cost
         # slice): 128*(N+1) algorithmic B/hyp over the summed device time of its kernels
-        group = [k for k in ("cost_pipe", "omega_stats1", "omega_stats2") if k in prof]
+        group = [k for k in ("cost_x", "omega_conv", "omega_stats1", "omega_stats2") if k in prof]
         if group:
             ms = sum(prof[k][1] for k in group)
             planes = D * args.steps

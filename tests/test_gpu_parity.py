@@ -156,3 +156,23 @@ def test_rejects_cpu_tensors_and_bad_shapes():
     y = torch.zeros(1, 32, 18, 16, device=DEV)
     with pytest.raises(AarmvsError):
         sw(y, [y], proj, [proj], torch.ones(1, 2))
+
+
+
+@pytest.mark.parametrize("cap", ["4", "96"])
+def test_pipeline_box_fallbacks_are_bit_identical(monkeypatch, cap):
+    """AARMVS_PIPE_BOX_CAP shrinks omega_conv's LDS source boxes, sending (tile, view)
+    blocks to the global-gather path.  The arithmetic is the same, so the sweep must be
+    bit-identical."""
+    B, N, H, W, D = 1, 4, 64, 96, 4
+    sc = syn.scene(B, N, H, W, D, seed=5)
+    feats = torch.from_numpy(sc["features"]).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    sw = _sweep_obj(2)
+    args = (feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+            [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]))
+    a = sw(*args, want_cost=True, debug=True)
+    monkeypatch.setenv("AARMVS_PIPE_BOX_CAP", cap)
+    b = sw(*args, want_cost=True, debug=True)
+    for k in ("cost", "slice", "omega", "depth", "conf"):
+        assert torch.equal(a[k], b[k]), k

@@ -1,5 +1,6 @@
 #!/bin/bash
-# tests + headline bench (kernel timing on)
+# tests + pipeline microbench + headline bench (kernel timing on)
 source tools/gpu_round.sh
-run pytest_gpu 900 python -m pytest tests -m gpu -q -x
-run bench_hl 900 python bench.py --steps 2 --warmup 1 --no-cpu
+run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+run pipe_bench 120 ./tools/microbench/pipe_bench
+run bench_hl 600 python bench.py --steps 2 --warmup 1 --no-cpu

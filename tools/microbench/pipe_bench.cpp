@@ -1,6 +1,7 @@
-// Diagnostic harness: times cost_pipe_kernel ablations at the headline geometry
-// (1600x1184, 6 source views).  Includes the kernel source; links libaarmvs.so for the
-// parameter layout / workspace carve.  Not shipped; numbers are for design decisions.
+// Diagnostic harness: times the cost-slice pipeline kernels (cost_x, omega_conv) at the
+// headline geometry (1600x1184, 6 source views).  Includes the kernel source; links
+// libaarmvs.so for the parameter layout / workspace carve.  Not shipped; numbers are
+// for design decisions.
 #include "../../aa-rmvsnet_amd/csrc/warp_cost.hip"
 
 #include <cstdio>
@@ -56,45 +57,38 @@ int main(int argc, char** argv) {
   ca.ref = feats[0];
   for (int v = 0; v < nsrc; ++v) ca.src[v] = feats[v + 1];
   ca.rel = drel; ca.depth_values = ddv; ca.params = dpar;
-  CK(launch_to_nhwc(feats[0], ws.nhwc[0], B, (int)HW, 0));
-  for (int v = 0; v < nsrc; ++v) CK(launch_to_nhwc(feats[v + 1], ws.nhwc[v + 1], B, (int)HW, 0));
+  CK(launch_to_c8(feats[0], ws.feat8[0], B, (int)HW, 0));
+  for (int v = 0; v < nsrc; ++v) CK(launch_to_c8(feats[v + 1], ws.feat8[v + 1], B, (int)HW, 0));
   CK(launch_cost_pipe(ca, g, ws, -1, 0, nullptr, 0));
   CK(hipDeviceSynchronize());
-  PipeArgs a = pipe_args(ca, g, ws);
-  a.d_prev = 0; a.d_next = 1;
-  a.ref = ws.nhwc[0];
-  for (int v = 0; v < nsrc; ++v) a.src[v] = ws.nhwc[v + 1];
-  a.t1_prev = reinterpret_cast<const float4*>(ws.t1[0]); a.st_prev = ws.omega_stats[0];
-  a.t1_next = reinterpret_cast<float4*>(ws.t1[1]); a.st_next = ws.omega_stats[1];
+  PipeArgs a0 = pipe_args(ca, g, ws);
+  a0.d_prev = 0; a0.d_next = 1;
+  a0.ref = ws.feat8[0];
+  for (int v = 0; v < nsrc; ++v) a0.src[v] = ws.feat8[v + 1];
+  a0.t1_prev = reinterpret_cast<const float4*>(ws.t1[0]); a0.st_prev = ws.omega_stats[0];
+  a0.t1_next = reinterpret_cast<float4*>(ws.t1[1]); a0.st_next = ws.omega_stats[1];
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  const int ntiles = ((W + 31) / 32) * ((H + 7) / 8);
-  auto run = [&](const char* name, auto kern, int blocks) {
-    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, dim3(blocks, B), dim3(256), 0, 0, a, dpar, drel);
+  const int tiles_x = (W + kTileW - 1) / kTileW;
+  auto run = [&](const char* name, auto kern, dim3 grid, int threads, double bytes) {
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, grid, dim3(threads), 0, 0, a0, dpar, drel);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
     const int R = 10;
-    for (int i = 0; i < R; ++i) hipLaunchKernelGGL(kern, dim3(blocks, B), dim3(256), 0, 0, a, dpar, drel);
+    for (int i = 0; i < R; ++i) hipLaunchKernelGGL(kern, grid, dim3(threads), 0, 0, a0, dpar, drel);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-    printf("%-44s blocks %5d  %8.3f ms\n", name, blocks, ms / R);
+    printf("%-36s %8.3f ms  %7.0f GB/s algorithmic\n", name, ms / R, bytes / (ms / R) / 1e6);
   };
-  run("full", cost_pipe_kernel<8, 0>, ntiles);
-  const int ntiles4 = ((W + 31) / 32) * ((H + 3) / 4);
-  run("full TH4", cost_pipe_kernel<4, 0>, ntiles4);
-  run("no prev part (1)", cost_pipe_kernel<8, 1>, ntiles);
-  run("no next own gathers (2)", cost_pipe_kernel<8, 2>, ntiles);
-  run("no ring gathers (4)", cost_pipe_kernel<8, 4>, ntiles);
-  run("no conv (8)", cost_pipe_kernel<8, 8>, ntiles);
-  run("only prev part (2|4|8)", cost_pipe_kernel<8, 14>, ntiles);
-  run("only next part gathers (1|8)", cost_pipe_kernel<8, 9>, ntiles);
-  run("nothing but launch/ring/conv-free (1|2|4|8)", cost_pipe_kernel<8, 15>, ntiles);
+  run("cost_x", cost_x_kernel, dim3(tiles_x * ((H + kXRows - 1) / kXRows), B), kTileThreads,
+      128.0 * (nsrc + 2) * HW);
+  run("omega_conv", omega_conv_kernel, dim3(tiles_x * ((H + kTileH - 1) / kTileH), nsrc, B),
+      kTileThreads, (128.0 * (nsrc + 1) + 16.0 * nsrc) * HW);
   {
-    // NHWC transpose of one view
     CK(hipEventRecord(e0));
-    for (int i = 0; i < 10; ++i) CK(launch_to_nhwc(feats[0], ws.nhwc[0], B, (int)HW, 0));
+    for (int i = 0; i < 10; ++i) CK(launch_to_c8(feats[0], ws.feat8[0], B, (int)HW, 0));
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-    printf("%-44s %8.3f ms (%.0f GB/s)\n", "to_nhwc one view", ms / 10, 2.0 * fn * 4 / (ms / 10) / 1e6);
+    printf("%-36s %8.3f ms (%.0f GB/s)\n", "to_c8 one view", ms / 10, 2.0 * fn * 4 / (ms / 10) / 1e6);
   }
   CK(hipGetLastError());
   return 0;
