@@ -490,6 +490,10 @@ __device__ __forceinline__ float4 box32(const float* box, uint32_t p, int h) {
 // its pixel's conv3x3 32->4 over the chunks.  The chunk's source box is staged in LDS
 // (the next chunk's box loads are in flight during the conv); a box past kCBoxPx
 // pixels is sampled from global memory.
+// ABL: ablation bits for the diagnostic harness only (tools/microbench/pipe_bench.cpp;
+// the library instantiates ABL = 0): 1 no conv FMAs, 2 no squared differences, 4 no box
+// loads.
+template <int ABL = 0>
 __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
                                                                   const float* __restrict__ P,
                                                                   const float* __restrict__ Rel) {
@@ -553,7 +557,7 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
   const uint32_t zp = lds ? (uint32_t)kCBoxPx : zg;
   const TapP to = tap_p(tfo, inside, H, W, lds, bx, zp), tr = tap_p(tfr, ring_in, H, W, lds, bx, zp);
   const uint32_t mg = box_magic(bx.nx);
-  const int items = lds ? bx.nx * bx.ny * 2 : 0;
+  const int items = (lds && !(ABL & 4)) ? bx.nx * bx.ny * 2 : 0;
   // box chunk c: item i = (pixel i >> 1, half i & 1); consecutive lanes read
   // consecutive 16-B pieces of a box row
   float4 pf[NPF];
@@ -592,7 +596,7 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < 2 && !(ABL & 2); ++h) {
       *reinterpret_cast<float4*>(&sqt[own_hp * kSqStride + 4 * h]) =
           sqdiff4(sample(to, c, h), ld_c8(rref, own_px, 2 * c + h, HW));
       if (has_ring)
@@ -603,7 +607,7 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
     if (c < 3) box_load(c + 1);
     // omega.reweight_network.0.0: conv3x3 32->4, pad 1 (input channels 8c..8c+7)
 #pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
+    for (int tap = 0; tap < ((ABL & 1) ? 0 : 9); ++tap) {
       const float* s8 = &sqt[(own_hp + (tap / 3 - 1) * kCHW + (tap % 3 - 1)) * kSqStride];
       const float4 qa = *reinterpret_cast<const float4*>(s8);
       const float4 qb = *reinterpret_cast<const float4*>(s8 + 4);
@@ -756,7 +760,7 @@ hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Worksp
   {
     const int ntiles = tiles_x * ((g.H + kTileH - 1) / kTileH);
     ProfScope ps(s, K_OMEGA_CONV);
-    hipLaunchKernelGGL(omega_conv_kernel, dim3(ntiles, g.nsrc, g.B), dim3(kTileThreads), 0, s, a,
+    hipLaunchKernelGGL(omega_conv_kernel<0>, dim3(ntiles, g.nsrc, g.B), dim3(kTileThreads), 0, s, a,
                        a.params, a.rel);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
