@@ -57,12 +57,14 @@ struct CellDef<0> {   // [x, h0] @ H
   static constexpr int NP = 2, CH[kMaxParts] = {32, 16, 0};
   static constexpr int MODE[kMaxParts] = {SRC_PLAIN, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16, TH = 4, NT = 1;
+  static constexpr int H3RW = 1, H3WAVES = 8;
 };
 template <>
 struct CellDef<1> {   // [maxpool(h0'), h1] @ H/2
   static constexpr int NP = 2, CH[kMaxParts] = {16, 16, 0};
   static constexpr int MODE[kMaxParts] = {SRC_POOL, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16, TH = 8, NT = 1;
+  static constexpr int H3RW = 1, H3WAVES = 8;
 };
 template <>
 struct CellDef<2> : CellDef<1> {};   // [maxpool(h1'), h2] @ H/4
@@ -71,12 +73,14 @@ struct CellDef<3> {   // [gnrelu(u0), h1', h3] @ H/2
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 16};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16, TH = 4, NT = 1;
+  static constexpr int H3RW = 1, H3WAVES = 8;
 };
 template <>
 struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 8};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 8, TH = 8, NT = 1;
+  static constexpr int H3RW = 1, H3WAVES = 8;
 };
 
 template <int KIND>
@@ -431,13 +435,16 @@ static hipError_t run_cell(const CellArgs& a, int cu, int kid, hipStream_t s) {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
-template <int KIND>
+// RW: rows (32-pixel n-tiles) per wave -- the A (weight) fragments of a tap are reused
+// RW times; WAVES: waves per block.  Defaults per cell in CellDef.
+template <int KIND, int RW_ = CellDef<KIND>::H3RW, int WAVES_ = CellDef<KIND>::H3WAVES>
 struct H3Cfg {
   using D = CellDef<KIND>;
   static constexpr int CIN = D::CH[0] + D::CH[1] + D::CH[2];
   static constexpr int NCHK = (CIN + 15) / 16;
   static constexpr int HID = D::HID, MT = HID / 8, COUT = 4 * HID;
-  static constexpr int TH = 8, THREADS = TH * 64, TW = 32, W2 = TW + 2, TROWS = TH + 2;
+  static constexpr int RW = RW_, WAVES = WAVES_;
+  static constexpr int TH = RW * WAVES, THREADS = WAVES * 64, TW = 32, W2 = TW + 2, TROWS = TH + 2;
   static constexpr int NPIX = TROWS * W2;
   static constexpr int A_HALVES = NCHK * 9 * MT * 64 * 8;   // per hi / lo
   static constexpr int SEGS = TW / 4;
@@ -467,9 +474,9 @@ __device__ __forceinline__ uint32_t h3_split2(float a, float b, uint32_t& lo_bit
   return __builtin_bit_cast(uint32_t, hi);
 }
 
-template <int KIND>
+template <int KIND, int RW, int WAVES>
 struct H3Stager {
-  using C = H3Cfg<KIND>;
+  using C = H3Cfg<KIND, RW, WAVES>;
   using D = typename C::D;
   float4 seg[C::NS][2][4];   // [item][channel of the pair][POOL window]
   float halo[C::NH][2][4];
@@ -611,36 +618,41 @@ struct H3Stager {
   }
 };
 
-template <int KIND, int CH>
-__device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[H3Cfg<KIND>::MT],
-                                              const char* wl_hi, const char* wl_lo,
-                                              const char* in_hi, const char* in_lo, int wave,
-                                              int lane) {
-  using C = H3Cfg<KIND>;
-  constexpr int MT = C::MT;
+template <class C, int CH>
+__device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], const char* wl_hi,
+                                              const char* wl_lo, const char* in_hi,
+                                              const char* in_lo, int wave, int lane) {
+  constexpr int MT = C::MT, RW = C::RW;
   const int col = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
-    const int p = (wave + tap / 3) * C::W2 + col + tap % 3;
-    const int boff = h3_pix(p, h);
-    const half8 bh = *reinterpret_cast<const half8*>(in_hi + boff);
-    const half8 bl = *reinterpret_cast<const half8*>(in_lo + boff);
+    half8 bh[RW], bl[RW];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const int p = (wave * RW + r + tap / 3) * C::W2 + col + tap % 3;
+      const int boff = h3_pix(p, h);
+      bh[r] = *reinterpret_cast<const half8*>(in_hi + boff);
+      bl[r] = *reinterpret_cast<const half8*>(in_lo + boff);
+    }
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int aoff = ((((CH * 9 + tap) * MT + m) * 64) + lane) * 16;
       const half8 ah = *reinterpret_cast<const half8*>(wl_hi + aoff);
       const half8 al = *reinterpret_cast<const half8*>(wl_lo + aoff);
-      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[m], 0, 0, 0);
-      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[m], 0, 0, 0);
-      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[m], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[r], acc[m][r], 0, 0, 0);
+        acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[r], acc[m][r], 0, 0, 0);
+        acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[r], acc[m][r], 0, 0, 0);
+      }
     }
   }
 }
 
-template <int KIND>
-__global__ void __launch_bounds__(H3Cfg<KIND>::THREADS) lstm_cell_h3_kernel(
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES>
+__global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
-  using C = H3Cfg<KIND>;
+  using C = H3Cfg<KIND, RW, WAVES>;
   using D = typename C::D;
   constexpr int MT = C::MT, HID = C::HID, NCHK = C::NCHK;
   extern __shared__ __attribute__((aligned(16))) char lds_h3[];
@@ -679,7 +691,7 @@ __global__ void __launch_bounds__(H3Cfg<KIND>::THREADS) lstm_cell_h3_kernel(
     y0 = (rem / tiles_x) * C::TH;
     x0 = (rem % tiles_x) * C::TW;
   };
-  H3Stager<KIND> st;
+  H3Stager<KIND, RW, WAVES> st;
   int tile = blockIdx.x;
   if (tile < ntiles) {
     int b, y0, x0;
@@ -693,13 +705,15 @@ __global__ void __launch_bounds__(H3Cfg<KIND>::THREADS) lstm_cell_h3_kernel(
     const int next = tile + (int)gridDim.x;
     int nb = 0, ny0 = 0, nx0 = 0;
     if (next < ntiles) coords(next, nb, ny0, nx0);
-    const int y = y0 + wave;
-    floatx16 acc[MT];
+    const int yw = y0 + wave * RW;   // this wave's first row
+    floatx16 acc[MT][RW];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) acc[m][j] = 0.0f;
-    float cst[MT][4];
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[m][r][j] = 0.0f;
+    float cst[MT][RW][4];
     // chunk loop, fully unrolled so that every chunk's staging mode is compile-time
     auto chunk = [&](auto CHc) {
       constexpr int CH = decltype(CHc)::value;
@@ -715,12 +729,14 @@ __global__ void __launch_bounds__(H3Cfg<KIND>::THREADS) lstm_cell_h3_kernel(
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int x = x0 + col, ch = m * 8 + 4 * hi + q;
-            cst[m][q] = (y < H && x < W) ? a.c[(((size_t)b * HID + ch) * H + y) * W + x] : 0.f;
-          }
+          for (int r = 0; r < RW; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int x = x0 + col, y = yw + r, ch = m * 8 + 4 * hi + q;
+              cst[m][r][q] = (y < H && x < W) ? a.c[(((size_t)b * HID + ch) * H + y) * W + x] : 0.f;
+            }
       }
-      h3_mfma_chunk<KIND, CH>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
+      h3_mfma_chunk<C, CH>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
     };
     chunk(std::integral_constant<int, 0>{});
     if constexpr (NCHK > 1) chunk(std::integral_constant<int, 1>{});
@@ -728,35 +744,39 @@ __global__ void __launch_bounds__(H3Cfg<KIND>::THREADS) lstm_cell_h3_kernel(
 
     // epilogue: LSTM gates (module.py:83-90); undo the weight scale, add the bias
     const int x = x0 + col;
-    if (y < H && x < W) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
+    for (int r = 0; r < RW; ++r) {
+      const int y = yw + r;
+      if (y < H && x < W) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int ch = m * 8 + 4 * hi + q;
-          const float gi = fmaf(acc[m][q], inv_scale, a.bias[ch]);
-          const float gf = fmaf(acc[m][4 + q], inv_scale, a.bias[HID + ch]);
-          const float go = fmaf(acc[m][8 + q], inv_scale, a.bias[2 * HID + ch]);
-          const float gg = fmaf(acc[m][12 + q], inv_scale, a.bias[3 * HID + ch]);
-          const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
-          const float cn = fast_sigmoid(gf) * cst[m][q] + fast_sigmoid(gi) * fast_tanh(gg);
-          a.c[idx] = cn;
-          a.h_new[idx] = fast_sigmoid(go) * fast_tanh(cn);
+        for (int m = 0; m < MT; ++m) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int ch = m * 8 + 4 * hi + q;
+            const float gi = fmaf(acc[m][r][q], inv_scale, a.bias[ch]);
+            const float gf = fmaf(acc[m][r][4 + q], inv_scale, a.bias[HID + ch]);
+            const float go = fmaf(acc[m][r][8 + q], inv_scale, a.bias[2 * HID + ch]);
+            const float gg = fmaf(acc[m][r][12 + q], inv_scale, a.bias[3 * HID + ch]);
+            const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
+            const float cn = fast_sigmoid(gf) * cst[m][r][q] + fast_sigmoid(gi) * fast_tanh(gg);
+            a.c[idx] = cn;
+            a.h_new[idx] = fast_sigmoid(go) * fast_tanh(cn);
+          }
         }
       }
     }
   }
 }
 
-template <int KIND>
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES>
 static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu, int kid,
                               hipStream_t s) {
-  using C = H3Cfg<KIND>;
+  using C = H3Cfg<KIND, RW, WAVES>;
   static_assert(C::LDS_BYTES <= 160 * 1024, "h3 cell tile exceeds LDS");
   static_assert(C::NS <= 32 && C::NH <= 32, "staging masks hold 32 items");
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_h3_kernel<KIND>,
+    hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_h3_kernel<KIND, RW, WAVES>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)C::LDS_BYTES);
     if (e != hipSuccess) return e;
@@ -766,8 +786,8 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
   const int per_cu = std::max(1, (int)((160 * 1024) / C::LDS_BYTES));
   const int grid = std::max(1, std::min(ntiles, cu * per_cu));
   ProfScope ps(s, kid);
-  hipLaunchKernelGGL(lstm_cell_h3_kernel<KIND>, dim3(grid), dim3(C::THREADS), C::LDS_BYTES, s, a,
-                     inv_scale);
+  hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES>), dim3(grid), dim3(C::THREADS),
+                     C::LDS_BYTES, s, a, inv_scale);
   return hipGetLastError();
 }
 

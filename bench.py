@@ -165,6 +165,9 @@ def main():
     ap.add_argument("--cpu-planes", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--planes", type=int, default=0,
+                    help="profiling aid: sweep only the first P depth planes (0 = all D); "
+                         "per-launch figures are unchanged, the headline value is not comparable")
     args = ap.parse_args()
 
     rank, local, world = env()
@@ -172,7 +175,9 @@ def main():
     dev = torch.device("cuda", local)
     init_process_group(dev)
 
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.planes:
+        cfg["D"] = min(cfg["D"], args.planes)
     N, H, W, D, B = cfg["N"], cfg["H"], cfg["W"], cfg["D"], args.batch
     P = {k: torch.from_numpy(v) for k, v in syn.sweep_weights(1).items()}
     feats_h, proj, dv, feats = make_inputs(cfg, B, seed=rank, device=dev)
