@@ -416,12 +416,12 @@ __device__ __forceinline__ float4 ld_c8(__amdgpu_buffer_rsrc_t r, uint32_t p, in
   return ld4(r, (uint32_t)(s >> 1) * (uint32_t)HW * 32u + p * 32u + 16u * (uint32_t)(s & 1));
 }
 
-// cost_x: x_d on an 4 x 32 tile, two lanes per reference pixel (lane h holds channels
+// cost_x: x_d on an 8 x 32 tile, two lanes per reference pixel (lane h holds channels
 // 8c + 4h .. 8c + 4h + 3 of every chunk c), so that one wave-wide tap load covers 32
 // pixels x 32 B of a chunk image: contiguous 1-KiB requests.  The views are
 // accumulated in view order in registers.
-constexpr int kXRows = 4;
-__global__ void __launch_bounds__(kTileThreads) cost_x_kernel(PipeArgs a,
+constexpr int kXRows = 8;
+__global__ void __launch_bounds__(2 * kXRows * kTileW) cost_x_kernel(PipeArgs a,
                                                               const float* __restrict__ P,
                                                               const float* __restrict__ Rel) {
   __shared__ GnStat gs[AARMVS_MAX_SRC][3];
@@ -445,6 +445,10 @@ __global__ void __launch_bounds__(kTileThreads) cost_x_kernel(PipeArgs a,
   const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's c8 image
   const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(a.ref + (size_t)b * kC * HW, fbytes);
   const size_t p = (size_t)gy * W + gx;
+  // this lane's half of the reference feature (16 channels), read once for all views
+  float4 rf[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) rf[c] = ld_c8(rref, (uint32_t)p, 2 * c + h, HW);
   float acc[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0.f;
@@ -462,7 +466,7 @@ __global__ void __launch_bounds__(kTileThreads) cost_x_kernel(PipeArgs a,
       const float4 g = bil4(ld_c8(rsrc, t.pix[0], s, HW), ld_c8(rsrc, t.pix[1], s, HW),
                             ld_c8(rsrc, t.pix[2], s, HW), ld_c8(rsrc, t.pix[3], s, HW), t);
       // x accumulation in view order (drmvsnet.py:311-316)
-      const float4 sq = sqdiff4(g, ld_c8(rref, (uint32_t)p, s, HW));
+      const float4 sq = sqdiff4(g, rf[c]);
       float* ac = &acc[4 * c];
       ac[0] = __fadd_rn(ac[0], __fmul_rn(wp1, sq.x));
       ac[1] = __fadd_rn(ac[1], __fmul_rn(wp1, sq.y));
@@ -512,20 +516,22 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
   const int gy = y0 + ty, gx = x0 + tx;
   const bool inside = gy < H && gx < W;
   const int own_hp = (ty + 1) * kCHW + tx + 1;
-  // this thread's ring pixel
-  const bool has_ring = tid < kCRing;
+  // this thread's ring pixel: ring pixel r goes to lane r / 4 of wave r % 4, so every
+  // wave carries a quarter of the ring (the sq phase is paced by its slowest wave)
+  const int rr = lane * kTileWaves + wave;
+  const bool has_ring = rr < kCRing;
   int hy, hx;
-  if (tid < kCHW) {
+  if (rr < kCHW) {
     hy = 0;
-    hx = tid;
-  } else if (tid < 2 * kCHW) {
+    hx = rr;
+  } else if (rr < 2 * kCHW) {
     hy = kCHH - 1;
-    hx = tid - kCHW;
-  } else if (tid < 2 * kCHW + kTileH) {
-    hy = 1 + tid - 2 * kCHW;
+    hx = rr - kCHW;
+  } else if (rr < 2 * kCHW + kTileH) {
+    hy = 1 + rr - 2 * kCHW;
     hx = 0;
   } else {
-    hy = 1 + tid - 2 * kCHW - kTileH;
+    hy = 1 + rr - 2 * kCHW - kTileH;
     hx = kCHW - 1;
   }
   const int ry = y0 - 1 + hy, rx = x0 - 1 + hx;
@@ -750,7 +756,7 @@ hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Worksp
     a.omega_out = omega_out;
     const int ntiles = tiles_x * ((g.H + kXRows - 1) / kXRows);
     ProfScope ps(s, K_COST_X);
-    hipLaunchKernelGGL(cost_x_kernel, dim3(ntiles, g.B), dim3(kTileThreads), 0, s, a, a.params,
+    hipLaunchKernelGGL(cost_x_kernel, dim3(ntiles, g.B), dim3(2 * kXRows * kTileW), 0, s, a, a.params,
                        a.rel);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

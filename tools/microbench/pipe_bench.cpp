@@ -79,7 +79,7 @@ int main(int argc, char** argv) {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     printf("%-36s %8.3f ms  %7.0f GB/s algorithmic\n", name, ms / R, bytes / (ms / R) / 1e6);
   };
-  run("cost_x", cost_x_kernel, dim3(tiles_x * ((H + kXRows - 1) / kXRows), B), kTileThreads,
+  run("cost_x", cost_x_kernel, dim3(tiles_x * ((H + kXRows - 1) / kXRows), B), 2 * kXRows * kTileW,
       128.0 * (nsrc + 2) * HW);
   const dim3 gc(tiles_x * ((H + kTileH - 1) / kTileH), nsrc, B);
   const double bc = (128.0 * (nsrc + 1) + 16.0 * nsrc) * HW;
