@@ -32,6 +32,7 @@ class SweepArgs(ctypes.Structure):
         ("cost_out", c_void_p),
         ("slice_out", c_void_p),
         ("omega_out", c_void_p),
+        ("aux_stream", c_void_p),
     ]
 
 

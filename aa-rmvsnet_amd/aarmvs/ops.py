@@ -104,10 +104,13 @@ class DepthSweep:
     Holds the packed parameters and a workspace per (B, H, W, nsrc) geometry.
     """
 
-    def __init__(self, params: dict, device):
+    def __init__(self, params: dict, device, overlap: bool = True):
+        """``overlap``: run each next plane's omega pipeline on a second stream, concurrent
+        with the current plane's cost slice and regulariser step (same results)."""
         self.device = torch.device(device)
         self.packed = pack_params(params, self.device)
         self._ws = {}
+        self._aux = torch.cuda.Stream(device=self.device) if overlap else None
 
     def workspace(self, B, H, W, nsrc) -> torch.Tensor:
         key = (B, H, W, nsrc)
@@ -175,6 +178,7 @@ class DepthSweep:
         a.cost_out = _ptr(out["cost"])
         a.slice_out = _ptr(out["slice"])
         a.omega_out = _ptr(out["omega"])
+        a.aux_stream = self._aux.cuda_stream if self._aux is not None else None
         check(lib().aarmvs_sweep(ctypes.byref(a), _stream()), "sweep")
         out["_keepalive"] = (rel, dv, srcs, ref)
         return out

@@ -108,11 +108,15 @@ struct CostArgs {
   const float* depth_values;  // [B,D]
   const float* params;    // packed
 };
-// One step of the cost-slice pipeline: cost slice x of plane d_prev (if >= 0) and the
-// omega conv output + GroupNorm statistics of plane d_next (if >= 0).
+// The cost-slice pipeline (warp_cost.hip): cost_x writes plane d's cost slice from t1_d
+// and plane d's statistics; omega_next produces t1 and the three GroupNorm statistics of
+// plane d (omega_conv + omega_stats<1> + <2>).  The statistics of a plane must be zero
+// before its omega_next and are cleared by the caller once its cost_x has run.
 hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s);
-hipError_t launch_cost_pipe(const CostArgs& a, const SweepGeom& g, const Workspace& ws,
-                            int d_prev, int d_next, float* omega_out, hipStream_t s);
+hipError_t launch_cost_x(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d,
+                         float* omega_out, hipStream_t s);
+hipError_t launch_omega_next(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d,
+                             hipStream_t s);
 
 hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
                             const Workspace& ws, int parity, hipStream_t s);

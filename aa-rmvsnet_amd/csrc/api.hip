@@ -363,48 +363,105 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   ca.rel = a->rel_proj;
   ca.depth_values = a->depth_values;
   ca.params = params;
+  // Two-stream schedule (a->aux_stream): the omega pipeline of plane d+1 (omega_conv +
+  // statistics) runs on the aux stream while the main stream runs plane d's cost slice
+  // and regulariser step.  Per plane two events: ev_aux[p] "t1/statistics of plane p
+  // ready" (aux -> main, before cost_x(p)) and ev_main[p] "cost_x(p) done and plane p's
+  // statistics cleared" (main -> aux, before omega of plane p + 2, which reuses the
+  // buffers of parity p).
+  hipStream_t aux = (a->aux_stream && a->aux_stream != stream) ? a->aux_stream : nullptr;
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // main[2], aux[2], fork/join
+  auto destroy_events = [&] {
+    for (hipEvent_t& x : ev)
+      if (x) (void)hipEventDestroy(x), x = nullptr;
+  };
+  auto sweep_fail = [&](hipError_t err, const char* where) {
+    destroy_events();
+    return hip_fail(err, where);
+  };
+  if (aux)
+    for (hipEvent_t& x : ev)
+      if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
+        return sweep_fail(e, "sweep: event create");
+  hipEvent_t* ev_main = ev;
+  hipEvent_t* ev_aux = ev + 2;
+  hipStream_t os = aux ? aux : stream;   // the omega pipeline's stream
+
   if (a->d_begin == 0) {
     // UNetConvLSTM._init_hidden (drmvsnet.py:133-134, 202-206) and the WTA images
-    // (drmvsnet.py:302-304); then prime the cost-slice pipeline with plane 0's omega
-    // conv output and statistics
+    // (drmvsnet.py:302-304)
     if ((e = hipMemsetAsync(ws.state_begin, 0, ws.state_bytes, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: state init");
+      return sweep_fail(e, "sweep: state init");
     if ((e = hipMemsetAsync(ws.max_prob, 0, ws.wta_bytes, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: wta init");
+      return sweep_fail(e, "sweep: wta init");
     if ((e = hipMemsetAsync(ws.omega_stats[0], 0, ws.stats_bytes, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: stats init");
-    // c8 copies of the features for the pipeline's LDS source boxes
+      return sweep_fail(e, "sweep: stats init");
+    // c8 copies of the features for the pipeline
     const int HW = a->H * a->W;
     if ((e = launch_to_c8(a->ref_fea, ws.feat8[0], a->B, HW, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: c8 copy");
+      return sweep_fail(e, "sweep: c8 copy");
     for (int v = 0; v < a->nsrc; ++v)
       if ((e = launch_to_c8(a->src_fea[v], ws.feat8[1 + v], a->B, HW, stream)) != hipSuccess)
-        return hip_fail(e, "sweep: c8 copy");
-    if ((e = launch_cost_pipe(ca, g, ws, -1, 0, nullptr, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: cost pipeline prologue");
+        return sweep_fail(e, "sweep: c8 copy");
+  }
+  if (aux) {   // fork: the aux stream starts after everything enqueued on `stream` so far
+    if ((e = hipEventRecord(ev[4], stream)) != hipSuccess ||
+        (e = hipStreamWaitEvent(aux, ev[4], 0)) != hipSuccess)
+      return sweep_fail(e, "sweep: fork");
+  }
+  if (a->d_begin == 0) {   // prime the pipeline with plane 0's omega conv and statistics
+    if ((e = launch_omega_next(ca, g, ws, 0, os)) != hipSuccess)
+      return sweep_fail(e, "sweep: omega pipeline prologue");
+    if (aux && (e = hipEventRecord(ev_aux[0], aux)) != hipSuccess)
+      return sweep_fail(e, "sweep: event record");
   }
   const bool wta = a->depth_out || a->conf_out;
+  const size_t stats_parity_bytes = ws.omega_stats_bytes;
   for (int d = a->d_begin; d < a->d_end; ++d) {
     const bool last = d == a->d_end - 1;
-    const int d_next = d + 1 < a->D ? d + 1 : -1;
-    if ((e = launch_cost_pipe(ca, g, ws, d, d_next, last ? a->omega_out : nullptr, stream)) !=
-        hipSuccess)
-      return hip_fail(e, "sweep: cost pipeline");
+    // omega pipeline of plane d + 1; its buffers were last read by cost_x(d - 1)
+    if (d + 1 < a->D) {
+      if (aux && d - 1 >= a->d_begin &&
+          (e = hipStreamWaitEvent(aux, ev_main[(d - 1) & 1], 0)) != hipSuccess)
+        return sweep_fail(e, "sweep: event wait");
+      if ((e = launch_omega_next(ca, g, ws, d + 1, os)) != hipSuccess)
+        return sweep_fail(e, "sweep: omega pipeline");
+      if (aux && (e = hipEventRecord(ev_aux[(d + 1) & 1], aux)) != hipSuccess)
+        return sweep_fail(e, "sweep: event record");
+    }
+    // cost slice of plane d (its omega pipeline ran in the previous iteration, or in the
+    // previous call for the first plane of a continued range)
+    if (aux && (d > a->d_begin || a->d_begin == 0) &&
+        (e = hipStreamWaitEvent(stream, ev_aux[d & 1], 0)) != hipSuccess)
+      return sweep_fail(e, "sweep: event wait");
+    if ((e = launch_cost_x(ca, g, ws, d, last ? a->omega_out : nullptr, stream)) != hipSuccess)
+      return sweep_fail(e, "sweep: cost slice");
+    // plane d's statistics are consumed: clear them for plane d + 2
+    if ((e = hipMemsetAsync(ws.omega_stats[d & 1], 0, stats_parity_bytes, stream)) != hipSuccess)
+      return sweep_fail(e, "sweep: stats clear");
+    if (aux && (e = hipEventRecord(ev_main[d & 1], stream)) != hipSuccess)
+      return sweep_fail(e, "sweep: event record");
     if (last && a->slice_out) {
       e = hipMemcpyAsync(a->slice_out, ws.x, (size_t)a->B * kC * a->H * a->W * 4,
                          hipMemcpyDeviceToDevice, stream);
-      if (e != hipSuccess) return hip_fail(e, "sweep: slice copy");
+      if (e != hipSuccess) return sweep_fail(e, "sweep: slice copy");
     }
     if ((e = launch_unet_step(ws.x, params, g, ws, d & 1, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: regulariser step");
+      return sweep_fail(e, "sweep: regulariser step");
     if ((e = launch_head_wta(params, g, ws, d & 1, a->depth_values, d, a->cost_out, wta, stream)) !=
         hipSuccess)
-      return hip_fail(e, "sweep: head/wta");
+      return sweep_fail(e, "sweep: head/wta");
+  }
+  if (aux) {   // join: everything the call enqueued is ordered on `stream` at return
+    if ((e = hipEventRecord(ev[4], aux)) != hipSuccess ||
+        (e = hipStreamWaitEvent(stream, ev[4], 0)) != hipSuccess)
+      return sweep_fail(e, "sweep: join");
   }
   if (wta && a->d_end == a->D) {
     if ((e = launch_finalize(g, ws, a->depth_out, a->conf_out, stream)) != hipSuccess)
-      return hip_fail(e, "sweep: finalize");
+      return sweep_fail(e, "sweep: finalize");
   }
+  destroy_events();
   return AARMVS_OK;
 }
 

@@ -198,8 +198,6 @@ struct PipeArgs {
       off_ob2, off_og2w, off_og2b, off_owo, off_obo;
   int B, H, W, nsrc;
   int box_cap;                // LDS source-box capacity in pixels (diagnostic override, <= the kernel's)
-  double* zero_ptr;           // omega_stats<1>: stale statistics to clear (or null)
-  int zero_n;
 };
 
 // omega pointwise chain helpers (ResnetBlockGn, module.py:252-264)
@@ -516,22 +514,20 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
   const int gy = y0 + ty, gx = x0 + tx;
   const bool inside = gy < H && gx < W;
   const int own_hp = (ty + 1) * kCHW + tx + 1;
-  // this thread's ring pixel: ring pixel r goes to lane r / 4 of wave r % 4, so every
-  // wave carries a quarter of the ring (the sq phase is paced by its slowest wave)
-  const int rr = lane * kTileWaves + wave;
-  const bool has_ring = rr < kCRing;
+  // this thread's ring pixel
+  const bool has_ring = tid < kCRing;
   int hy, hx;
-  if (rr < kCHW) {
+  if (tid < kCHW) {
     hy = 0;
-    hx = rr;
-  } else if (rr < 2 * kCHW) {
+    hx = tid;
+  } else if (tid < 2 * kCHW) {
     hy = kCHH - 1;
-    hx = rr - kCHW;
-  } else if (rr < 2 * kCHW + kTileH) {
-    hy = 1 + rr - 2 * kCHW;
+    hx = tid - kCHW;
+  } else if (tid < 2 * kCHW + kTileH) {
+    hy = 1 + tid - 2 * kCHW;
     hx = 0;
   } else {
-    hy = 1 + rr - 2 * kCHW - kTileH;
+    hy = 1 + tid - 2 * kCHW - kTileH;
     hx = kCHW - 1;
   }
   const int ry = y0 - 1 + hy, rx = x0 - 1 + hx;
@@ -657,8 +653,7 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
   }
 }
 
-// GN #STAGE (1 or 2) partial sums of the omega chain on t1 (plane d_next).  Stage 1
-// also clears the statistics of the plane before (their last reader has finished).
+// GN #STAGE (1 or 2) partial sums of the omega chain on t1 (plane d_next).
 template <int STAGE>
 __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
                                                           const float* __restrict__ P) {
@@ -666,9 +661,6 @@ __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
   __shared__ GnStat gs[2];
   const int v = blockIdx.y, b = blockIdx.z;
   const int HW = a.H * a.W;
-  if (STAGE == 1 && a.zero_ptr && v == 0 && b == 0)
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.zero_n; i += gridDim.x * blockDim.x)
-      a.zero_ptr[i] = 0.0;
   if (threadIdx.x < STAGE)
     gs[threadIdx.x] = stat_read(a.st_next + st_index(b, v, threadIdx.x, a.nsrc), 4.0 * HW);
   __syncthreads();
@@ -739,42 +731,46 @@ static int pipe_box_cap() {
   return (s && *s) ? std::max(4, std::atoi(s)) : INT_MAX;
 }
 
-hipError_t launch_cost_pipe(const CostArgs& ca, const SweepGeom& g, const Workspace& ws,
-                            int d_prev, int d_next, float* omega_out, hipStream_t s) {
+static PipeArgs pipe_args_c8(const CostArgs& ca, const SweepGeom& g, const Workspace& ws) {
   PipeArgs a = pipe_args(ca, g, ws);
-  a.box_cap = pipe_box_cap();
   // the pipeline reads the c8 copies of the features in the workspace
   a.ref = ws.feat8[0];
   for (int v = 0; v < g.nsrc; ++v) a.src[v] = ws.feat8[1 + v];
-  a.d_prev = d_prev;
-  a.d_next = d_next;
+  a.box_cap = pipe_box_cap();
+  return a;
+}
+
+hipError_t launch_cost_x(const CostArgs& ca, const SweepGeom& g, const Workspace& ws, int d,
+                         float* omega_out, hipStream_t s) {
+  PipeArgs a = pipe_args_c8(ca, g, ws);
+  a.d_prev = d;
+  a.d_next = -1;
+  a.t1_prev = reinterpret_cast<const float4*>(ws.t1[d & 1]);
+  a.st_prev = ws.omega_stats[d & 1];
+  a.omega_out = omega_out;
+  const int ntiles = ((g.W + kTileW - 1) / kTileW) * ((g.H + kXRows - 1) / kXRows);
+  ProfScope ps(s, K_COST_X);
+  hipLaunchKernelGGL(cost_x_kernel, dim3(ntiles, g.B), dim3(2 * kXRows * kTileW), 0, s, a, a.params,
+                     a.rel);
+  return hipGetLastError();
+}
+
+hipError_t launch_omega_next(const CostArgs& ca, const SweepGeom& g, const Workspace& ws, int d,
+                             hipStream_t s) {
+  PipeArgs a = pipe_args_c8(ca, g, ws);
+  a.d_prev = -1;
+  a.d_next = d;
+  a.t1_next = reinterpret_cast<float4*>(ws.t1[d & 1]);
+  a.st_next = ws.omega_stats[d & 1];
   hipError_t e;
-  const int tiles_x = (g.W + kTileW - 1) / kTileW;
-  if (d_prev >= 0) {
-    a.t1_prev = reinterpret_cast<const float4*>(ws.t1[d_prev & 1]);
-    a.st_prev = ws.omega_stats[d_prev & 1];
-    a.omega_out = omega_out;
-    const int ntiles = tiles_x * ((g.H + kXRows - 1) / kXRows);
-    ProfScope ps(s, K_COST_X);
-    hipLaunchKernelGGL(cost_x_kernel, dim3(ntiles, g.B), dim3(2 * kXRows * kTileW), 0, s, a, a.params,
-                       a.rel);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  }
-  if (d_next < 0) return hipSuccess;
-  a.t1_next = reinterpret_cast<float4*>(ws.t1[d_next & 1]);
-  a.st_next = ws.omega_stats[d_next & 1];
   {
-    const int ntiles = tiles_x * ((g.H + kTileH - 1) / kTileH);
+    const int ntiles = ((g.W + kTileW - 1) / kTileW) * ((g.H + kTileH - 1) / kTileH);
     ProfScope ps(s, K_OMEGA_CONV);
     hipLaunchKernelGGL(omega_conv_kernel<0>, dim3(ntiles, g.nsrc, g.B), dim3(kTileThreads), 0, s, a,
                        a.params, a.rel);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  // GN #1 / #2 statistics of plane d_next; stage 1 clears plane d_prev's statistics
-  if (d_prev >= 0) {
-    a.zero_ptr = ws.omega_stats[d_prev & 1];
-    a.zero_n = (int)(ws.omega_stats_bytes / sizeof(double));
-  }
+  // GN #1 / #2 statistics of plane d
   const int HW = g.H * g.W;
   const int pblk =
       std::max(1, std::min((HW + 255) / 256, 2 * g.cu_count / std::max(1, g.B * g.nsrc) + 1));

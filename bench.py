@@ -165,6 +165,10 @@ def main():
     ap.add_argument("--cpu-planes", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run the omega pipeline on the main stream (no second stream)")
+    ap.add_argument("--high-priority", action="store_true",
+                    help="run the sweep's main stream at high priority (aux stream normal)")
     ap.add_argument("--planes", type=int, default=0,
                     help="profiling aid: sweep only the first P depth planes (0 = all D); "
                          "per-launch figures are unchanged, the headline value is not comparable")
@@ -181,7 +185,9 @@ def main():
     N, H, W, D, B = cfg["N"], cfg["H"], cfg["W"], cfg["D"], args.batch
     P = {k: torch.from_numpy(v) for k, v in syn.sweep_weights(1).items()}
     feats_h, proj, dv, feats = make_inputs(cfg, B, seed=rank, device=dev)
-    sweep = ops.DepthSweep({k: v.to(dev) for k, v in P.items()}, dev)
+    sweep = ops.DepthSweep({k: v.to(dev) for k, v in P.items()}, dev, overlap=not args.no_overlap)
+    if args.high_priority:
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     ref, srcs = feats[0], list(feats[1:])
     src_proj = list(proj[:, 1:].unbind(1))
 

@@ -176,3 +176,27 @@ def test_pipeline_box_fallbacks_are_bit_identical(monkeypatch, cap):
     b = sw(*args, want_cost=True, debug=True)
     for k in ("cost", "slice", "omega", "depth", "conf"):
         assert torch.equal(a[k], b[k]), k
+
+
+def test_two_stream_schedule_is_bit_identical():
+    """The omega pipeline of plane d+1 on a second stream (the default) against the
+    single-stream schedule: same kernels, same inputs, so bit-identical outputs; a
+    continued range (d_range) must also match a full sweep."""
+    from aarmvs import ops
+    B, N, H, W, D = 1, 4, 64, 96, 6
+    sc = syn.scene(B, N, H, W, D, seed=9)
+    feats = torch.from_numpy(sc["features"]).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    args = (feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+            [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]))
+    P = P_of(4)
+    a = ops.DepthSweep(P, DEV, overlap=True)(*args, want_cost=True)
+    b = ops.DepthSweep(P, DEV, overlap=False)(*args, want_cost=True)
+    sw = ops.DepthSweep(P, DEV, overlap=True)
+    cost = torch.empty(B, D, H, W, device=DEV)
+    sw(*args, d_range=(0, 2), cost_out=cost)
+    c = sw(*args, d_range=(2, D), cost_out=cost)
+    for k in ("cost", "depth", "conf"):
+        assert torch.equal(a[k], b[k]), k
+    assert torch.equal(a["cost"], cost)
+    assert torch.equal(a["depth"], c["depth"]) and torch.equal(a["conf"], c["conf"])

@@ -59,7 +59,7 @@ int main(int argc, char** argv) {
   ca.rel = drel; ca.depth_values = ddv; ca.params = dpar;
   CK(launch_to_c8(feats[0], ws.feat8[0], B, (int)HW, 0));
   for (int v = 0; v < nsrc; ++v) CK(launch_to_c8(feats[v + 1], ws.feat8[v + 1], B, (int)HW, 0));
-  CK(launch_cost_pipe(ca, g, ws, -1, 0, nullptr, 0));
+  CK(launch_omega_next(ca, g, ws, 0, 0));
   CK(hipDeviceSynchronize());
   PipeArgs a0 = pipe_args(ca, g, ws);
   a0.d_prev = 0; a0.d_next = 1;
