@@ -110,7 +110,19 @@ class DepthSweep:
         self.device = torch.device(device)
         self.packed = pack_params(params, self.device)
         self._ws = {}
-        self._aux = torch.cuda.Stream(device=self.device) if overlap else None
+        self._aux = None
+        self.overlap = overlap
+
+    @property
+    def overlap(self) -> bool:
+        return self._aux is not None
+
+    @overlap.setter
+    def overlap(self, on: bool):
+        if on and self._aux is None:
+            self._aux = torch.cuda.Stream(device=self.device)
+        elif not on:
+            self._aux = None
 
     def workspace(self, B, H, W, nsrc) -> torch.Tensor:
         key = (B, H, W, nsrc)
