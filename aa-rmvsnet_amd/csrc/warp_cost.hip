@@ -275,7 +275,6 @@ constexpr int kTileW = 32, kTileH = 8, kTileThreads = kTileW * kTileH;
 constexpr int kTileWaves = kTileThreads / 64;
 constexpr int kCHH = kTileH + 2, kCHW = kTileW + 2;   // omega_conv haloed tile
 constexpr int kCRing = 2 * kCHW + 2 * kTileH;         // its halo-only (ring) pixels
-constexpr int kSqStride = 12;   // floats per halo pixel in the sq tile (8 used): conflict-free b128
 constexpr int kCBoxPx = 448;    // omega_conv LDS source box: 32-B pixels (one chunk)
 static_assert(kCRing <= kTileThreads, "one ring pixel per thread at most");
 
@@ -480,40 +479,67 @@ __global__ void __launch_bounds__(2 * kXRows * kTileW) cost_x_kernel(PipeArgs a,
       xo[(size_t)(8 * c + 4 * h + j) * HW] = -1.0f * __fdiv_rn(acc[4 * c + j], (float)nsrc);
 }
 
-// omega_conv LDS box: 32-B pixels (one chunk), the two 16-B halves of pixel p swapped
-// when bit 3 of p is set (16 consecutive pixels' reads of one half cover all banks)
-__device__ __forceinline__ float4 box32(const float* box, uint32_t p, int h) {
-  return *reinterpret_cast<const float4*>(box + p * 8u + (uint32_t)((h ^ (int)((p >> 3) & 1u)) << 2));
+// omega_conv LDS images (source box, reference tile, sq tile): 32-B pixels (one chunk),
+// the two 16-B halves of pixel p swapped when bit 3 of p is set, so that 16 consecutive
+// pixels' reads of one half cover all banks.  Piece i of an image (pixel i >> 1, slot
+// i & 1) sits at byte 16 i: images are lane-linear and filled by LDS-DMA.
+__device__ __forceinline__ uint32_t img_slot(uint32_t p, int h) {
+  return p * 8u + ((uint32_t)(h ^ (int)((p >> 3) & 1u)) << 2);
+}
+__device__ __forceinline__ float4 img_ld(const float* img, uint32_t p, int h) {
+  return *reinterpret_cast<const float4*>(img + img_slot(p, h));
+}
+__device__ __forceinline__ void img_st(float* img, uint32_t p, int h, float4 v) {
+  *reinterpret_cast<float4*>(img + img_slot(p, h)) = v;
+}
+// the half of pixel p held in slot s of its image: slot ^ swizzle bit
+__device__ __forceinline__ int img_half(uint32_t p, int s) { return s ^ (int)((p >> 3) & 1u); }
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+// LDS-DMA, 16 B per lane: lane l of the wave lands at wave_dst + 16 l (wave_dst uniform);
+// an offset past the buffer's range loads zeros
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float* wave_dst, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)wave_dst, 16, off, 0, 0, 0);
+}
+__device__ __forceinline__ void dma_wait() {
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
 }
 
-// omega_conv: t1 of plane d_next for one (tile, view) per block.  The squared difference
-// on the (8+2) x 34 haloed tile goes through LDS one 8-channel chunk at a time (own
-// pixel by every thread, ring pixels by threads 0..kCRing-1); each thread accumulates
-// its pixel's conv3x3 32->4 over the chunks.  The chunk's source box is staged in LDS
-// (the next chunk's box loads are in flight during the conv); a box past kCBoxPx
-// pixels is sampled from global memory.
+// omega_conv: t1 of plane d_next for one (tile, view) per block.  Per 8-channel chunk c:
+// the chunk's source box (bounding box of the block's bilinear taps) and the haloed
+// (8+2) x 34 reference tile arrive in LDS by LDS-DMA, issued while the previous chunk's
+// conv runs; the squared difference on the haloed tile goes to the sq image (own pixel
+// by every thread, ring pixels by threads 0..kCRing-1); each thread accumulates its
+// pixel's conv3x3 32->4 over the chunks.  A box past kCBoxPx pixels is sampled from
+// global memory instead.
 // ABL: ablation bits for the diagnostic harness only (tools/microbench/pipe_bench.cpp;
 // the library instantiates ABL = 0): 1 no conv FMAs, 2 no squared differences, 4 no box
-// loads.
+// loads, 8 conv tap loop rolled.
 template <int ABL = 0>
 __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
                                                                   const float* __restrict__ P,
                                                                   const float* __restrict__ Rel) {
-  constexpr int NPF = (2 * kCBoxPx + kTileThreads - 1) / kTileThreads;   // box items per thread
+  constexpr int NHP = kCHH * kCHW;                                      // haloed tile pixels
+  constexpr int NB = (2 * kCBoxPx + kTileThreads - 1) / kTileThreads;   // box pieces per thread
+  constexpr int NR = (2 * NHP + kTileThreads - 1) / kTileThreads;       // ref pieces per thread
   __shared__ __attribute__((aligned(16))) float box[(kCBoxPx + 1) * 8];
-  __shared__ __attribute__((aligned(16))) float sqt[kCHH * kCHW * kSqStride];
+  __shared__ __attribute__((aligned(16))) float rt[NHP * 8];
+  __shared__ __attribute__((aligned(16))) float sqt[NHP * 8];
   __shared__ int red[kTileWaves][4];
   __shared__ float wsum[kTileWaves][2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int v = blockIdx.y, b = blockIdx.z;
+  const int b = blockIdx.z;
   const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  // the views of one tile are consecutive blocks on one XCD: the reference tile is
+  // fetched from HBM once and re-read from that XCD's L2
+  const int seq = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = seq / nsrc, v = seq - tile * nsrc;
   const int tiles_x = (W + kTileW - 1) / kTileW;
   const int y0 = (tile / tiles_x) * kTileH, x0 = (tile % tiles_x) * kTileW;
   const int ty = tid / kTileW, tx = tid % kTileW;
   const int gy = y0 + ty, gx = x0 + tx;
   const bool inside = gy < H && gx < W;
-  const int own_hp = (ty + 1) * kCHW + tx + 1;
+  const uint32_t own_hp = (uint32_t)((ty + 1) * kCHW + tx + 1);
   // this thread's ring pixel
   const bool has_ring = tid < kCRing;
   int hy, hx;
@@ -532,18 +558,15 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
   }
   const int ry = y0 - 1 + hy, rx = x0 - 1 + hx;
   const bool ring_in = has_ring && ry >= 0 && ry < H && rx >= 0 && rx < W;
-  const int ring_hp = hy * kCHW + hx;
+  const uint32_t ring_hp = (uint32_t)(hy * kCHW + hx);
   if (tid < 8) box[kCBoxPx * 8 + tid] = 0.f;   // the zero pixel
 
   const float dep = a.dvals[b * a.D + a.d_next];
   const float* __restrict__ m = Rel + 12 * (v * a.B + b);
   const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's c8 image
-  const uint32_t zg = fbytes / 32u;                          // a pixel index past the buffer
+  const uint32_t cbytes = (uint32_t)HW * 32u;                // one chunk image
   const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(a.ref + (size_t)b * kC * HW, fbytes);
   const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
-  // pixels outside the image read zeros everywhere: the conv's zero padding
-  const uint32_t own_px = inside ? (uint32_t)(gy * W + gx) : zg;
-  const uint32_t ring_px = ring_in ? (uint32_t)(ry * W + rx) : zg;
   TapF tfo{}, tfr{};
   int lx = INT_MAX, ly = INT_MAX, bhx = INT_MIN, bhy = INT_MIN;
   if (inside) {
@@ -556,34 +579,41 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
   }
   const Box bx = box_reduce(lx, ly, bhx, bhy, red);
   const bool lds = bx.nx * bx.ny <= min(kCBoxPx, a.box_cap);
-  const uint32_t zp = lds ? (uint32_t)kCBoxPx : zg;
+  const uint32_t zp = lds ? (uint32_t)kCBoxPx : fbytes / 32u;
   const TapP to = tap_p(tfo, inside, H, W, lds, bx, zp), tr = tap_p(tfr, ring_in, H, W, lds, bx, zp);
-  const uint32_t mg = box_magic(bx.nx);
+  // chunk-0 byte offsets of this thread's DMA pieces (chunk c adds c * cbytes)
   const int items = (lds && !(ABL & 4)) ? bx.nx * bx.ny * 2 : 0;
-  // box chunk c: item i = (pixel i >> 1, half i & 1); consecutive lanes read
-  // consecutive 16-B pieces of a box row
-  float4 pf[NPF];
-  auto box_load = [&](int c) {
+  const uint32_t mg = box_magic(bx.nx);
+  uint32_t boff[NB], roff[NR];
 #pragma unroll
-    for (int j = 0; j < NPF; ++j) {
-      const int i = tid + j * kTileThreads;
-      if (i < items) {
-        const int p = i >> 1, r = box_row(p, bx.nx, mg);
-        const uint32_t gp = (uint32_t)((bx.y0 + r) * W + bx.x0 + (p - r * bx.nx));
-        pf[j] = ld_c8(rsrc, gp, 2 * c + ((i & 1) ^ ((p >> 3) & 1)), HW);
-      }
-    }
-  };
-  auto box_store = [&]() {
+  for (int j = 0; j < NB; ++j) {
+    const int i = tid + j * kTileThreads, p = i >> 1, r = box_row(p, bx.nx, mg);
+    const uint32_t gp = (uint32_t)((bx.y0 + r) * W + bx.x0 + (p - r * bx.nx));
+    boff[j] = gp * 32u + 16u * (uint32_t)img_half((uint32_t)p, i & 1);
+  }
 #pragma unroll
-    for (int j = 0; j < NPF; ++j) {
-      const int i = tid + j * kTileThreads;
-      if (i < items) *reinterpret_cast<float4*>(&box[(i >> 1) * 8 + ((i & 1) << 2)]) = pf[j];
-    }
+  for (int j = 0; j < NR; ++j) {
+    const int i = tid + j * kTileThreads, hp = i >> 1, py = hp / kCHW;
+    const int y = y0 - 1 + py, x = x0 - 1 + (hp - py * kCHW);
+    roff[j] = (y >= 0 && y < H && x >= 0 && x < W)
+                  ? (uint32_t)(y * W + x) * 32u + 16u * (uint32_t)img_half((uint32_t)hp, i & 1)
+                  : fbytes;   // zero padding
+  }
+  auto stage = [&](int c) {
+    const uint32_t cb = (uint32_t)c * cbytes;
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      if (tid + j * kTileThreads < items)
+        dma16(rsrc, box + (j * kTileThreads + wave * 64) * 4, boff[j] + cb);
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      if (tid + j * kTileThreads < 2 * NHP)
+        dma16(rref, rt + (j * kTileThreads + wave * 64) * 4, roff[j] < cbytes ? roff[j] + cb : fbytes);
   };
   auto sample = [&](const TapP& t, int c, int h) {
-    if (lds) return bil4(box32(box, t.pix[0], h), box32(box, t.pix[1], h), box32(box, t.pix[2], h),
-                         box32(box, t.pix[3], h), t);
+    if (lds)
+      return bil4(img_ld(box, t.pix[0], h), img_ld(box, t.pix[1], h), img_ld(box, t.pix[2], h),
+                  img_ld(box, t.pix[3], h), t);
     const int s = 2 * c + h;
     return bil4(ld_c8(rsrc, t.pix[0], s, HW), ld_c8(rsrc, t.pix[1], s, HW),
                 ld_c8(rsrc, t.pix[2], s, HW), ld_c8(rsrc, t.pix[3], s, HW), t);
@@ -591,38 +621,42 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
   const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]
   const float* __restrict__ b0 = P + a.off_ob0;
 
-  box_load(0);
-  box_store();
+  stage(0);
+  dma_wait();
   __syncthreads();
   float o4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
 #pragma unroll
     for (int h = 0; h < 2 && !(ABL & 2); ++h) {
-      *reinterpret_cast<float4*>(&sqt[own_hp * kSqStride + 4 * h]) =
-          sqdiff4(sample(to, c, h), ld_c8(rref, own_px, 2 * c + h, HW));
-      if (has_ring)
-        *reinterpret_cast<float4*>(&sqt[ring_hp * kSqStride + 4 * h]) =
-            sqdiff4(sample(tr, c, h), ld_c8(rref, ring_px, 2 * c + h, HW));
+      img_st(sqt, own_hp, h, sqdiff4(sample(to, c, h), img_ld(rt, own_hp, h)));
+      if (has_ring) img_st(sqt, ring_hp, h, sqdiff4(sample(tr, c, h), img_ld(rt, ring_hp, h)));
     }
-    __syncthreads();   // sq visible; this chunk's box reads are done
-    if (c < 3) box_load(c + 1);
+    __syncthreads();   // sq visible; this chunk's box / reference reads are done
+    if (c < 3) stage(c + 1);
     // omega.reweight_network.0.0: conv3x3 32->4, pad 1 (input channels 8c..8c+7)
-#pragma unroll 1
-    for (int tap = 0; tap < ((ABL & 1) ? 0 : 9); ++tap) {
-      const float* s8 = &sqt[(own_hp + (tap / 3 - 1) * kCHW + (tap % 3 - 1)) * kSqStride];
-      const float4 qa = *reinterpret_cast<const float4*>(s8);
-      const float4 qb = *reinterpret_cast<const float4*>(s8 + 4);
+    auto conv_tap = [&](int tap) {
+      const uint32_t hp = own_hp + (uint32_t)((tap / 3 - 1) * kCHW + (tap % 3 - 1));
+      const float4 qa = img_ld(sqt, hp, 0), qb = img_ld(sqt, hp, 1);
       const float qq[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
       const float* wt = w0t + (tap * kC + 8 * c) * 4;   // [j][co], contiguous
 #pragma unroll
       for (int j = 0; j < 8; ++j)
 #pragma unroll
         for (int co = 0; co < 4; ++co) o4[co] = fmaf(qq[j], wt[j * 4 + co], o4[co]);
+    };
+    // fully unrolled: the LDS reads and weight loads of later taps are issued ahead
+    // (0.72 vs 0.82 ms per plane at the headline geometry with a rolled loop)
+    if constexpr (ABL & 8) {
+#pragma unroll 1
+      for (int tap = 0; tap < 9; ++tap) conv_tap(tap);
+    } else if constexpr (!(ABL & 1)) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) conv_tap(tap);
     }
     if (c < 3) {
-      box_store();
-      __syncthreads();   // next box visible; the conv's sq reads are done
+      dma_wait();
+      __syncthreads();   // next chunk's images visible; the conv's sq reads are done
     }
   }
   float ps = 0.f, pss = 0.f;
@@ -766,7 +800,7 @@ hipError_t launch_omega_next(const CostArgs& ca, const SweepGeom& g, const Works
   {
     const int ntiles = ((g.W + kTileW - 1) / kTileW) * ((g.H + kTileH - 1) / kTileH);
     ProfScope ps(s, K_OMEGA_CONV);
-    hipLaunchKernelGGL(omega_conv_kernel<0>, dim3(ntiles, g.nsrc, g.B), dim3(kTileThreads), 0, s, a,
+    hipLaunchKernelGGL(omega_conv_kernel<0>, dim3(ntiles * g.nsrc, 1, g.B), dim3(kTileThreads), 0, s, a,
                        a.params, a.rel);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

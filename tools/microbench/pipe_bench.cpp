@@ -81,7 +81,7 @@ int main(int argc, char** argv) {
   };
   run("cost_x", cost_x_kernel, dim3(tiles_x * ((H + kXRows - 1) / kXRows), B), 2 * kXRows * kTileW,
       128.0 * (nsrc + 2) * HW);
-  const dim3 gc(tiles_x * ((H + kTileH - 1) / kTileH), nsrc, B);
+  const dim3 gc(tiles_x * ((H + kTileH - 1) / kTileH) * nsrc, 1, B);
   const double bc = (128.0 * (nsrc + 1) + 16.0 * nsrc) * HW;
   run("omega_conv", omega_conv_kernel<0>, gc, kTileThreads, bc);
   run("omega_conv no conv (1)", omega_conv_kernel<1>, gc, kTileThreads, bc);
@@ -89,6 +89,7 @@ int main(int argc, char** argv) {
   run("omega_conv no box loads (4)", omega_conv_kernel<4>, gc, kTileThreads, bc);
   run("omega_conv no sq/box (6)", omega_conv_kernel<6>, gc, kTileThreads, bc);
   run("omega_conv skeleton (7)", omega_conv_kernel<7>, gc, kTileThreads, bc);
+  run("omega_conv conv loop rolled (8)", omega_conv_kernel<8>, gc, kTileThreads, bc);
   a0.box_cap = 64;
   run("omega_conv (box cap 64: global gathers)", omega_conv_kernel<0>, gc, kTileThreads, bc);
   {
