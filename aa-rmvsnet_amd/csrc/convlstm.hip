@@ -618,6 +618,96 @@ struct H3Stager {
   }
 };
 
+// Pixel-major staging (the default): item = (half h of the chunk's 16 channels, pixel p
+// of the haloed tile), consecutive lanes on consecutive pixels.  A channel's loads are
+// contiguous runs of an image row, and an item lands in each LDS plane as ONE 16-B store
+// (8 channels as fp16 pairs) at h3_pix(p, h): 2-way bank conflicts at most, where the
+// segment stager above writes 4-B pairs 128 B apart (32-way).  Out-of-image pixels and
+// channels past the chunk's valid count load zeros through the buffer range check.
+template <int KIND, int RW, int WAVES>
+struct H3PixStager {
+  using C = H3Cfg<KIND, RW, WAVES>;
+  using D = typename C::D;
+  static constexpr int NITEM = 2 * C::NPIX;
+  static constexpr int NI = (NITEM + C::THREADS - 1) / C::THREADS;
+  static_assert(NI <= 32, "item mask holds 32 items");
+  float val[NI][8][4];   // [item][channel][POOL window: fine (2y,2x) (2y,2x+1) (2y+1,2x) (2y+1,2x+1)]
+  uint32_t in_mask;      // bit j: item j is an in-image pixel of valid channels
+
+  template <int CH>
+  __device__ __forceinline__ void load(const CellArgs& a, int b, int y0, int x0, int tid) {
+    constexpr int P = C::chunk_part(CH), MODE = D::MODE[P], NCH = D::CH[P];
+    constexpr int LC0 = C::chunk_lc0(CH), NV = C::chunk_nv(CH);
+    static_assert(NV % 8 == 0, "chunks hold whole 8-channel halves");
+    const ChanSrc& s = a.part[P];
+    const int H = a.H, W = a.W;
+    const int Hs = MODE == SRC_POOL ? 2 * H : H, Ws = MODE == SRC_POOL ? 2 * W : W;
+    const uint32_t plane = (uint32_t)Hs * (uint32_t)Ws * 4u;   // bytes of one channel image
+    const uint32_t nbytes = (uint32_t)NCH * plane;
+    const __amdgpu_buffer_rsrc_t r = uniform_rsrc(s.ptr + (size_t)b * NCH * Hs * Ws, nbytes);
+    in_mask = 0u;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int e = tid + j * C::THREADS;
+      const int h = e >= C::NPIX ? 1 : 0, p = e - h * C::NPIX;
+      const int row = p / C::W2, col = p - row * C::W2;
+      const int gy = y0 - 1 + row, gx = x0 - 1 + col;
+      const bool in = e < NITEM && 8 * h < NV && gy >= 0 && gy < H && gx >= 0 && gx < W;
+      if (in) in_mask |= 1u << j;
+      const uint32_t pix = MODE == SRC_POOL ? (uint32_t)(2 * gy * Ws + 2 * gx) : (uint32_t)(gy * W + gx);
+      const uint32_t base = (uint32_t)(LC0 + 8 * h) * plane + pix * 4u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t off = in ? base + (uint32_t)k * plane : nbytes;
+        if (MODE == SRC_POOL) {
+          const float2 t0 = ld2(r, off), t1 = ld2(r, in ? off + (uint32_t)Ws * 4u : nbytes);
+          val[j][k][0] = t0.x;
+          val[j][k][1] = t0.y;
+          val[j][k][2] = t1.x;
+          val[j][k][3] = t1.y;
+        } else {
+          val[j][k][0] = ld1(r, off);
+        }
+      }
+    }
+  }
+
+  template <int CH>
+  __device__ __forceinline__ void store(char* hi_plane, char* lo_plane, const float* gn, int tid,
+                                        int x0, int W) const {
+    constexpr int MODE = D::MODE[C::chunk_part(CH)];
+    constexpr int LC0 = C::chunk_lc0(CH);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int e = tid + j * C::THREADS;
+      if (e < NITEM) {
+        const int h = e >= C::NPIX ? 1 : 0, p = e - h * C::NPIX;
+        const bool in = in_mask & (1u << j);
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float x;
+          if (MODE == SRC_POOL) {
+            x = fmaxf(fmaxf(val[j][k][0], val[j][k][1]), fmaxf(val[j][k][2], val[j][k][3]));
+          } else if (MODE == SRC_GNRELU) {
+            const int lc = LC0 + 8 * h + k;
+            x = fmaxf(val[j][k][0] * gn[lc] + gn[16 + lc], 0.0f);
+          } else {
+            x = val[j][k][0];
+          }
+          v[k] = in ? x : 0.0f;
+        }
+        uint32_t hw[4], lw[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hw[i] = h3_split2(v[2 * i], v[2 * i + 1], lw[i]);
+        const int off = h3_pix(p, h);
+        *reinterpret_cast<u32x4*>(hi_plane + off) = u32x4{hw[0], hw[1], hw[2], hw[3]};
+        *reinterpret_cast<u32x4*>(lo_plane + off) = u32x4{lw[0], lw[1], lw[2], lw[3]};
+      }
+    }
+  }
+};
+
 template <class C, int CH>
 __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], const char* wl_hi,
                                               const char* wl_lo, const char* in_hi,
@@ -649,7 +739,9 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], con
   }
 }
 
-template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES>
+// STG: 1 pixel-major staging (H3PixStager, the library's), 0 segment staging (H3Stager;
+// kept for the cell microbenchmark's comparison)
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int STG = 1>
 __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
@@ -691,7 +783,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     y0 = (rem / tiles_x) * C::TH;
     x0 = (rem % tiles_x) * C::TW;
   };
-  H3Stager<KIND, RW, WAVES> st;
+  typename std::conditional<STG == 1, H3PixStager<KIND, RW, WAVES>, H3Stager<KIND, RW, WAVES>>::type st;
   int tile = blockIdx.x;
   if (tile < ntiles) {
     int b, y0, x0;
@@ -768,7 +860,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
   }
 }
 
-template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES>
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int STG = 1>
 static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu, int kid,
                               hipStream_t s) {
   using C = H3Cfg<KIND, RW, WAVES>;
@@ -776,7 +868,7 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
   static_assert(C::NS <= 32 && C::NH <= 32, "staging masks hold 32 items");
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_h3_kernel<KIND, RW, WAVES>,
+    hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, STG>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)C::LDS_BYTES);
     if (e != hipSuccess) return e;
@@ -786,7 +878,7 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
   const int per_cu = std::max(1, (int)((160 * 1024) / C::LDS_BYTES));
   const int grid = std::max(1, std::min(ntiles, cu * per_cu));
   ProfScope ps(s, kid);
-  hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES>), dim3(grid), dim3(C::THREADS),
+  hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, STG>), dim3(grid), dim3(C::THREADS),
                      C::LDS_BYTES, s, a, inv_scale);
   return hipGetLastError();
 }

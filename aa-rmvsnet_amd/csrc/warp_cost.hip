@@ -77,25 +77,6 @@ __device__ __forceinline__ float bilinear(const float* __restrict__ plane, const
                    __fmaf_rn(v[2], t.wt[2], __fmaf_rn(v[1], t.wt[1], __fmul_rn(v[0], t.wt[0]))));
 }
 
-// Buffer-descriptor loads for the streaming kernels: 32-bit byte offsets instead of
-// 64-bit addresses (VGPR pressure), and the hardware range check does the zero padding:
-// an offset at or past num_records loads 0.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const float* base, uint32_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
-  void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)n, 0x00020000);
-}
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ float4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
-                     __uint_as_float(v.w));
-}
 
 // ---------------------------------------------------------------------------
 // Standalone warp (aarmvs_homo_warp): one thread per (b, pixel), all channels.

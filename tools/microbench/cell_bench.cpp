@@ -76,5 +76,9 @@ int main() {
   run("cell1 h3", [&] { return run_cell_h3<1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
   run("cell3 h3", [&] { return run_cell_h3<3>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
   run("cell4 h3", [&] { return run_cell_h3<4>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+  run("cell0 h3 segment staging", [&] { return run_cell_h3<0, 1, 8, 0>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell1 h3 segment staging", [&] { return run_cell_h3<1, 1, 8, 0>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell3 h3 segment staging", [&] { return run_cell_h3<3, 1, 8, 0>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+  run("cell4 h3 segment staging", [&] { return run_cell_h3<4, 1, 8, 0>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
   return 0;
 }
