@@ -57,14 +57,14 @@ struct CellDef<0> {   // [x, h0] @ H
   static constexpr int NP = 2, CH[kMaxParts] = {32, 16, 0};
   static constexpr int MODE[kMaxParts] = {SRC_PLAIN, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16, TH = 4, NT = 1;
-  static constexpr int H3RW = 1, H3WAVES = 8;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1;
 };
 template <>
 struct CellDef<1> {   // [maxpool(h0'), h1] @ H/2
   static constexpr int NP = 2, CH[kMaxParts] = {16, 16, 0};
   static constexpr int MODE[kMaxParts] = {SRC_POOL, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16, TH = 8, NT = 1;
-  static constexpr int H3RW = 1, H3WAVES = 8;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 0;
 };
 template <>
 struct CellDef<2> : CellDef<1> {};   // [maxpool(h1'), h2] @ H/4
@@ -73,14 +73,14 @@ struct CellDef<3> {   // [gnrelu(u0), h1', h3] @ H/2
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 16};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16, TH = 4, NT = 1;
-  static constexpr int H3RW = 1, H3WAVES = 8;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1;
 };
 template <>
 struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 8};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 8, TH = 8, NT = 1;
-  static constexpr int H3RW = 1, H3WAVES = 8;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 0;
 };
 
 template <int KIND>
@@ -740,8 +740,10 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], con
 }
 
 // STG: 1 pixel-major staging (H3PixStager, the library's), 0 segment staging (H3Stager;
-// kept for the cell microbenchmark's comparison)
-template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int STG = 1>
+// kept for the cell microbenchmark's comparison).  ABL: ablation bits for the
+// microbenchmark only (1 no MFMA, 2 no staging loads/stores, 4 no gate math)
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int STG = 1,
+          int ABL = 0>
 __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
@@ -785,7 +787,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
   };
   typename std::conditional<STG == 1, H3PixStager<KIND, RW, WAVES>, H3Stager<KIND, RW, WAVES>>::type st;
   int tile = blockIdx.x;
-  if (tile < ntiles) {
+  if (tile < ntiles && !(ABL & 2)) {
     int b, y0, x0;
     coords(tile, b, y0, x0);
     st.template load<0>(a, b, y0, x0, tid);
@@ -810,9 +812,10 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     auto chunk = [&](auto CHc) {
       constexpr int CH = decltype(CHc)::value;
       __syncthreads();   // previous chunk's B reads done (weights / gn visible the first time)
-      st.template store<CH>(in_hi, in_lo, gn, tid, x0, W);
+      if (!(ABL & 2)) st.template store<CH>(in_hi, in_lo, gn, tid, x0, W);
       __syncthreads();
-      if (CH + 1 < NCHK) {
+      if (ABL & 2) {
+      } else if (CH + 1 < NCHK) {
         st.template load<(CH + 1 < NCHK ? CH + 1 : 0)>(a, b, y0, x0, tid);
       } else if (next < ntiles) {
         st.template load<0>(a, nb, ny0, nx0, tid);
@@ -828,7 +831,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
               cst[m][r][q] = (y < H && x < W) ? a.c[(((size_t)b * HID + ch) * H + y) * W + x] : 0.f;
             }
       }
-      h3_mfma_chunk<C, CH>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
     };
     chunk(std::integral_constant<int, 0>{});
     if constexpr (NCHK > 1) chunk(std::integral_constant<int, 1>{});
@@ -850,6 +853,11 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
             const float go = fmaf(acc[m][r][8 + q], inv_scale, a.bias[2 * HID + ch]);
             const float gg = fmaf(acc[m][r][12 + q], inv_scale, a.bias[3 * HID + ch]);
             const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
+            if (ABL & 4) {
+              a.c[idx] = gi + gf;
+              a.h_new[idx] = go + gg + cst[m][r][q];
+              continue;
+            }
             const float cn = fast_sigmoid(gf) * cst[m][r][q] + fast_sigmoid(gi) * fast_tanh(gg);
             a.c[idx] = cn;
             a.h_new[idx] = fast_sigmoid(go) * fast_tanh(cn);
@@ -860,26 +868,171 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
   }
 }
 
-template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int STG = 1>
+// Double-buffered variant (cells 0 and 3): the haloed input tile has two LDS buffers, so
+// a chunk's MFMAs and the staging of the following chunk share one phase (one barrier
+// per chunk).  Per step: MFMAs on buffer `par`; store the prefetched following chunk
+// (this tile's next, or the next tile's first) into buffer par ^ 1; issue the loads of
+// the chunk after that; at a tile's last chunk, the gate epilogue.  Across the two
+// waves of a SIMD one wave's staging VALU work fills the other's MFMA issue gaps.
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0>
+__global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
+    CellArgs a, const float* __restrict__ inv_scale_ptr) {
+  using C = H3Cfg<KIND, RW, WAVES>;
+  using D = typename C::D;
+  constexpr int MT = C::MT, HID = C::HID, NCHK = C::NCHK;
+  constexpr int PB = C::NPIX * 32;   // one plane (hi or lo) of one input buffer
+  static_assert(NCHK >= 2, "two or more input chunks");
+  extern __shared__ __attribute__((aligned(16))) char lds_h3[];
+  char* wl_hi = lds_h3;
+  char* wl_lo = wl_hi + C::A_HALVES * 2;
+  char* inb = wl_lo + C::A_HALVES * 2;   // buffer k: hi plane at 2k PB, lo plane at (2k+1) PB
+  float* gn = reinterpret_cast<float*>(inb + 4 * PB);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, W = a.W;
+  const float inv_scale = *inv_scale_ptr;
+  {
+    const float4* s = reinterpret_cast<const float4*>(a.wpk);
+    float4* d = reinterpret_cast<float4*>(wl_hi);
+    constexpr int N4 = C::A_HALVES * 2 * 2 / 16;
+#pragma unroll 8
+    for (int i = tid; i < N4; i += C::THREADS) d[i] = s[i];
+  }
+#pragma unroll
+  for (int p = 0; p < D::NP; ++p) {
+    if (D::MODE[p] == SRC_GNRELU && tid < 16) {
+      const GnStat st = stat_read(a.part[p].stats + (tid >> 3) * kSlots * 2, 8.0 * H * W);
+      const float sc = st.rstd * a.part[p].gamma[tid];
+      gn[tid] = sc;
+      gn[16 + tid] = a.part[p].beta[tid] - st.mean * sc;
+    }
+  }
+  const int tiles_x = (W + C::TW - 1) / C::TW, tiles_y = (H + C::TH - 1) / C::TH;
+  const int ntiles = a.B * tiles_x * tiles_y;
+  auto coords = [&](int tile, int& b, int& y0, int& x0) {
+    b = tile / (tiles_x * tiles_y);
+    const int rem = tile % (tiles_x * tiles_y);
+    y0 = (rem / tiles_x) * C::TH;
+    x0 = (rem % tiles_x) * C::TW;
+  };
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;   // whole block
+  H3PixStager<KIND, RW, WAVES> st;
+  int b, y0, x0;
+  coords(tile, b, y0, x0);
+  if (!(ABL & 2)) st.template load<0>(a, b, y0, x0, tid);
+  __syncthreads();   // gn visible to the staging
+  if (!(ABL & 2)) {
+    st.template store<0>(inb, inb + PB, gn, tid, x0, W);
+    st.template load<1>(a, b, y0, x0, tid);
+  }
+  __syncthreads();
+  int par = 0;
+  const int hi = lane >> 5, col = lane & 31;
+  for (; tile < ntiles; tile += gridDim.x) {
+    coords(tile, b, y0, x0);
+    const int next = tile + (int)gridDim.x;
+    int nb = 0, ny0 = 0, nx0 = 0;
+    if (next < ntiles) coords(next, nb, ny0, nx0);
+    const int yw = y0 + wave * RW;   // this wave's first row
+    const int x = x0 + col;
+    floatx16 acc[MT][RW];
+    float cst[MT][RW][4];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[m][r][j] = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int y = yw + r, ch = m * 8 + 4 * hi + q;
+          cst[m][r][q] = (y < H && x < W) ? a.c[(((size_t)b * HID + ch) * H + y) * W + x] : 0.f;
+        }
+      }
+    auto step = [&](auto CHc) {
+      constexpr int CH = decltype(CHc)::value;
+      constexpr bool F_NEXT = CH + 1 >= NCHK;   // following chunk: the next tile's first
+      constexpr int F = F_NEXT ? 0 : CH + 1;
+      constexpr bool A_NEXT = CH + 2 >= NCHK;   // the chunk after it
+      constexpr int AC = A_NEXT ? CH + 2 - NCHK : CH + 2;
+      const char* cur = inb + 2 * par * PB;
+      char* oth = inb + 2 * (par ^ 1) * PB;
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH>(acc, wl_hi, wl_lo, cur, cur + PB, wave, lane);
+      if (!(ABL & 2)) {
+        if (!F_NEXT || next < ntiles) st.template store<F>(oth, oth + PB, gn, tid, 0, W);
+        if (!A_NEXT)
+          st.template load<AC>(a, b, y0, x0, tid);
+        else if (next < ntiles)
+          st.template load<AC>(a, nb, ny0, nx0, tid);
+      }
+      if constexpr (CH == NCHK - 1) {
+        // epilogue: LSTM gates (module.py:83-90); undo the weight scale, add the bias
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          const int y = yw + r;
+          if (y < H && x < W) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const int ch = m * 8 + 4 * hi + q;
+                const float gi = fmaf(acc[m][r][q], inv_scale, a.bias[ch]);
+                const float gf = fmaf(acc[m][r][4 + q], inv_scale, a.bias[HID + ch]);
+                const float go = fmaf(acc[m][r][8 + q], inv_scale, a.bias[2 * HID + ch]);
+                const float gg = fmaf(acc[m][r][12 + q], inv_scale, a.bias[3 * HID + ch]);
+                const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
+                if (ABL & 4) {
+                  a.c[idx] = gi + gf;
+                  a.h_new[idx] = go + gg + cst[m][r][q];
+                  continue;
+                }
+                const float cn = fast_sigmoid(gf) * cst[m][r][q] + fast_sigmoid(gi) * fast_tanh(gg);
+                a.c[idx] = cn;
+                a.h_new[idx] = fast_sigmoid(go) * fast_tanh(cn);
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();   // buffer `oth` staged; buffer `cur` free for the step after next
+      par ^= 1;
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    if constexpr (NCHK > 2) step(std::integral_constant<int, 2>{});
+  }
+}
+
+// DB: 1 double-buffered kernel, 0 single-buffered; per cell in CellDef (measured at the
+// headline geometry: double buffering wins on the 48-channel cells 0 and 3 and loses
+// where the second buffer costs occupancy or the chunks are few)
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int STG = 1,
+          int ABL = 0, int DB = CellDef<KIND>::H3DB>
 static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu, int kid,
                               hipStream_t s) {
   using C = H3Cfg<KIND, RW, WAVES>;
-  static_assert(C::LDS_BYTES <= 160 * 1024, "h3 cell tile exceeds LDS");
+  constexpr size_t lds = C::LDS_BYTES + (DB ? (size_t)C::NPIX * 32 * 2 : 0);
+  static_assert(lds <= 160 * 1024, "h3 cell tile exceeds LDS");
   static_assert(C::NS <= 32 && C::NH <= 32, "staging masks hold 32 items");
+  const void* fn = DB ? (const void*)lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL>
+                      : (const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, STG, ABL>;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, STG>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)C::LDS_BYTES);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int ntiles = a.B * ((a.W + C::TW - 1) / C::TW) * ((a.H + C::TH - 1) / C::TH);
-  const int per_cu = std::max(1, (int)((160 * 1024) / C::LDS_BYTES));
+  const int per_cu = std::max(1, (int)((160 * 1024) / lds));
   const int grid = std::max(1, std::min(ntiles, cu * per_cu));
   ProfScope ps(s, kid);
-  hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, STG>), dim3(grid), dim3(C::THREADS),
-                     C::LDS_BYTES, s, a, inv_scale);
+  if (DB)
+    hipLaunchKernelGGL((lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL>), dim3(grid), dim3(C::THREADS),
+                       lds, s, a, inv_scale);
+  else
+    hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, STG, ABL>), dim3(grid),
+                       dim3(C::THREADS), lds, s, a, inv_scale);
   return hipGetLastError();
 }
 

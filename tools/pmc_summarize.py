@@ -16,13 +16,16 @@ from collections import defaultdict
 
 SHORT = [("cost_x_kernel", "cost_x"), ("omega_conv_kernel", "omega_conv"),
          ("omega_stats_kernel<1>", "omega_stats1"),
-         ("omega_stats_kernel<2>", "omega_stats2"), ("lstm_cell_h3_kernel<0,", "lstm_cell0"),
-         ("lstm_cell_h3_kernel<1,", "lstm_cell1"), ("lstm_cell_h3_kernel<2,", "lstm_cell2"),
-         ("lstm_cell_h3_kernel<3,", "lstm_cell3"), ("lstm_cell_h3_kernel<4,", "lstm_cell4"),
-         ("deconv_kernel", "deconv"), ("head_wta", "head_wta"), ("nchw_to_c8", "to_c8")]
+         ("omega_stats_kernel<2>", "omega_stats2"), ("deconv_kernel", "deconv"), ("head_wta", "head_wta"), ("nchw_to_c8", "to_c8")]
+
+
+CELL = re.compile(r"lstm_cell_h3(?:db)?_kernel<(\d),")
 
 
 def short(name):
+    m = CELL.search(name)
+    if m:
+        return "lstm_cell" + m.group(1)
     for key, s in SHORT:
         if key in name:
             return s
