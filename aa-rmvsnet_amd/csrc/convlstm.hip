@@ -624,7 +624,7 @@ struct H3Stager {
 // (8 channels as fp16 pairs) at h3_pix(p, h): 2-way bank conflicts at most, where the
 // segment stager above writes 4-B pairs 128 B apart (32-way).  Out-of-image pixels and
 // channels past the chunk's valid count load zeros through the buffer range check.
-template <int KIND, int RW, int WAVES>
+template <int KIND, int RW, int WAVES, int NHWC = 0>
 struct H3PixStager {
   using C = H3Cfg<KIND, RW, WAVES>;
   using D = typename C::D;
@@ -656,6 +656,25 @@ struct H3PixStager {
       if (in) in_mask |= 1u << j;
       const uint32_t pix = MODE == SRC_POOL ? (uint32_t)(2 * gy * Ws + 2 * gx) : (uint32_t)(gy * W + gx);
       const uint32_t base = (uint32_t)(LC0 + 8 * h) * plane + pix * 4u;
+      if constexpr (NHWC) {
+        // [B][Hs][Ws][NCH]: the item's 8 channels are 32 contiguous bytes
+        const uint32_t ob = (pix * (uint32_t)NCH + (uint32_t)(LC0 + 8 * h)) * 4u;
+        constexpr int NW = MODE == SRC_POOL ? 4 : 1;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const uint32_t o = in ? ob + (uint32_t)(((w >> 1) * Ws + (w & 1)) * NCH * 4) : nbytes;
+          const float4 q0 = ld4(r, o), q1 = ld4(r, in ? o + 16u : nbytes);
+          val[j][0][w] = q0.x;
+          val[j][1][w] = q0.y;
+          val[j][2][w] = q0.z;
+          val[j][3][w] = q0.w;
+          val[j][4][w] = q1.x;
+          val[j][5][w] = q1.y;
+          val[j][6][w] = q1.z;
+          val[j][7][w] = q1.w;
+        }
+        continue;
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const uint32_t off = in ? base + (uint32_t)k * plane : nbytes;
@@ -708,32 +727,71 @@ struct H3PixStager {
   }
 };
 
-template <class C, int CH>
+// One input chunk's MFMAs: 9 taps x MT m-tiles x RW rows x 3 split products.  PIPE
+// (microbenchmark variant): the A/B fragments of tap t+1 are read from LDS into a second
+// register set before tap t's MFMAs issue.  The compiler's own schedule reads each tap's
+// fragments just before use; measured equal on cells 0-3 (the other wave of the SIMD
+// covers the LDS latency) and 18% slower on cell 4, whose extra VGPRs cost occupancy.
+template <class C, int CH, bool PIPE = false>
 __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], const char* wl_hi,
                                               const char* wl_lo, const char* in_hi,
                                               const char* in_lo, int wave, int lane) {
   constexpr int MT = C::MT, RW = C::RW;
   const int col = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
-    half8 bh[RW], bl[RW];
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      const int p = (wave * RW + r + tap / 3) * C::W2 + col + tap % 3;
-      const int boff = h3_pix(p, h);
-      bh[r] = *reinterpret_cast<const half8*>(in_hi + boff);
-      bl[r] = *reinterpret_cast<const half8*>(in_lo + boff);
-    }
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int aoff = ((((CH * 9 + tap) * MT + m) * 64) + lane) * 16;
-      const half8 ah = *reinterpret_cast<const half8*>(wl_hi + aoff);
-      const half8 al = *reinterpret_cast<const half8*>(wl_lo + aoff);
+  if constexpr (PIPE) {
+    half8 bh[2][RW], bl[2][RW], ah[2][MT], al[2][MT];
+    auto fetch = [&](int tap, int s) {
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
-        acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[r], acc[m][r], 0, 0, 0);
-        acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[r], acc[m][r], 0, 0, 0);
-        acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[r], acc[m][r], 0, 0, 0);
+        const int boff = h3_pix((wave * RW + r + tap / 3) * C::W2 + col + tap % 3, h);
+        bh[s][r] = *reinterpret_cast<const half8*>(in_hi + boff);
+        bl[s][r] = *reinterpret_cast<const half8*>(in_lo + boff);
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int aoff = ((((CH * 9 + tap) * MT + m) * 64) + lane) * 16;
+        ah[s][m] = *reinterpret_cast<const half8*>(wl_hi + aoff);
+        al[s][m] = *reinterpret_cast<const half8*>(wl_lo + aoff);
+      }
+    };
+    fetch(0, 0);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int s = tap & 1;
+      if (tap + 1 < 9) fetch(tap + 1, s ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s][m], bh[s][r], acc[m][r], 0, 0, 0);
+          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s][m], bl[s][r], acc[m][r], 0, 0, 0);
+          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s][m], bh[s][r], acc[m][r], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      half8 bh[RW], bl[RW];
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const int p = (wave * RW + r + tap / 3) * C::W2 + col + tap % 3;
+        const int boff = h3_pix(p, h);
+        bh[r] = *reinterpret_cast<const half8*>(in_hi + boff);
+        bl[r] = *reinterpret_cast<const half8*>(in_lo + boff);
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int aoff = ((((CH * 9 + tap) * MT + m) * 64) + lane) * 16;
+        const half8 ah = *reinterpret_cast<const half8*>(wl_hi + aoff);
+        const half8 al = *reinterpret_cast<const half8*>(wl_lo + aoff);
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[r], acc[m][r], 0, 0, 0);
+          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[r], acc[m][r], 0, 0, 0);
+          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[r], acc[m][r], 0, 0, 0);
+        }
       }
     }
   }
@@ -741,7 +799,8 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], con
 
 // STG: 1 pixel-major staging (H3PixStager, the library's), 0 segment staging (H3Stager;
 // kept for the cell microbenchmark's comparison).  ABL: ablation bits for the
-// microbenchmark only (1 no MFMA, 2 no staging loads/stores, 4 no gate math)
+// microbenchmark only (1 no MFMA, 2 no staging loads/stores, 4 no gate math, 8 the
+// software-pipelined fragment reads)
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int STG = 1,
           int ABL = 0>
 __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
@@ -785,7 +844,8 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     y0 = (rem / tiles_x) * C::TH;
     x0 = (rem % tiles_x) * C::TW;
   };
-  typename std::conditional<STG == 1, H3PixStager<KIND, RW, WAVES>, H3Stager<KIND, RW, WAVES>>::type st;
+  typename std::conditional<STG >= 1, H3PixStager<KIND, RW, WAVES, STG == 2>,
+                            H3Stager<KIND, RW, WAVES>>::type st;
   int tile = blockIdx.x;
   if (tile < ntiles && !(ABL & 2)) {
     int b, y0, x0;
@@ -831,7 +891,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
               cst[m][r][q] = (y < H && x < W) ? a.c[(((size_t)b * HID + ch) * H + y) * W + x] : 0.f;
             }
       }
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, (ABL & 8) != 0>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
     };
     chunk(std::integral_constant<int, 0>{});
     if constexpr (NCHK > 1) chunk(std::integral_constant<int, 1>{});
@@ -874,7 +934,8 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
 // (this tile's next, or the next tile's first) into buffer par ^ 1; issue the loads of
 // the chunk after that; at a tile's last chunk, the gate epilogue.  Across the two
 // waves of a SIMD one wave's staging VALU work fills the other's MFMA issue gaps.
-template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0>
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
+          int STG = 1>
 __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
@@ -917,7 +978,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
   };
   int tile = blockIdx.x;
   if (tile >= ntiles) return;   // whole block
-  H3PixStager<KIND, RW, WAVES> st;
+  H3PixStager<KIND, RW, WAVES, STG == 2> st;
   int b, y0, x0;
   coords(tile, b, y0, x0);
   if (!(ABL & 2)) st.template load<0>(a, b, y0, x0, tid);
@@ -958,7 +1019,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
       constexpr int AC = A_NEXT ? CH + 2 - NCHK : CH + 2;
       const char* cur = inb + 2 * par * PB;
       char* oth = inb + 2 * (par ^ 1) * PB;
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH>(acc, wl_hi, wl_lo, cur, cur + PB, wave, lane);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, (ABL & 8) != 0>(acc, wl_hi, wl_lo, cur, cur + PB, wave, lane);
       if (!(ABL & 2)) {
         if (!F_NEXT || next < ntiles) st.template store<F>(oth, oth + PB, gn, tid, 0, W);
         if (!A_NEXT)
@@ -1015,7 +1076,7 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
   constexpr size_t lds = C::LDS_BYTES + (DB ? (size_t)C::NPIX * 32 * 2 : 0);
   static_assert(lds <= 160 * 1024, "h3 cell tile exceeds LDS");
   static_assert(C::NS <= 32 && C::NH <= 32, "staging masks hold 32 items");
-  const void* fn = DB ? (const void*)lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL>
+  const void* fn = DB ? (const void*)lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, STG>
                       : (const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, STG, ABL>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1028,7 +1089,7 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
   const int grid = std::max(1, std::min(ntiles, cu * per_cu));
   ProfScope ps(s, kid);
   if (DB)
-    hipLaunchKernelGGL((lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL>), dim3(grid), dim3(C::THREADS),
+    hipLaunchKernelGGL((lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, STG>), dim3(grid), dim3(C::THREADS),
                        lds, s, a, inv_scale);
   else
     hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, STG, ABL>), dim3(grid),

@@ -80,6 +80,16 @@ int main() {
   run("cell1 h3 double-buffered", [&] { return run_cell_h3<1, 1, 8, 1, 0, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
   run("cell3 h3 single-buffered", [&] { return run_cell_h3<3, 1, 8, 1, 0, 0>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
   run("cell4 h3 double-buffered", [&] { return run_cell_h3<4, 1, 8, 1, 0, 1>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+  run("cell0 h3 pipelined frags (8)", [&] { return run_cell_h3<0, 1, 8, 1, 8>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell1 h3 pipelined frags (8)", [&] { return run_cell_h3<1, 1, 8, 1, 8>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell3 h3 pipelined frags (8)", [&] { return run_cell_h3<3, 1, 8, 1, 8>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+  run("cell4 h3 pipelined frags (8)", [&] { return run_cell_h3<4, 1, 8, 1, 8>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+  run("cell0 h3 NHWC staging", [&] { return run_cell_h3<0, 1, 8, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell1 h3 NHWC staging", [&] { return run_cell_h3<1, 1, 8, 2>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell3 h3 NHWC staging", [&] { return run_cell_h3<3, 1, 8, 2>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+  run("cell4 h3 NHWC staging", [&] { return run_cell_h3<4, 1, 8, 2>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+  run("cell4 h3 NHWC staging, DB", [&] { return run_cell_h3<4, 1, 8, 2, 0, 1>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+  run("cell0 h3 NHWC no MFMA", [&] { return run_cell_h3<0, 1, 8, 2, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 no MFMA (1)", [&] { return run_cell_h3<0, 1, 8, 1, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 no staging (2)", [&] { return run_cell_h3<0, 1, 8, 1, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 MFMA only (6)", [&] { return run_cell_h3<0, 1, 8, 1, 6>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
