@@ -42,6 +42,10 @@ const ParamLayout& param_layout() {
     pk += 64;
     l.ow0t_off = pk;
     pk += 4 * 32 * 9;
+    l.owb_off = pk;
+    pk += 4 * 5 * 64 * 8 / 2;   // halves -> floats
+    l.owb_scale_off = pk;
+    pk += 64;
     l.raw_total = raw;
     l.pk_total = pk;
     return l;
@@ -228,14 +232,47 @@ __global__ void __launch_bounds__(256) pack_cell_h3_kernel(const float* __restri
 }
 
 // omega conv3x3 32->4 weights [co][ci][tap] -> [tap][ci][co]: the 16 weights of one
-// (tap, 4-channel group) are contiguous (one s_load_dwordx16 in the pipeline's conv)
+// (tap, 4-channel group) are contiguous (scalar loads in the VALU form of the conv)
+// and -> split-fp16 B fragments of v_mfma_f32_16x16x32_f16 for omega_conv's MFMA conv:
+// per 8-channel chunk c, K = [a_hi taps 0..8 | a_lo taps 0..8] x 8 channels (k8 group
+// q = 9 s + tap, 18 groups, padded to 20 = 5 MFMAs of K 32), N = 16 columns
+// n = co + 4 ws (ws: weight hi / lo part; columns 8..15 zero).  Lane l of MFMA j holds
+// B[k8 group 4 j + l / 16][n = l % 16] (8 halves).  A power-of-two scale keeps the
+// weights in fp16's normal range (undone in the kernel's epilogue).
 __global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __restrict__ pk,
                                        ParamLayout L) {
+  __shared__ float red[4];
   const float* w = raw + L.raw_off[P_OW0];
   float* d = pk + L.ow0t_off;
+  float mx = 0.f;
   for (int i = threadIdx.x; i < 4 * 32 * 9; i += blockDim.x) {
     const int co = i % 4, ci = (i / 4) % 32, tap = i / 128;
     d[i] = w[(co * 32 + ci) * 9 + tap];
+    mx = fmaxf(mx, fabsf(d[i]));
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  int e = 0;
+  if (mx > 0.f) {
+    e = (int)floorf(log2f(16384.0f / mx));
+    e = e < -20 ? -20 : (e > 20 ? 20 : e);
+  }
+  const float sc = ldexpf(1.0f, e);
+  if (threadIdx.x == 0) pk[L.owb_scale_off] = ldexpf(1.0f, -e);
+  _Float16* b = reinterpret_cast<_Float16*>(pk + L.owb_off);
+  for (int i = threadIdx.x; i < 4 * 5 * 64 * 8; i += blockDim.x) {
+    const int ci8 = i & 7, lane = (i >> 3) & 63, j = (i >> 9) % 5, c = (i >> 9) / 5;
+    const int q = 4 * j + (lane >> 4), n = lane & 15;
+    float v = 0.f;
+    if (q < 18 && n < 8) {
+      const int tap = q % 9, co = n & 3;
+      const float x = w[(co * 32 + 8 * c + ci8) * 9 + tap] * sc;
+      const _Float16 xh = (_Float16)x;
+      v = (n < 4) ? (float)xh : (float)(_Float16)(x - (float)xh);
+    }
+    b[i] = (_Float16)v;
   }
 }
 

@@ -175,6 +175,7 @@ struct PipeArgs {
   float* x;                   // [B,32,H,W]
   float* omega_out;           // [nsrc,B,H,W] (prev plane) or null
   const float* params;
+  size_t off_owb, off_owb_scale;   // omega conv MFMA B fragments, their scale
   size_t off_ow0t, off_ow0, off_ob0, off_og0w, off_og0b, off_ow1, off_ob1, off_og1w, off_og1b, off_ow2,
       off_ob2, off_og2w, off_og2b, off_owo, off_obo;
   int B, H, W, nsrc;
@@ -476,6 +477,21 @@ __device__ __forceinline__ void img_st(float* img, uint32_t p, int h, float4 v) 
 // the half of pixel p held in slot s of its image: slot ^ swizzle bit
 __device__ __forceinline__ int img_half(uint32_t p, int s) { return s ^ (int)((p >> 3) & 1u); }
 
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// split-fp16 sq image (MFMA A operand): channels 4h..4h+3 of pixel p as fp16 hi parts in
+// the hi plane and fp16(v - hi) in the lo plane, [plane][pixel][8 channels]
+__device__ __forceinline__ void sq_st16(_Float16* img, uint32_t p, int h, float4 v) {
+  constexpr uint32_t NHP = kCHH * kCHW;
+  const half4 hi = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+  const half4 lo = {(_Float16)(v.x - (float)hi.x), (_Float16)(v.y - (float)hi.y),
+                    (_Float16)(v.z - (float)hi.z), (_Float16)(v.w - (float)hi.w)};
+  *reinterpret_cast<half4*>(img + p * 8u + 4u * (uint32_t)h) = hi;
+  *reinterpret_cast<half4*>(img + NHP * 8u + p * 8u + 4u * (uint32_t)h) = lo;
+}
+
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 // LDS-DMA, 16 B per lane: lane l of the wave lands at wave_dst + 16 l (wave_dst uniform);
 // an offset past the buffer's range loads zeros
@@ -491,13 +507,19 @@ __device__ __forceinline__ void dma_wait() {
 // (8+2) x 34 reference tile arrive in LDS by LDS-DMA, issued while the previous chunk's
 // conv runs; the squared difference on the haloed tile goes to the sq image (own pixel
 // by every thread, ring pixels by threads 0..kCRing-1); each thread accumulates its
-// pixel's conv3x3 32->4 over the chunks.  A box past kCBoxPx pixels is sampled from
-// global memory instead.
+// pixel's conv3x3 32->4 over the chunks (fmaf chains, scalar weights, taps unrolled).
+// A box past kCBoxPx pixels is sampled from global memory instead.
 // ABL: ablation bits for the diagnostic harness only (tools/microbench/pipe_bench.cpp;
-// the library instantiates ABL = 0): 1 no conv FMAs, 2 no squared differences, 4 no box
-// loads, 8 conv tap loop rolled.
+// the library instantiates ABL = 0): 1 no conv, 2 no squared differences, 4 no box
+// loads, 8 conv tap loop rolled, 16 the conv on the matrix cores: an implicit GEMM per
+// chunk, M = 16 pixels of a tile row, K = 9 taps x 8 channels x {sq hi, sq lo} (split
+// fp16 sq image), N = 4 output channels x {w hi, w lo}, v_mfma_f32_16x16x32_f16 (all four
+// split products, fp32 accumulation).  Measured slower (0.90 vs 0.74 ms per plane): the
+// A fragments re-read every pixel once per tap from LDS, 1 KiB per MFMA, which saturates
+// the LDS at 16 cycles per MFMA on four SIMDs; the parity tests pass on it.
 template <int ABL = 0>
-__global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
+__global__ void __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(4)))
+omega_conv_kernel(PipeArgs a,
                                                                   const float* __restrict__ P,
                                                                   const float* __restrict__ Rel) {
   constexpr int NHP = kCHH * kCHW;                                      // haloed tile pixels
@@ -601,6 +623,24 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
   };
   const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]
   const float* __restrict__ b0 = P + a.off_ob0;
+  // MFMA conv: this lane's A rows (pixel i = lane & 15 of the wave's four 16-pixel row
+  // tiles) and k8 groups (q = 4 j + lane / 16 of MFMA j: plane q / 9, tap q % 9; the two
+  // padding groups re-read group 17 against zero weights)
+  constexpr bool MF = (ABL & 16) != 0;
+  _Float16* sqh = reinterpret_cast<_Float16*>(sqt);   // [hi plane | lo plane][NHP][8]
+  const half8* __restrict__ owb = reinterpret_cast<const half8*>(P + a.off_owb);
+  uint32_t mrow[4], koff[5];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    mrow[t] = (uint32_t)(((2 * wave + (t >> 1) + 1) * kCHW + 16 * (t & 1) + (lane & 15) + 1) * 16);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int q = min(4 * j + (lane >> 4), 17), tap = q % 9;
+    koff[j] = (uint32_t)((q / 9) * NHP * 16 + ((tap / 3 - 1) * kCHW + (tap % 3 - 1)) * 16);
+  }
+  floatx4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   stage(0);
   dma_wait();
@@ -610,8 +650,14 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
   for (int c = 0; c < 4; ++c) {
 #pragma unroll
     for (int h = 0; h < 2 && !(ABL & 2); ++h) {
-      img_st(sqt, own_hp, h, sqdiff4(sample(to, c, h), img_ld(rt, own_hp, h)));
-      if (has_ring) img_st(sqt, ring_hp, h, sqdiff4(sample(tr, c, h), img_ld(rt, ring_hp, h)));
+      const float4 so = sqdiff4(sample(to, c, h), img_ld(rt, own_hp, h));
+      if (MF) sq_st16(sqh, own_hp, h, so);
+      else img_st(sqt, own_hp, h, so);
+      if (has_ring) {
+        const float4 sr = sqdiff4(sample(tr, c, h), img_ld(rt, ring_hp, h));
+        if (MF) sq_st16(sqh, ring_hp, h, sr);
+        else img_st(sqt, ring_hp, h, sr);
+      }
     }
     __syncthreads();   // sq visible; this chunk's box / reference reads are done
     if (c < 3) stage(c + 1);
@@ -628,10 +674,22 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
     };
     // fully unrolled: the LDS reads and weight loads of later taps are issued ahead
     // (0.72 vs 0.82 ms per plane at the headline geometry with a rolled loop)
-    if constexpr (ABL & 8) {
+    if constexpr (ABL & 1) {
+    } else if constexpr (MF) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const half8 bf = owb[(c * 5 + j) * 64 + lane];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const half8 af = *reinterpret_cast<const half8*>(
+              reinterpret_cast<const char*>(sqh) + mrow[t] + koff[j]);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc[t], 0, 0, 0);
+        }
+      }
+    } else if constexpr ((ABL & 8) != 0) {
 #pragma unroll 1
       for (int tap = 0; tap < 9; ++tap) conv_tap(tap);
-    } else if constexpr (!(ABL & 1)) {
+    } else {
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) conv_tap(tap);
     }
@@ -639,6 +697,29 @@ __global__ void __launch_bounds__(kTileThreads) omega_conv_kernel(PipeArgs a,
       dma_wait();
       __syncthreads();   // next chunk's images visible; the conv's sq reads are done
     }
+  }
+  if constexpr (MF) {
+    // D[row = 4 (lane / 16) + r][col = lane % 16] of row tile t -> LDS [pixel][8] (cols
+    // 0..3: x w_hi, 4..7: x w_lo), then every thread sums its own pixel's parts.  The box
+    // image is free: its last reads were chunk 3's sq phase.
+    float* dt = box;
+    if ((lane & 15) < 8) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int px = (2 * wave + (t >> 1)) * kTileW + 16 * (t & 1) + 4 * (lane >> 4) + r;
+          dt[px * 8 + (lane & 15)] = acc[t][r];
+        }
+    }
+    __syncthreads();
+    const float4 d0 = *reinterpret_cast<const float4*>(&dt[tid * 8]);
+    const float4 d1 = *reinterpret_cast<const float4*>(&dt[tid * 8 + 4]);
+    const float isc = P[a.off_owb_scale];
+    o4[0] = (d0.x + d1.x) * isc;
+    o4[1] = (d0.y + d1.y) * isc;
+    o4[2] = (d0.z + d1.z) * isc;
+    o4[3] = (d0.w + d1.w) * isc;
   }
   float ps = 0.f, pss = 0.f;
   if (inside) {
@@ -722,6 +803,8 @@ static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspac
   a.box_cap = INT_MAX;
   a.off_ow0 = L.pk_off[P_OW0];
   a.off_ow0t = L.ow0t_off;
+  a.off_owb = L.owb_off;
+  a.off_owb_scale = L.owb_scale_off;
   a.off_ob0 = L.pk_off[P_OB0];
   a.off_og0w = L.pk_off[P_OG0W];
   a.off_og0b = L.pk_off[P_OG0B];
