@@ -204,13 +204,14 @@ class DepthSweep:
         hid = (16, 16, 16, 16, 8)[cell]
         sc = (1, 2, 4, 2, 1)[cell]
         off = ptr - ws.data_ptr()
+        # stored NHWC (include/aarmvs.h); returned as the reference's NCHW view
         return ws[off: off + B * hid * (H // sc) * (W // sc) * 4].view(torch.float32).view(
-            B, hid, H // sc, W // sc)
+            B, H // sc, W // sc, hid).permute(0, 3, 1, 2)
 
     def snapshot_state(self, B, H, W, nsrc, parity):
         """Copies of the regulariser's (h, c) per cell as left for the plane of `parity`."""
-        return [[self.state(B, H, W, nsrc, parity, k, 0).clone(),
-                 self.state(B, H, W, nsrc, parity, k, 1).clone()] for k in range(5)]
+        return [[self.state(B, H, W, nsrc, parity, k, 0).contiguous().clone(),
+                 self.state(B, H, W, nsrc, parity, k, 1).contiguous().clone()] for k in range(5)]
 
     def unet_step(self, x: torch.Tensor, step: int, nsrc: int = 1) -> torch.Tensor:
         _require_device(x)

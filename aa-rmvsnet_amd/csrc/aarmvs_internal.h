@@ -114,6 +114,9 @@ struct CostArgs {
 // and plane d's statistics; omega_next produces t1 and the three GroupNorm statistics of
 // plane d (omega_conv + omega_stats<1> + <2>).  The statistics of a plane must be zero
 // before its omega_next and are cleared by the caller once its cost_x has run.
+// NCHW <-> NHWC copy of a [B][C][HW] / [B][HW][C] fp32 tensor (API edges only)
+hipError_t launch_layout(const float* in, float* out, int B, int C, int HW, bool to_nhwc,
+                         hipStream_t s);
 hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s);
 hipError_t launch_cost_x(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d,
                          float* omega_out, hipStream_t s);

@@ -479,8 +479,7 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     if (aux && (e = hipEventRecord(ev_main[d & 1], stream)) != hipSuccess)
       return sweep_fail(e, "sweep: event record");
     if (last && a->slice_out) {
-      e = hipMemcpyAsync(a->slice_out, ws.x, (size_t)a->B * kC * a->H * a->W * 4,
-                         hipMemcpyDeviceToDevice, stream);
+      e = launch_layout(ws.x, a->slice_out, a->B, kC, a->H * a->W, false, stream);
       if (e != hipSuccess) return sweep_fail(e, "sweep: slice copy");
     }
     if ((e = launch_unet_step(ws.x, params, g, ws, d & 1, stream)) != hipSuccess)
@@ -517,7 +516,10 @@ int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
     return hip_fail(e, "unet_step: state init");
   if ((e = hipMemsetAsync(ws.reg_stats, 0, ws.reg_stats_bytes, stream)) != hipSuccess)
     return hip_fail(e, "unet_step: stats reset");
-  if ((e = launch_unet_step(x, params, g, ws, step & 1, stream)) != hipSuccess)
+  // the workspace's slice buffer holds x as NHWC, like the sweep's cost slice
+  if ((e = launch_layout(x, ws.x, B, kC, H * W, true, stream)) != hipSuccess)
+    return hip_fail(e, "unet_step: x layout");
+  if ((e = launch_unet_step(ws.x, params, g, ws, step & 1, stream)) != hipSuccess)
     return hip_fail(e, "unet_step");
   // head conv only (no WTA): cost_out is [B,1,H,W] == [B,D=1,H,W] at plane 0
   if ((e = launch_head_wta(params, g, ws, step & 1, nullptr, 0, cost_out, false, stream)) !=

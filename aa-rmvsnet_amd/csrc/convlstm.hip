@@ -1,18 +1,18 @@
 // Recurrent regulariser step (UNetConvLSTM, models/drmvsnet.py:119-167) for gfx950.
 //
-// ConvLSTM cell (models/module.py:76-92) = implicit-GEMM 3x3 conv on the fp32
-// matrix cores (v_mfma_f32_32x32x2_f32, exact f32 FMA chain) with the LSTM gate
-// math fused into the epilogue:
+// ConvLSTM cell (models/module.py:76-92) = implicit-GEMM 3x3 conv on the matrix cores
+// (split-fp16 v_mfma_f32_32x32x16_f16, below) with the LSTM gate math fused into the
+// epilogue:
 //   M = 4*hid output channels (gates i,f,o,g), N = pixels, K = 9 taps x Cin.
 //   One m-tile = 32 rows = the 4 gates of 8 hidden channels, so every lane holds
 //   i,f,o,g of the same (pixel, channel) in its accumulator registers and the
 //   c/h update needs no data exchange.
-//   A (weights) and the haloed input tile live in LDS; B operands are read
-//   straight from the tile (lanes 0-31: 32 consecutive pixels, lanes 32-63: the
-//   next channel), conflict-free ds_read_b32.
+//   A (weights) and the haloed input tile live in LDS.
 // Input staging fuses the U-Net glue: 2x2 max-pool (drmvsnet.py:148,152),
 // GroupNorm(2,16)+ReLU of the deconv output (module.py:286-287) and the channel
 // concatenations (drmvsnet.py:80, 157, 161).
+// Layout: every U-Net tensor in the workspace (the cost slice x, h and c of each cell,
+// the deconv outputs) is NHWC, [B][H][W][C] fp32.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -56,15 +56,15 @@ template <>
 struct CellDef<0> {   // [x, h0] @ H
   static constexpr int NP = 2, CH[kMaxParts] = {32, 16, 0};
   static constexpr int MODE[kMaxParts] = {SRC_PLAIN, SRC_PLAIN, SRC_PLAIN};
-  static constexpr int HID = 16, TH = 4, NT = 1;
-  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1;
+  static constexpr int HID = 16;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1, H3PIPE = 1;
 };
 template <>
 struct CellDef<1> {   // [maxpool(h0'), h1] @ H/2
   static constexpr int NP = 2, CH[kMaxParts] = {16, 16, 0};
   static constexpr int MODE[kMaxParts] = {SRC_POOL, SRC_PLAIN, SRC_PLAIN};
-  static constexpr int HID = 16, TH = 8, NT = 1;
-  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 0;
+  static constexpr int HID = 16;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1, H3PIPE = 1;
 };
 template <>
 struct CellDef<2> : CellDef<1> {};   // [maxpool(h1'), h2] @ H/4
@@ -72,358 +72,25 @@ template <>
 struct CellDef<3> {   // [gnrelu(u0), h1', h3] @ H/2
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 16};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
-  static constexpr int HID = 16, TH = 4, NT = 1;
-  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1;
+  static constexpr int HID = 16;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 0, H3PIPE = 1;
 };
 template <>
 struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 8};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
-  static constexpr int HID = 8, TH = 8, NT = 1;
-  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 0;
+  static constexpr int HID = 8;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 0, H3PIPE = 0;
 };
-
-template <int KIND>
-struct CellCfg {
-  using D = CellDef<KIND>;
-  static constexpr int CIN = D::CH[0] + D::CH[1] + D::CH[2];
-  static constexpr int HID = D::HID, TH = D::TH, NT = D::NT;
-  static constexpr int MT = HID / 8;
-  static constexpr int COUT = 4 * HID;
-  static constexpr int CP = CIN / 2;            // k-steps per tap
-  static constexpr int TW = 32 * NT;            // tile width (pixels)
-  // LDS row: [pad pad pad halo | TW interior (16-B aligned) | halo pad pad pad]
-  static constexpr int LEFT = 4;                 // interior starts at column 4
-  static constexpr int W2 = TW + 8, TROWS = TH + 2;
-  static constexpr int SEGS = TW / 4;            // float4 segments of an interior row
-  static constexpr int PLANE = TROWS * W2;       // one channel of the haloed tile
-  static constexpr int IN_FLOATS = CIN * PLANE;
-  static constexpr int W_FLOATS = COUT * 9 * CIN;
-  static constexpr int THREADS = TH * 64;
-  static constexpr size_t LDS_BYTES = (size_t)(W_FLOATS + IN_FLOATS + 32) * 4;
-  static constexpr int c0(int p) { return p == 0 ? 0 : (p == 1 ? D::CH[0] : D::CH[0] + D::CH[1]); }
-};
-
-// Input staging through registers: the next tile's loads are issued before the current
-// tile's MFMA loop and land in LDS after it (one tile of prefetch, no second LDS buffer).
-// The interior of each (channel, row) is moved as float4 segments (x0 is a multiple of
-// 32 and W of 4, so they are 16-B aligned; POOL reads two float4 per fine row), the two
-// halo columns as scalars.  One register block per input part, sized exactly.
-template <int KIND, int P>
-struct PartRegs {
-  using C = CellCfg<KIND>;
-  using D = typename C::D;
-  static constexpr int MODE = D::MODE[P < D::NP ? P : 0];
-  static constexpr int NCH = P < D::NP ? D::CH[P] : 0;
-  static constexpr int SEG_ITEMS = NCH * C::TROWS * C::SEGS;   // float4 items
-  static constexpr int HALO_ITEMS = NCH * C::TROWS * 2;        // scalar items
-  static constexpr int NS = (SEG_ITEMS + C::THREADS - 1) / C::THREADS;
-  static constexpr int NH = (HALO_ITEMS + C::THREADS - 1) / C::THREADS;
-  static constexpr int WIN = MODE == SRC_POOL ? 4 : 1;   // fine-row float4 pairs x 2 rows
-  float4 seg[NS > 0 ? NS : 1][WIN];
-  float halo[NH > 0 ? NH : 1][WIN];
-  uint32_t seg_in, halo_in;   // bit j: item j lies inside the image (else zero padding)
-
-  // 4 consecutive floats at p (x .. x+3 of a row of width w): one aligned float4 when
-  // the row width is a multiple of 4, else guarded scalars (zero past the row end)
-  __device__ __forceinline__ static float4 row4(const float* p, int x, int w, bool vec) {
-    if (vec) return *reinterpret_cast<const float4*>(p);
-    float4 r;
-    r.x = p[0];
-    r.y = x + 1 < w ? p[1] : 0.f;
-    r.z = x + 2 < w ? p[2] : 0.f;
-    r.w = x + 3 < w ? p[3] : 0.f;
-    return r;
-  }
-
-  __device__ __forceinline__ void load(const ChanSrc& s, int b, int y0, int x0, int H, int W,
-                                       int tid) {
-    seg_in = halo_in = 0u;
-    const bool vec = (W & 3) == 0;   // the full-resolution W is; W/4 of a small image may not be
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const int e = tid + j * C::THREADS;
-      const int lc = e / (C::TROWS * C::SEGS), rem = e % (C::TROWS * C::SEGS);
-      const int gy = y0 - 1 + rem / C::SEGS, gx = x0 + 4 * (rem % C::SEGS);
-      if (e < SEG_ITEMS && gy >= 0 && gy < H && gx < W) {
-        seg_in |= 1u << j;
-        if (MODE == SRC_POOL) {
-          const int Ws = 2 * W;
-          const float* q = s.ptr + (((size_t)b * NCH + lc) * (2 * H) + 2 * gy) * Ws + 2 * gx;
-          seg[j][0] = row4(q, 2 * gx, Ws, vec);
-          seg[j][WIN > 1 ? 1 : 0] = row4(q + 4, 2 * gx + 4, Ws, vec);
-          seg[j][WIN > 2 ? 2 : 0] = row4(q + Ws, 2 * gx, Ws, vec);
-          seg[j][WIN > 3 ? 3 : 0] = row4(q + Ws + 4, 2 * gx + 4, Ws, vec);
-        } else {
-          seg[j][0] = row4(s.ptr + (((size_t)b * NCH + lc) * H + gy) * W + gx, gx, W, vec);
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NH; ++j) {
-      const int e = tid + j * C::THREADS;
-      const int lc = e / (C::TROWS * 2), rem = e % (C::TROWS * 2);
-      const int gy = y0 - 1 + rem / 2, gx = (rem & 1) ? x0 + C::TW : x0 - 1;
-      if (e < HALO_ITEMS && gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        halo_in |= 1u << j;
-        if (MODE == SRC_POOL) {
-          const int Ws = 2 * W;
-          const float* q = s.ptr + (((size_t)b * NCH + lc) * (2 * H) + 2 * gy) * Ws + 2 * gx;
-          halo[j][0] = q[0];
-          halo[j][WIN > 1 ? 1 : 0] = q[1];
-          halo[j][WIN > 2 ? 2 : 0] = q[Ws];
-          halo[j][WIN > 3 ? 3 : 0] = q[Ws + 1];
-        } else {
-          halo[j][0] = s.ptr[(((size_t)b * NCH + lc) * H + gy) * W + gx];
-        }
-      }
-    }
-  }
-
-  __device__ __forceinline__ static float post(float v, int lc, const float* gn) {
-    return MODE == SRC_GNRELU ? fmaxf(v * gn[lc] + gn[16 + lc], 0.0f) : v;
-  }
-
-  __device__ __forceinline__ void store(float* in, const float* gn, int tid, int x0,
-                                        int W) const {
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const int e = tid + j * C::THREADS;
-      if (e < SEG_ITEMS) {
-        const int lc = e / (C::TROWS * C::SEGS), rem = e % (C::TROWS * C::SEGS);
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (seg_in & (1u << j)) {
-          if (MODE == SRC_POOL) {
-            // 2x2 max-pool: fine rows 2gy, 2gy+1, fine columns 2gx .. 2gx+7
-            const float4 a0 = seg[j][0], a1 = seg[j][WIN > 1 ? 1 : 0];
-            const float4 c0 = seg[j][WIN > 2 ? 2 : 0], c1 = seg[j][WIN > 3 ? 3 : 0];
-            x.x = fmaxf(fmaxf(a0.x, a0.y), fmaxf(c0.x, c0.y));
-            x.y = fmaxf(fmaxf(a0.z, a0.w), fmaxf(c0.z, c0.w));
-            x.z = fmaxf(fmaxf(a1.x, a1.y), fmaxf(c1.x, c1.y));
-            x.w = fmaxf(fmaxf(a1.z, a1.w), fmaxf(c1.z, c1.w));
-          } else {
-            const float4 v = seg[j][0];
-            x = make_float4(post(v.x, lc, gn), post(v.y, lc, gn), post(v.z, lc, gn),
-                            post(v.w, lc, gn));
-          }
-          // columns past the image edge are the conv's zero padding (W % 4 != 0 only)
-          const int gx = x0 + 4 * (rem % C::SEGS);
-          if (gx + 1 >= W) x.y = 0.f;
-          if (gx + 2 >= W) x.z = 0.f;
-          if (gx + 3 >= W) x.w = 0.f;
-        }
-        *reinterpret_cast<float4*>(&in[(C::c0(P) + lc) * C::PLANE + (rem / C::SEGS) * C::W2 +
-                                       C::LEFT + 4 * (rem % C::SEGS)]) = x;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NH; ++j) {
-      const int e = tid + j * C::THREADS;
-      if (e < HALO_ITEMS) {
-        const int lc = e / (C::TROWS * 2), rem = e % (C::TROWS * 2);
-        float x = 0.0f;
-        if (halo_in & (1u << j)) {
-          if (MODE == SRC_POOL)
-            x = fmaxf(fmaxf(halo[j][0], halo[j][WIN > 1 ? 1 : 0]),
-                      fmaxf(halo[j][WIN > 2 ? 2 : 0], halo[j][WIN > 3 ? 3 : 0]));
-          else
-            x = post(halo[j][0], lc, gn);
-        }
-        in[(C::c0(P) + lc) * C::PLANE + (rem / 2) * C::W2 +
-           ((rem & 1) ? C::LEFT + C::TW : C::LEFT - 1)] = x;
-      }
-    }
-  }
-};
-
-template <int KIND>
-struct Stager {
-  using D = CellDef<KIND>;
-  PartRegs<KIND, 0> p0;
-  PartRegs<KIND, 1> p1;
-  PartRegs<KIND, 2> p2;
-  __device__ __forceinline__ void load(const CellArgs& a, int b, int y0, int x0, int tid) {
-    p0.load(a.part[0], b, y0, x0, a.H, a.W, tid);
-    p1.load(a.part[1], b, y0, x0, a.H, a.W, tid);
-    if (D::NP > 2) p2.load(a.part[2], b, y0, x0, a.H, a.W, tid);
-  }
-  __device__ __forceinline__ void store(float* in, const float* gn, int tid, int x0,
-                                        int W) const {
-    p0.store(in, gn, tid, x0, W);
-    p1.store(in, gn, tid, x0, W);
-    if (D::NP > 2) p2.store(in, gn, tid, x0, W);
-  }
-};
-
-template <int KIND>
-__global__ void __launch_bounds__(CellCfg<KIND>::THREADS) lstm_cell_kernel(CellArgs a) {
-  using C = CellCfg<KIND>;
-  using D = typename C::D;
-  constexpr int MT = C::MT, NT = C::NT, HID = C::HID;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* wl = lds;
-  float* in = lds + C::W_FLOATS;
-  float* gn = in + C::IN_FLOATS;   // [16] scale, [16] shift of the GN+ReLU part
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int H = a.H, W = a.W;
-
-  // weights -> LDS once per block (persistent over tiles); 8 float4 loads in flight
-  {
-    const float4* s = reinterpret_cast<const float4*>(a.wpk);
-    float4* d = reinterpret_cast<float4*>(wl);
-    constexpr int N4 = C::W_FLOATS / 4;
-#pragma unroll 8
-    for (int i = tid; i < N4; i += C::THREADS) d[i] = s[i];
-  }
-  // fused GroupNorm(2,16) scale/shift of the normalised part (module.py:284-287)
-#pragma unroll
-  for (int p = 0; p < D::NP; ++p) {
-    if (D::MODE[p] == SRC_GNRELU && tid < 16) {
-      const GnStat st = stat_read(a.part[p].stats + (tid >> 3) * kSlots * 2, 8.0 * H * W);
-      const float sc = st.rstd * a.part[p].gamma[tid];
-      gn[tid] = sc;
-      gn[16 + tid] = a.part[p].beta[tid] - st.mean * sc;
-    }
-  }
-
-  const int tiles_x = (W + C::TW - 1) / C::TW, tiles_y = (H + C::TH - 1) / C::TH;
-  const int ntiles = a.B * tiles_x * tiles_y;
-  auto tile_coords = [&](int tile, int& b, int& y0, int& x0) {
-    b = tile / (tiles_x * tiles_y);
-    const int rem = tile % (tiles_x * tiles_y);
-    y0 = (rem / tiles_x) * C::TH;
-    x0 = (rem % tiles_x) * C::TW;
-  };
-
-  Stager<KIND> st;
-  int tile = blockIdx.x;
-  if (tile < ntiles) {
-    int b, y0, x0;
-    tile_coords(tile, b, y0, x0);
-    st.load(a, b, y0, x0, tid);
-  }
-  const int hi = lane >> 5, col = lane & 31;
-  for (; tile < ntiles; tile += gridDim.x) {
-    int b, y0, x0;
-    tile_coords(tile, b, y0, x0);
-    __syncthreads();   // previous tile's MFMA reads done (and weights / gn visible)
-    st.store(in, gn, tid, x0, W);
-    __syncthreads();
-    if (tile + (int)gridDim.x < ntiles) {   // prefetch the next tile during the MFMAs
-      int nb, ny0, nx0;
-      tile_coords(tile + gridDim.x, nb, ny0, nx0);
-      st.load(a, nb, ny0, nx0, tid);
-    }
-    // cell state of this lane's outputs, needed by the epilogue
-    const int y = y0 + wave;
-    float cst[MT][NT][4];
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int x = x0 + nt * 32 + col;
-          const int ch = m * 8 + 4 * hi + q;
-          cst[m][nt][q] = (y < H && x < W) ? a.c[(((size_t)b * HID + ch) * H + y) * W + x] : 0.f;
-        }
-
-    floatx16 acc[MT][NT];
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[m][nt][j] = 0.0f;
-
-    // implicit GEMM: k = tap * CIN + ci; operands of step cp+1 are read while the
-    // MFMAs of step cp issue
-    const float* inb = in + hi * C::PLANE + wave * C::W2 + (C::LEFT - 1) + col;
-#pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      const int dy = tap / 3, dx = tap % 3;
-      const float* bt = inb + dy * C::W2 + dx;
-      const float* at = wl + (tap * C::CP) * MT * 64 + lane;
-      float av[2][MT], bv[2][NT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) av[0][m] = at[m * 64];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bv[0][nt] = bt[nt * 32];
-#pragma unroll
-      for (int cp = 0; cp < C::CP; ++cp) {
-        const int cur = cp & 1, nxt = cur ^ 1;
-        if (cp + 1 < C::CP) {
-#pragma unroll
-          for (int m = 0; m < MT; ++m) av[nxt][m] = at[((cp + 1) * MT + m) * 64];
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) bv[nxt][nt] = bt[2 * (cp + 1) * C::PLANE + nt * 32];
-        }
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-            acc[m][nt] =
-                __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][m], bv[cur][nt], acc[m][nt], 0, 0, 0);
-      }
-    }
-
-    // epilogue: LSTM gates (module.py:83-90)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int x = x0 + nt * 32 + col;
-      if (y < H && x < W) {
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int ch = m * 8 + 4 * hi + q;
-            const float gi = acc[m][nt][q] + a.bias[ch];
-            const float gf = acc[m][nt][4 + q] + a.bias[HID + ch];
-            const float go = acc[m][nt][8 + q] + a.bias[2 * HID + ch];
-            const float gg = acc[m][nt][12 + q] + a.bias[3 * HID + ch];
-            const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
-            const float cn = fast_sigmoid(gf) * cst[m][nt][q] + fast_sigmoid(gi) * fast_tanh(gg);
-            a.c[idx] = cn;
-            a.h_new[idx] = fast_sigmoid(go) * fast_tanh(cn);
-          }
-        }
-      }
-    }
-  }
-}
-
-template <int KIND>
-static hipError_t run_cell(const CellArgs& a, int cu, int kid, hipStream_t s) {
-  using C = CellCfg<KIND>;
-  static_assert(C::LDS_BYTES <= 160 * 1024, "cell tile exceeds LDS");
-  static_assert(PartRegs<KIND, 0>::NS <= 32 && PartRegs<KIND, 1>::NS <= 32 &&
-                    PartRegs<KIND, 2>::NS <= 32 && PartRegs<KIND, 0>::NH <= 32,
-                "staging masks hold 32 items per part");
-  static_assert(C::TW % 32 == 0, "tile width is a multiple of 32 (16-B aligned interior)");
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)lstm_cell_kernel<KIND>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)C::LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  const int ntiles = a.B * ((a.W + C::TW - 1) / C::TW) * ((a.H + C::TH - 1) / C::TH);
-  const int per_cu = (int)((160 * 1024) / C::LDS_BYTES);
-  const int grid = std::max(1, std::min(ntiles, cu * std::max(1, per_cu)));
-  ProfScope ps(s, kid);
-  hipLaunchKernelGGL(lstm_cell_kernel<KIND>, dim3(grid), dim3(C::THREADS), C::LDS_BYTES, s, a);
-  return hipGetLastError();
-}
 
 // ---------------------------------------------------------------------------
-// Split-fp16 ConvLSTM cell ("h3"): the same implicit GEMM on v_mfma_f32_32x32x16_f16
-// with each fp32 operand split into fp16 hi + lo and three products per k-step,
+// Split-fp16 ConvLSTM cell ("h3"): the 3x3 conv as an implicit GEMM on
+// v_mfma_f32_32x32x16_f16 (M = 4 hid gate rows, N = 32 pixels of a tile row, K = 9 taps x
+// Cin) with each fp32 operand split into fp16 hi + lo and three products per k-step,
 //   w x = w_hi x_hi + w_hi x_lo + w_lo x_hi   (+ w_lo x_lo, dropped: ~2^-22 relative),
 // accumulated in fp32.  The weights carry a power-of-two scale (pack_cell_h3_kernel)
 // undone in the epilogue.  Per product the error is ~2^-21 relative, i.e. within a few
-// fp32 roundings; the depth/confidence parity is that of the fp32 path.
+// fp32 roundings.
 // Rate: 3 x 16 K per 3 x 32 cycles vs 2 K per 64 cycles for the f32 MFMA, 5.3x.
 //
 // Input channels are processed in 16-channel chunks (one k-group of every tap); a
@@ -447,11 +114,6 @@ struct H3Cfg {
   static constexpr int TH = RW * WAVES, THREADS = WAVES * 64, TW = 32, W2 = TW + 2, TROWS = TH + 2;
   static constexpr int NPIX = TROWS * W2;
   static constexpr int A_HALVES = NCHK * 9 * MT * 64 * 8;   // per hi / lo
-  static constexpr int SEGS = TW / 4;
-  static constexpr int SEG_ITEMS = 8 * TROWS * SEGS;         // (channel pair, row, float4 segment)
-  static constexpr int HALO_ITEMS = 8 * TROWS * 2;
-  static constexpr int NS = (SEG_ITEMS + THREADS - 1) / THREADS;
-  static constexpr int NH = (HALO_ITEMS + THREADS - 1) / THREADS;
   static constexpr size_t LDS_BYTES = (size_t)A_HALVES * 2 * 2 + (size_t)NPIX * 32 * 2 + 32 * 4;
   static constexpr int c0(int p) { return p == 0 ? 0 : (p == 1 ? D::CH[0] : D::CH[0] + D::CH[1]); }
   static constexpr int chunk_part(int c) {
@@ -474,162 +136,20 @@ __device__ __forceinline__ uint32_t h3_split2(float a, float b, uint32_t& lo_bit
   return __builtin_bit_cast(uint32_t, hi);
 }
 
-template <int KIND, int RW, int WAVES>
-struct H3Stager {
-  using C = H3Cfg<KIND, RW, WAVES>;
-  using D = typename C::D;
-  float4 seg[C::NS][2][4];   // [item][channel of the pair][POOL window]
-  float halo[C::NH][2][4];
-  uint32_t seg_in, halo_in;
-
-  template <int CH>
-  __device__ __forceinline__ void load(const CellArgs& a, int b, int y0, int x0, int tid) {
-    constexpr int P = C::chunk_part(CH), MODE = D::MODE[P], NCH = D::CH[P];
-    constexpr int LC0 = C::chunk_lc0(CH), NV = C::chunk_nv(CH);
-    const ChanSrc& s = a.part[P];
-    const int H = a.H, W = a.W;
-    const bool vec = (W & 3) == 0;
-    seg_in = halo_in = 0u;
-#pragma unroll
-    for (int j = 0; j < C::NS; ++j) {
-      const int e = tid + j * C::THREADS;
-      const int q = e / (C::TROWS * C::SEGS), rem = e % (C::TROWS * C::SEGS);
-      const int gy = y0 - 1 + rem / C::SEGS, gx = x0 + 4 * (rem % C::SEGS);
-      if (e < C::SEG_ITEMS && 2 * q < NV && gy >= 0 && gy < H && gx < W) {
-        seg_in |= 1u << j;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int lc = LC0 + 2 * q + u;
-          if (MODE == SRC_POOL) {
-            const int Ws = 2 * W;
-            const float* p = s.ptr + (((size_t)b * NCH + lc) * (2 * H) + 2 * gy) * Ws + 2 * gx;
-            seg[j][u][0] = PartRegs<0, 0>::row4(p, 2 * gx, Ws, vec);
-            seg[j][u][1] = PartRegs<0, 0>::row4(p + 4, 2 * gx + 4, Ws, vec);
-            seg[j][u][2] = PartRegs<0, 0>::row4(p + Ws, 2 * gx, Ws, vec);
-            seg[j][u][3] = PartRegs<0, 0>::row4(p + Ws + 4, 2 * gx + 4, Ws, vec);
-          } else {
-            seg[j][u][0] =
-                PartRegs<0, 0>::row4(s.ptr + (((size_t)b * NCH + lc) * H + gy) * W + gx, gx, W, vec);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < C::NH; ++j) {
-      const int e = tid + j * C::THREADS;
-      const int q = e / (C::TROWS * 2), rem = e % (C::TROWS * 2);
-      const int gy = y0 - 1 + rem / 2, gx = (rem & 1) ? x0 + C::TW : x0 - 1;
-      if (e < C::HALO_ITEMS && 2 * q < NV && gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        halo_in |= 1u << j;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int lc = LC0 + 2 * q + u;
-          if (MODE == SRC_POOL) {
-            const int Ws = 2 * W;
-            const float* p = s.ptr + (((size_t)b * NCH + lc) * (2 * H) + 2 * gy) * Ws + 2 * gx;
-            halo[j][u][0] = p[0];
-            halo[j][u][1] = p[1];
-            halo[j][u][2] = p[Ws];
-            halo[j][u][3] = p[Ws + 1];
-          } else {
-            halo[j][u][0] = s.ptr[(((size_t)b * NCH + lc) * H + gy) * W + gx];
-          }
-        }
-      }
-    }
-  }
-
-  template <int CH>
-  __device__ __forceinline__ float value(float4 v0, float4 v1, float4 v2, float4 v3, int e4,
-                                         int lc, const float* gn) const {
-    constexpr int MODE = D::MODE[C::chunk_part(CH)];
-    auto comp = [](float4 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w)); };
-    if (MODE == SRC_POOL) {
-      // coarse column e4 of the segment <- fine columns 2 e4, 2 e4 + 1 of rows 2gy, 2gy + 1
-      const float4 a = e4 < 2 ? v0 : v1, c = e4 < 2 ? v2 : v3;
-      const int i0 = 2 * (e4 & 1);
-      return fmaxf(fmaxf(comp(a, i0), comp(a, i0 + 1)), fmaxf(comp(c, i0), comp(c, i0 + 1)));
-    }
-    const float x = comp(v0, e4);
-    return MODE == SRC_GNRELU ? fmaxf(x * gn[lc] + gn[16 + lc], 0.0f) : x;
-  }
-
-  template <int CH>
-  __device__ __forceinline__ void store(char* hi_plane, char* lo_plane, const float* gn, int tid,
-                                        int x0, int W) const {
-    constexpr int MODE = D::MODE[C::chunk_part(CH)];
-    constexpr int LC0 = C::chunk_lc0(CH);
-#pragma unroll
-    for (int j = 0; j < C::NS; ++j) {
-      const int e = tid + j * C::THREADS;
-      if (e < C::SEG_ITEMS) {
-        const int q = e / (C::TROWS * C::SEGS), rem = e % (C::TROWS * C::SEGS);
-        const int row = rem / C::SEGS, sg = rem % C::SEGS;
-        const bool in = seg_in & (1u << j);
-        const int gx = x0 + 4 * sg;
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-          float v[2];
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-            v[u] = (in && gx + e4 < W)
-                       ? value<CH>(seg[j][u][0], seg[j][u][MODE == SRC_POOL ? 1 : 0],
-                                   seg[j][u][MODE == SRC_POOL ? 2 : 0],
-                                   seg[j][u][MODE == SRC_POOL ? 3 : 0], e4, LC0 + 2 * q + u, gn)
-                       : 0.0f;
-          uint32_t lo;
-          const uint32_t hi = h3_split2(v[0], v[1], lo);
-          const int p = row * C::W2 + 1 + 4 * sg + e4;
-          const int off = h3_pix(p, q >> 2) + 4 * (q & 3);
-          *reinterpret_cast<uint32_t*>(hi_plane + off) = hi;
-          *reinterpret_cast<uint32_t*>(lo_plane + off) = lo;
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < C::NH; ++j) {
-      const int e = tid + j * C::THREADS;
-      if (e < C::HALO_ITEMS) {
-        const int q = e / (C::TROWS * 2), rem = e % (C::TROWS * 2);
-        const int row = rem / 2;
-        const bool in = halo_in & (1u << j);
-        float v[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          float x = 0.0f;
-          if (in) {
-            if (MODE == SRC_POOL)
-              x = fmaxf(fmaxf(halo[j][u][0], halo[j][u][1]), fmaxf(halo[j][u][2], halo[j][u][3]));
-            else if (MODE == SRC_GNRELU)
-              x = fmaxf(halo[j][u][0] * gn[LC0 + 2 * q + u] + gn[16 + LC0 + 2 * q + u], 0.0f);
-            else
-              x = halo[j][u][0];
-          }
-          v[u] = x;
-        }
-        uint32_t lo;
-        const uint32_t hi = h3_split2(v[0], v[1], lo);
-        const int p = row * C::W2 + ((rem & 1) ? C::W2 - 1 : 0);
-        const int off = h3_pix(p, q >> 2) + 4 * (q & 3);
-        *reinterpret_cast<uint32_t*>(hi_plane + off) = hi;
-        *reinterpret_cast<uint32_t*>(lo_plane + off) = lo;
-      }
-    }
-  }
-};
-
-// Pixel-major staging (the default): item = (half h of the chunk's 16 channels, pixel p
-// of the haloed tile), consecutive lanes on consecutive pixels.  A channel's loads are
-// contiguous runs of an image row, and an item lands in each LDS plane as ONE 16-B store
-// (8 channels as fp16 pairs) at h3_pix(p, h): 2-way bank conflicts at most, where the
-// segment stager above writes 4-B pairs 128 B apart (32-way).  Out-of-image pixels and
-// channels past the chunk's valid count load zeros through the buffer range check.
-template <int KIND, int RW, int WAVES, int NHWC = 0>
+// Input staging: item = (half h of the chunk's 16 channels, pixel p of the haloed tile),
+// consecutive lanes on consecutive pixels.  The U-Net tensors are NHWC ([B][H][W][C]), so
+// an item's 8 channels are 32 contiguous bytes (two 16-B loads; POOL: two per fine pixel
+// of the 2x2 window) and a tile row is one contiguous run per part.  An item lands in
+// each LDS plane as ONE 16-B store (8 channels as fp16 pairs) at h3_pix(p, h): 2-way bank
+// conflicts at most.  Out-of-image pixels and channels past the chunk's valid count load
+// zeros through the buffer range check.  NTH: staging threads (default: the block).
+template <int KIND, int RW, int WAVES, int NTH = 0>
 struct H3PixStager {
   using C = H3Cfg<KIND, RW, WAVES>;
   using D = typename C::D;
+  static constexpr int TH = NTH ? NTH : C::THREADS;   // staging threads
   static constexpr int NITEM = 2 * C::NPIX;
-  static constexpr int NI = (NITEM + C::THREADS - 1) / C::THREADS;
+  static constexpr int NI = (NITEM + TH - 1) / TH;
   static_assert(NI <= 32, "item mask holds 32 items");
   float val[NI][8][4];   // [item][channel][POOL window: fine (2y,2x) (2y,2x+1) (2y+1,2x) (2y+1,2x+1)]
   uint32_t in_mask;      // bit j: item j is an in-image pixel of valid channels
@@ -642,51 +162,32 @@ struct H3PixStager {
     const ChanSrc& s = a.part[P];
     const int H = a.H, W = a.W;
     const int Hs = MODE == SRC_POOL ? 2 * H : H, Ws = MODE == SRC_POOL ? 2 * W : W;
-    const uint32_t plane = (uint32_t)Hs * (uint32_t)Ws * 4u;   // bytes of one channel image
-    const uint32_t nbytes = (uint32_t)NCH * plane;
+    const uint32_t nbytes = (uint32_t)NCH * (uint32_t)Hs * (uint32_t)Ws * 4u;   // one image
     const __amdgpu_buffer_rsrc_t r = uniform_rsrc(s.ptr + (size_t)b * NCH * Hs * Ws, nbytes);
     in_mask = 0u;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const int e = tid + j * C::THREADS;
+      const int e = tid + j * TH;
       const int h = e >= C::NPIX ? 1 : 0, p = e - h * C::NPIX;
       const int row = p / C::W2, col = p - row * C::W2;
       const int gy = y0 - 1 + row, gx = x0 - 1 + col;
       const bool in = e < NITEM && 8 * h < NV && gy >= 0 && gy < H && gx >= 0 && gx < W;
       if (in) in_mask |= 1u << j;
       const uint32_t pix = MODE == SRC_POOL ? (uint32_t)(2 * gy * Ws + 2 * gx) : (uint32_t)(gy * W + gx);
-      const uint32_t base = (uint32_t)(LC0 + 8 * h) * plane + pix * 4u;
-      if constexpr (NHWC) {
-        // [B][Hs][Ws][NCH]: the item's 8 channels are 32 contiguous bytes
-        const uint32_t ob = (pix * (uint32_t)NCH + (uint32_t)(LC0 + 8 * h)) * 4u;
-        constexpr int NW = MODE == SRC_POOL ? 4 : 1;
+      const uint32_t ob = (pix * (uint32_t)NCH + (uint32_t)(LC0 + 8 * h)) * 4u;
+      constexpr int NW = MODE == SRC_POOL ? 4 : 1;   // POOL: the 2x2 fine window
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          const uint32_t o = in ? ob + (uint32_t)(((w >> 1) * Ws + (w & 1)) * NCH * 4) : nbytes;
-          const float4 q0 = ld4(r, o), q1 = ld4(r, in ? o + 16u : nbytes);
-          val[j][0][w] = q0.x;
-          val[j][1][w] = q0.y;
-          val[j][2][w] = q0.z;
-          val[j][3][w] = q0.w;
-          val[j][4][w] = q1.x;
-          val[j][5][w] = q1.y;
-          val[j][6][w] = q1.z;
-          val[j][7][w] = q1.w;
-        }
-        continue;
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t off = in ? base + (uint32_t)k * plane : nbytes;
-        if (MODE == SRC_POOL) {
-          const float2 t0 = ld2(r, off), t1 = ld2(r, in ? off + (uint32_t)Ws * 4u : nbytes);
-          val[j][k][0] = t0.x;
-          val[j][k][1] = t0.y;
-          val[j][k][2] = t1.x;
-          val[j][k][3] = t1.y;
-        } else {
-          val[j][k][0] = ld1(r, off);
-        }
+      for (int w = 0; w < NW; ++w) {
+        const uint32_t o = in ? ob + (uint32_t)(((w >> 1) * Ws + (w & 1)) * NCH * 4) : nbytes;
+        const float4 q0 = ld4(r, o), q1 = ld4(r, in ? o + 16u : nbytes);
+        val[j][0][w] = q0.x;
+        val[j][1][w] = q0.y;
+        val[j][2][w] = q0.z;
+        val[j][3][w] = q0.w;
+        val[j][4][w] = q1.x;
+        val[j][5][w] = q1.y;
+        val[j][6][w] = q1.z;
+        val[j][7][w] = q1.w;
       }
     }
   }
@@ -698,7 +199,7 @@ struct H3PixStager {
     constexpr int LC0 = C::chunk_lc0(CH);
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const int e = tid + j * C::THREADS;
+      const int e = tid + j * TH;
       if (e < NITEM) {
         const int h = e >= C::NPIX ? 1 : 0, p = e - h * C::NPIX;
         const bool in = in_mask & (1u << j);
@@ -727,11 +228,10 @@ struct H3PixStager {
   }
 };
 
-// One input chunk's MFMAs: 9 taps x MT m-tiles x RW rows x 3 split products.  PIPE
-// (microbenchmark variant): the A/B fragments of tap t+1 are read from LDS into a second
-// register set before tap t's MFMAs issue.  The compiler's own schedule reads each tap's
-// fragments just before use; measured equal on cells 0-3 (the other wave of the SIMD
-// covers the LDS latency) and 18% slower on cell 4, whose extra VGPRs cost occupancy.
+// One input chunk's MFMAs: 9 taps x MT m-tiles x RW rows x 3 split products.  PIPE: the
+// A/B fragments of tap t+1 are read from LDS into a second register set before tap t's
+// MFMAs issue (sched_barrier pins the order); otherwise the compiler's schedule reads
+// each tap's fragments just before use and waits on them every 2-3 MFMAs.
 template <class C, int CH, bool PIPE = false>
 __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], const char* wl_hi,
                                               const char* wl_lo, const char* in_hi,
@@ -797,12 +297,69 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], con
   }
 }
 
-// STG: 1 pixel-major staging (H3PixStager, the library's), 0 segment staging (H3Stager;
-// kept for the cell microbenchmark's comparison).  ABL: ablation bits for the
-// microbenchmark only (1 no MFMA, 2 no staging loads/stores, 4 no gate math, 8 the
-// software-pipelined fragment reads)
-template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int STG = 1,
-          int ABL = 0>
+// Cell state I/O (NHWC [B][H][W][HID]): lane (col, hi) of m-tile m owns channels
+// m*8 + 4 hi .. +3 of pixel (y, x): one 16-B load / store per (m, row).
+template <class C>
+__device__ __forceinline__ void cell_c_load(const CellArgs& a, int b, int yw, int x, int hi,
+                                            float (&cst)[C::MT][C::RW][4]) {
+#pragma unroll
+  for (int m = 0; m < C::MT; ++m)
+#pragma unroll
+    for (int r = 0; r < C::RW; ++r) {
+      const int y = yw + r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (y < a.H && x < a.W)
+        v = *reinterpret_cast<const float4*>(
+            a.c + (((size_t)b * a.H + y) * a.W + x) * C::HID + m * 8 + 4 * hi);
+      cst[m][r][0] = v.x;
+      cst[m][r][1] = v.y;
+      cst[m][r][2] = v.z;
+      cst[m][r][3] = v.w;
+    }
+}
+
+// gate epilogue (module.py:83-90): undo the weight scale, add the bias, LSTM update
+template <class C, int ABL>
+__device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 (&acc)[C::MT][C::RW],
+                                              const float (&cst)[C::MT][C::RW][4], float inv_scale,
+                                              int b, int yw, int x, int hi) {
+  constexpr int HID = C::HID;
+#pragma unroll
+  for (int r = 0; r < C::RW; ++r) {
+    const int y = yw + r;
+    if (y < a.H && x < a.W) {
+      const size_t pix = ((size_t)b * a.H + y) * a.W + x;
+#pragma unroll
+      for (int m = 0; m < C::MT; ++m) {
+        float cn[4], hn[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ch = m * 8 + 4 * hi + q;
+          const float gi = fmaf(acc[m][r][q], inv_scale, a.bias[ch]);
+          const float gf = fmaf(acc[m][r][4 + q], inv_scale, a.bias[HID + ch]);
+          const float go = fmaf(acc[m][r][8 + q], inv_scale, a.bias[2 * HID + ch]);
+          const float gg = fmaf(acc[m][r][12 + q], inv_scale, a.bias[3 * HID + ch]);
+          if (ABL & 4) {
+            cn[q] = gi + gf;
+            hn[q] = go + gg + cst[m][r][q];
+          } else {
+            cn[q] = fast_sigmoid(gf) * cst[m][r][q] + fast_sigmoid(gi) * fast_tanh(gg);
+            hn[q] = fast_sigmoid(go) * fast_tanh(cn[q]);
+          }
+        }
+        const size_t o = pix * HID + m * 8 + 4 * hi;
+        *reinterpret_cast<float4*>(a.c + o) = make_float4(cn[0], cn[1], cn[2], cn[3]);
+        *reinterpret_cast<float4*>(a.h_new + o) = make_float4(hn[0], hn[1], hn[2], hn[3]);
+      }
+    }
+  }
+}
+
+// Single-buffered kernel.  PIPE: software-pipelined fragment reads (h3_mfma_chunk).  ABL:
+// ablation bits for the microbenchmark only (1 no MFMA, 2 no staging loads/stores, 4 no
+// gate math)
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
+          int PIPE = CellDef<KIND>::H3PIPE>
 __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
@@ -844,8 +401,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     y0 = (rem / tiles_x) * C::TH;
     x0 = (rem % tiles_x) * C::TW;
   };
-  typename std::conditional<STG >= 1, H3PixStager<KIND, RW, WAVES, STG == 2>,
-                            H3Stager<KIND, RW, WAVES>>::type st;
+  H3PixStager<KIND, RW, WAVES> st;
   int tile = blockIdx.x;
   if (tile < ntiles && !(ABL & 2)) {
     int b, y0, x0;
@@ -880,51 +436,14 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
       } else if (next < ntiles) {
         st.template load<0>(a, nb, ny0, nx0, tid);
       }
-      if (CH == 0) {
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int r = 0; r < RW; ++r)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int x = x0 + col, y = yw + r, ch = m * 8 + 4 * hi + q;
-              cst[m][r][q] = (y < H && x < W) ? a.c[(((size_t)b * HID + ch) * H + y) * W + x] : 0.f;
-            }
-      }
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH, (ABL & 8) != 0>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
+      if (CH == 0) cell_c_load<C>(a, b, yw, x0 + col, hi, cst);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
     };
     chunk(std::integral_constant<int, 0>{});
     if constexpr (NCHK > 1) chunk(std::integral_constant<int, 1>{});
     if constexpr (NCHK > 2) chunk(std::integral_constant<int, 2>{});
 
-    // epilogue: LSTM gates (module.py:83-90); undo the weight scale, add the bias
-    const int x = x0 + col;
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      const int y = yw + r;
-      if (y < H && x < W) {
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int ch = m * 8 + 4 * hi + q;
-            const float gi = fmaf(acc[m][r][q], inv_scale, a.bias[ch]);
-            const float gf = fmaf(acc[m][r][4 + q], inv_scale, a.bias[HID + ch]);
-            const float go = fmaf(acc[m][r][8 + q], inv_scale, a.bias[2 * HID + ch]);
-            const float gg = fmaf(acc[m][r][12 + q], inv_scale, a.bias[3 * HID + ch]);
-            const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
-            if (ABL & 4) {
-              a.c[idx] = gi + gf;
-              a.h_new[idx] = go + gg + cst[m][r][q];
-              continue;
-            }
-            const float cn = fast_sigmoid(gf) * cst[m][r][q] + fast_sigmoid(gi) * fast_tanh(gg);
-            a.c[idx] = cn;
-            a.h_new[idx] = fast_sigmoid(go) * fast_tanh(cn);
-          }
-        }
-      }
-    }
+    cell_epilogue<C, ABL>(a, acc, cst, inv_scale, b, yw, x0 + col, hi);
   }
 }
 
@@ -935,7 +454,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
 // the chunk after that; at a tile's last chunk, the gate epilogue.  Across the two
 // waves of a SIMD one wave's staging VALU work fills the other's MFMA issue gaps.
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
-          int STG = 1>
+          int PIPE = CellDef<KIND>::H3PIPE>
 __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
@@ -978,7 +497,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
   };
   int tile = blockIdx.x;
   if (tile >= ntiles) return;   // whole block
-  H3PixStager<KIND, RW, WAVES, STG == 2> st;
+  H3PixStager<KIND, RW, WAVES> st;
   int b, y0, x0;
   coords(tile, b, y0, x0);
   if (!(ABL & 2)) st.template load<0>(a, b, y0, x0, tid);
@@ -1002,15 +521,10 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int r = 0; r < RW; ++r) {
+      for (int r = 0; r < RW; ++r)
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[m][r][j] = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int y = yw + r, ch = m * 8 + 4 * hi + q;
-          cst[m][r][q] = (y < H && x < W) ? a.c[(((size_t)b * HID + ch) * H + y) * W + x] : 0.f;
-        }
-      }
+    cell_c_load<C>(a, b, yw, x, hi, cst);
     auto step = [&](auto CHc) {
       constexpr int CH = decltype(CHc)::value;
       constexpr bool F_NEXT = CH + 1 >= NCHK;   // following chunk: the next tile's first
@@ -1019,7 +533,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
       constexpr int AC = A_NEXT ? CH + 2 - NCHK : CH + 2;
       const char* cur = inb + 2 * par * PB;
       char* oth = inb + 2 * (par ^ 1) * PB;
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH, (ABL & 8) != 0>(acc, wl_hi, wl_lo, cur, cur + PB, wave, lane);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0>(acc, wl_hi, wl_lo, cur, cur + PB, wave, lane);
       if (!(ABL & 2)) {
         if (!F_NEXT || next < ntiles) st.template store<F>(oth, oth + PB, gn, tid, 0, W);
         if (!A_NEXT)
@@ -1027,35 +541,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
         else if (next < ntiles)
           st.template load<AC>(a, nb, ny0, nx0, tid);
       }
-      if constexpr (CH == NCHK - 1) {
-        // epilogue: LSTM gates (module.py:83-90); undo the weight scale, add the bias
-#pragma unroll
-        for (int r = 0; r < RW; ++r) {
-          const int y = yw + r;
-          if (y < H && x < W) {
-#pragma unroll
-            for (int m = 0; m < MT; ++m) {
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const int ch = m * 8 + 4 * hi + q;
-                const float gi = fmaf(acc[m][r][q], inv_scale, a.bias[ch]);
-                const float gf = fmaf(acc[m][r][4 + q], inv_scale, a.bias[HID + ch]);
-                const float go = fmaf(acc[m][r][8 + q], inv_scale, a.bias[2 * HID + ch]);
-                const float gg = fmaf(acc[m][r][12 + q], inv_scale, a.bias[3 * HID + ch]);
-                const size_t idx = (((size_t)b * HID + ch) * H + y) * W + x;
-                if (ABL & 4) {
-                  a.c[idx] = gi + gf;
-                  a.h_new[idx] = go + gg + cst[m][r][q];
-                  continue;
-                }
-                const float cn = fast_sigmoid(gf) * cst[m][r][q] + fast_sigmoid(gi) * fast_tanh(gg);
-                a.c[idx] = cn;
-                a.h_new[idx] = fast_sigmoid(go) * fast_tanh(cn);
-              }
-            }
-          }
-        }
-      }
+      if constexpr (CH == NCHK - 1) cell_epilogue<C, ABL>(a, acc, cst, inv_scale, b, yw, x, hi);
       __syncthreads();   // buffer `oth` staged; buffer `cur` free for the step after next
       par ^= 1;
     };
@@ -1065,19 +551,21 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
   }
 }
 
-// DB: 1 double-buffered kernel, 0 single-buffered; per cell in CellDef (measured at the
-// headline geometry: double buffering wins on the 48-channel cells 0 and 3 and loses
-// where the second buffer costs occupancy or the chunks are few)
-template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int STG = 1,
-          int ABL = 0, int DB = CellDef<KIND>::H3DB>
+// DB: 1 double-buffered kernel, 0 single-buffered; PIPE: pipelined fragment reads.  Per
+// cell in CellDef, from tools/microbench/cell_bench.cpp at the headline geometry (ms,
+// DB0/PIPE0 DB0/PIPE1 DB1/PIPE0 DB1/PIPE1): cell0 .405 .379 .352 .324, cell1 .097 .090
+// .091 .086, cell3 .087 .082 .083 .082, cell4 .155 .170 .208 .193 (cell 4's second
+// buffer or second fragment set costs it a block per CU).  A warp-specialised form (4
+// staging waves beside the 8 MFMA waves) measured slower (cell 0 0.43 vs 0.40 ms).
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
+          int DB = CellDef<KIND>::H3DB, int PIPE = CellDef<KIND>::H3PIPE>
 static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu, int kid,
                               hipStream_t s) {
   using C = H3Cfg<KIND, RW, WAVES>;
   constexpr size_t lds = C::LDS_BYTES + (DB ? (size_t)C::NPIX * 32 * 2 : 0);
   static_assert(lds <= 160 * 1024, "h3 cell tile exceeds LDS");
-  static_assert(C::NS <= 32 && C::NH <= 32, "staging masks hold 32 items");
-  const void* fn = DB ? (const void*)lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, STG>
-                      : (const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, STG, ABL>;
+  const void* fn = DB ? (const void*)lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE>
+                      : (const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1089,10 +577,10 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
   const int grid = std::max(1, std::min(ntiles, cu * per_cu));
   ProfScope ps(s, kid);
   if (DB)
-    hipLaunchKernelGGL((lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, STG>), dim3(grid), dim3(C::THREADS),
-                       lds, s, a, inv_scale);
+    hipLaunchKernelGGL((lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE>), dim3(grid),
+                       dim3(C::THREADS), lds, s, a, inv_scale);
   else
-    hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, STG, ABL>), dim3(grid),
+    hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE>), dim3(grid),
                        dim3(C::THREADS), lds, s, a, inv_scale);
   return hipGetLastError();
 }
@@ -1101,7 +589,7 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
 // deConvGnReLU's transposed conv (module.py:281): ConvTranspose2d(16,16,3,s2,p1,op1).
 // One thread per input pixel produces its 2x2 output quad (uniform weight taps),
 // plus GroupNorm(2,16) partial sums (the GN+ReLU itself is fused into the
-// consuming cell's input staging).
+// consuming cell's input staging).  NHWC in and out: a pixel's 16 channels are 64 B.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) deconv_kernel(const float* __restrict__ in,
                                                      const float* __restrict__ w,
@@ -1122,36 +610,51 @@ __global__ void __launch_bounds__(256) deconv_kernel(const float* __restrict__ i
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int co = 0; co < 16; ++co) o[q][co] = 0.f;
-    for (int ci = 0; ci < 16; ++ci) {
-      const float* ic = ib + (size_t)ci * HWi + p;
-      const float v00 = ic[0];
-      const float v01 = hx ? ic[1] : 0.f;
-      const float v10 = hy ? ic[Wi] : 0.f;
-      const float v11 = (hx && hy) ? ic[Wi + 1] : 0.f;
-      const float* wc = w + ci * 16 * 9;   // [ci][co][ky][kx]
+    const float4* i00 = reinterpret_cast<const float4*>(ib + (size_t)p * 16);
+    const float4* i01 = i00 + 4;
+    const float4* i10 = i00 + 4 * Wi;
+    const float4* i11 = i10 + 4;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+    for (int c4 = 0; c4 < 4; ++c4) {
+      const float4 a00 = i00[c4], a01 = hx ? i01[c4] : z4, a10 = hy ? i10[c4] : z4,
+                   a11 = (hx && hy) ? i11[c4] : z4;
+      const float f00[4] = {a00.x, a00.y, a00.z, a00.w}, f01[4] = {a01.x, a01.y, a01.z, a01.w};
+      const float f10[4] = {a10.x, a10.y, a10.z, a10.w}, f11[4] = {a11.x, a11.y, a11.z, a11.w};
 #pragma unroll
-      for (int co = 0; co < 16; ++co) {
-        const float* k = wc + co * 9;
-        // out(2iy,2ix): (ky,kx)=(1,1) from (iy,ix)
-        o[0][co] = fmaf(v00, k[4], o[0][co]);
-        // out(2iy,2ix+1): kx=2 from ix, kx=0 from ix+1 (ky=1)
-        o[1][co] = fmaf(v00, k[5], fmaf(v01, k[3], o[1][co]));
-        // out(2iy+1,2ix): ky=2 from iy, ky=0 from iy+1 (kx=1)
-        o[2][co] = fmaf(v00, k[7], fmaf(v10, k[1], o[2][co]));
-        // out(2iy+1,2ix+1)
-        o[3][co] = fmaf(v00, k[8], fmaf(v01, k[6], fmaf(v10, k[2], fmaf(v11, k[0], o[3][co]))));
+      for (int u = 0; u < 4; ++u) {
+        const int ci = 4 * c4 + u;
+        const float v00 = f00[u], v01 = f01[u], v10 = f10[u], v11 = f11[u];
+        const float* wc = w + ci * 16 * 9;   // [ci][co][ky][kx]
+#pragma unroll
+        for (int co = 0; co < 16; ++co) {
+          const float* k = wc + co * 9;
+          // out(2iy,2ix): (ky,kx)=(1,1) from (iy,ix)
+          o[0][co] = fmaf(v00, k[4], o[0][co]);
+          // out(2iy,2ix+1): kx=2 from ix, kx=0 from ix+1 (ky=1)
+          o[1][co] = fmaf(v00, k[5], fmaf(v01, k[3], o[1][co]));
+          // out(2iy+1,2ix): ky=2 from iy, ky=0 from iy+1 (kx=1)
+          o[2][co] = fmaf(v00, k[7], fmaf(v10, k[1], o[2][co]));
+          // out(2iy+1,2ix+1)
+          o[3][co] = fmaf(v00, k[8], fmaf(v01, k[6], fmaf(v10, k[2], fmaf(v11, k[0], o[3][co]))));
+        }
       }
     }
-    // the two output columns 2ix, 2ix+1 of a row are adjacent: one float2 store each
 #pragma unroll
-    for (int ry = 0; ry < 2; ++ry) {
-      const int oy = 2 * iy + ry;
+    for (int q = 0; q < 4; ++q) {
+      const int oy = 2 * iy + (q >> 1), ox = 2 * ix + (q & 1);
+      float4* op = reinterpret_cast<float4*>(ob + ((size_t)oy * Wo + ox) * 16);
 #pragma unroll
-      for (int co = 0; co < 16; ++co) {
-        const float r0 = o[2 * ry][co] + bias[co], r1 = o[2 * ry + 1][co] + bias[co];
-        *reinterpret_cast<float2*>(&ob[((size_t)co * Ho + oy) * Wo + 2 * ix]) = make_float2(r0, r1);
-        part[(co >> 3) * 2] += r0 + r1;
-        part[(co >> 3) * 2 + 1] += r0 * r0 + r1 * r1;
+      for (int c4 = 0; c4 < 4; ++c4) {
+        float r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int co = 4 * c4 + u;
+          r[u] = o[q][co] + bias[co];
+          part[(co >> 3) * 2] += r[u];
+          part[(co >> 3) * 2 + 1] += r[u] * r[u];
+        }
+        op[c4] = make_float4(r[0], r[1], r[2], r[3]);
       }
     }
   }
@@ -1188,12 +691,18 @@ __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__
   const int tiles_x = (W + kHeadTW - 1) / kHeadTW;
   const int y0 = (blockIdx.x / tiles_x) * kHeadTH, x0 = (blockIdx.x % tiles_x) * kHeadTW;
   const float* hb = h4 + (size_t)b * 8 * HW;
-  // h4 tile with a 1-px zero-padded halo -> LDS (coalesced along x)
-  for (int i = threadIdx.x; i < 8 * (kHeadTH + 2) * (kHeadTW + 2); i += 256) {
-    const int ci = i / ((kHeadTH + 2) * (kHeadTW + 2)), rem = i % ((kHeadTH + 2) * (kHeadTW + 2));
+  // h4 tile (NHWC: 32 B per pixel) with a 1-px zero-padded halo -> LDS [ci][y][x]
+  for (int rem = threadIdx.x; rem < (kHeadTH + 2) * (kHeadTW + 2); rem += 256) {
     const int yy = y0 - 1 + rem / (kHeadTW + 2), xx = x0 - 1 + rem % (kHeadTW + 2);
-    (&t[ci][0][0])[rem] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? hb[(size_t)ci * HW + yy * W + xx]
-                                                                     : 0.0f;
+    float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+      const float4* src = reinterpret_cast<const float4*>(hb + ((size_t)yy * W + xx) * 8);
+      q0 = src[0];
+      q1 = src[1];
+    }
+    const float v8[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) (&t[ci][0][0])[rem] = v8[ci];
   }
   __syncthreads();
   const int ty = threadIdx.x / kHeadTW, tx = threadIdx.x % kHeadTW;
@@ -1243,6 +752,31 @@ __global__ void __launch_bounds__(256) softmax_depth_kernel(const float* __restr
     const float inv = 1.0f / s;
     for (int d = 0; d < D; ++d) o[(size_t)d * HW] = expf(c[(size_t)d * HW] - m) * inv;
   }
+}
+
+// NCHW <-> NHWC for the API edges (aarmvs_unet_step's input slice, the debug slice copy):
+// one thread per (b, pixel), all channels.
+__global__ void __launch_bounds__(256) layout_kernel(const float* __restrict__ in,
+                                                     float* __restrict__ out, int C, int HW,
+                                                     int to_nhwc) {
+  const int b = blockIdx.y;
+  const float* ib = in + (size_t)b * C * HW;
+  float* ob = out + (size_t)b * C * HW;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x)
+    for (int c = 0; c < C; ++c) {
+      if (to_nhwc)
+        ob[(size_t)p * C + c] = ib[(size_t)c * HW + p];
+      else
+        ob[(size_t)c * HW + p] = ib[(size_t)p * C + c];
+    }
+}
+
+hipError_t launch_layout(const float* in, float* out, int B, int C, int HW, bool to_nhwc,
+                         hipStream_t s) {
+  const int blocks = std::max(1, std::min((HW + 255) / 256, 4096));
+  hipLaunchKernelGGL(layout_kernel, dim3(blocks, B), dim3(256), 0, s, in, out, C, HW,
+                     to_nhwc ? 1 : 0);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -172,7 +172,7 @@ struct PipeArgs {
   float4* t1_next;
   const double* st_prev;      // [B][nsrc][3][kSlots][2]
   double* st_next;
-  float* x;                   // [B,32,H,W]
+  float* x;                   // [B,H,W,32] (NHWC)
   float* omega_out;           // [nsrc,B,H,W] (prev plane) or null
   const float* params;
   size_t off_owb, off_owb_scale;   // omega conv MFMA B fragments, their scale
@@ -395,11 +395,41 @@ __device__ __forceinline__ float4 ld_c8(__amdgpu_buffer_rsrc_t r, uint32_t p, in
   return ld4(r, (uint32_t)(s >> 1) * (uint32_t)HW * 32u + p * 32u + 16u * (uint32_t)(s & 1));
 }
 
+// sample_pos split over the two lanes of a pixel: lane h computes coordinate h (x for 0,
+// y for 1) with exactly sample_pos's operations, and the pair swaps results (DPP
+// quad_perm [1,0,3,2]): one numerator division chain per lane instead of two.
+__device__ __forceinline__ float swap_pair(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void sample_pos_pair(const float* __restrict__ m, float depth, float x,
+                                                float y, int H, int W, int h, float& ix,
+                                                float& iy) {
+  auto row = [&](int k) {
+    const float rx = __fadd_rn(__fadd_rn(__fmul_rn(m[4 * k + 0], x), __fmul_rn(m[4 * k + 1], y)),
+                               m[4 * k + 2]);
+    return __fadd_rn(__fmul_rn(rx, depth), m[4 * k + 3]);
+  };
+  const float ph = h ? row(1) : row(0);
+  float z = row(2);
+  if (z == 0.0f) z = __fadd_rn(z, 1e-4f);
+  const int dim = h ? H : W;
+  const float g = __fsub_rn(__fdiv_rn(__fdiv_rn(ph, z), (float)(dim - 1) * 0.5f), 1.0f);
+  const float i = __fmaf_rn(__fadd_rn(g, 1.0f), (float)dim * 0.5f, -0.5f);
+  const float o = swap_pair(i);
+  ix = h ? o : i;
+  iy = h ? i : o;
+}
+
 // cost_x: x_d on an 8 x 32 tile, two lanes per reference pixel (lane h holds channels
 // 8c + 4h .. 8c + 4h + 3 of every chunk c), so that one wave-wide tap load covers 32
 // pixels x 32 B of a chunk image: contiguous 1-KiB requests.  The views are
 // accumulated in view order in registers.
+// XV: bit 2 (the library's) the omega weights split over the lane pair (view v by lane
+// v & 1, swapped by DPP) and computed before the view loop: 0.46 vs 0.50 ms per plane;
+// bit 1 (microbenchmark variant) the sampling position split over the pair as well
+// (sample_pos_pair): no further gain.
 constexpr int kXRows = 8;
+template <int XV = 0>
 __global__ void __launch_bounds__(2 * kXRows * kTileW) cost_x_kernel(PipeArgs a,
                                                               const float* __restrict__ P,
                                                               const float* __restrict__ Rel) {
@@ -431,14 +461,50 @@ __global__ void __launch_bounds__(2 * kXRows * kTileW) cost_x_kernel(PipeArgs a,
   float acc[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  // omega weights of all views, each computed by one lane of the pair (view v by lane
+  // v & 1) and swapped
+  float wv[AARMVS_MAX_SRC];
+#pragma unroll
+  for (int vp = 0; vp < AARMVS_MAX_SRC; vp += 2) {
+    if ((XV & 2) && vp < nsrc) {
+      const int vm = min(vp + h, nsrc - 1);
+      const float w = omega_weight(a.t1_prev[((size_t)b * nsrc + vm) * HW + p], gs[vm], o);
+      if (a.omega_out && vp + h < nsrc) a.omega_out[((size_t)(vp + h) * a.B + b) * HW + p] = w;
+      const float ws = swap_pair(w);
+      wv[vp] = h ? ws : w;
+      if (vp + 1 < AARMVS_MAX_SRC) wv[vp + 1] = h ? w : ws;
+    }
+  }
   for (int v = 0; v < nsrc; ++v) {
     const float* __restrict__ m = Rel + 12 * (v * a.B + b);
     const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
-    const float w = omega_weight(a.t1_prev[((size_t)b * nsrc + v) * HW + p], gs[v], o);
+    float w;
+    if constexpr ((XV & 2) != 0) {
+      w = wv[0];
+#pragma unroll
+      for (int k = 1; k < AARMVS_MAX_SRC; ++k) w = v == k ? wv[k] : w;
+    } else {
+      w = omega_weight(a.t1_prev[((size_t)b * nsrc + v) * HW + p], gs[v], o);
+      if (a.omega_out && h == 0) a.omega_out[((size_t)v * a.B + b) * HW + p] = w;
+    }
     const float wp1 = __fadd_rn(w, 1.0f);
-    if (a.omega_out && h == 0) a.omega_out[((size_t)v * a.B + b) * HW + p] = w;
     const Box none{0, 0, 0, 0};
-    const TapP t = tap_p(tap_f(m, dep, gx, gy, H, W), true, H, W, false, none, fbytes / 32u);
+    TapF tf;
+    if constexpr ((XV & 1) == 0) {
+      tf = tap_f(m, dep, gx, gy, H, W);
+    } else {
+      float ix, iy;
+      sample_pos_pair(m, dep, (float)gx, (float)gy, H, W, h, ix, iy);
+      tf.xf = floorf(ix);
+      tf.yf = floorf(iy);
+      const float wx = __fsub_rn(ix, tf.xf), wy = __fsub_rn(iy, tf.yf);
+      const float ex = __fsub_rn(1.0f, wx), sy = __fsub_rn(1.0f, wy);
+      tf.wt[0] = __fmul_rn(sy, ex);
+      tf.wt[1] = __fmul_rn(sy, wx);
+      tf.wt[2] = __fmul_rn(wy, ex);
+      tf.wt[3] = __fmul_rn(wy, wx);
+    }
+    const TapP t = tap_p(tf, true, H, W, false, none, fbytes / 32u);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int s = 2 * c + h;
@@ -453,12 +519,15 @@ __global__ void __launch_bounds__(2 * kXRows * kTileW) cost_x_kernel(PipeArgs a,
       ac[3] = __fadd_rn(ac[3], __fmul_rn(wp1, sq.w));
     }
   }
-  float* xo = a.x + (size_t)b * kC * HW + p;   // NCHW
+  // NHWC: this lane's channels 8c + 4h .. +3 of pixel p, one 16-B store per chunk
+  float* xo = a.x + ((size_t)b * HW + p) * kC + 4 * h;
 #pragma unroll
-  for (int c = 0; c < 4; ++c)
+  for (int c = 0; c < 4; ++c) {
+    float r[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      xo[(size_t)(8 * c + 4 * h + j) * HW] = -1.0f * __fdiv_rn(acc[4 * c + j], (float)nsrc);
+    for (int j = 0; j < 4; ++j) r[j] = -1.0f * __fdiv_rn(acc[4 * c + j], (float)nsrc);
+    *reinterpret_cast<float4*>(xo + 8 * c) = make_float4(r[0], r[1], r[2], r[3]);
+  }
 }
 
 // omega_conv LDS images (source box, reference tile, sq tile): 32-B pixels (one chunk),
@@ -848,7 +917,7 @@ hipError_t launch_cost_x(const CostArgs& ca, const SweepGeom& g, const Workspace
   a.omega_out = omega_out;
   const int ntiles = ((g.W + kTileW - 1) / kTileW) * ((g.H + kXRows - 1) / kXRows);
   ProfScope ps(s, K_COST_X);
-  hipLaunchKernelGGL(cost_x_kernel, dim3(ntiles, g.B), dim3(2 * kXRows * kTileW), 0, s, a, a.params,
+  hipLaunchKernelGGL(cost_x_kernel<2>, dim3(ntiles, g.B), dim3(2 * kXRows * kTileW), 0, s, a, a.params,
                      a.rel);
   return hipGetLastError();
 }

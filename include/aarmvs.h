@@ -112,7 +112,8 @@ int aarmvs_sweep(const aarmvs_sweep_args* args, hipStream_t stream);
 
 /* Hidden state of the regulariser inside the workspace, for inspection/BPTT:
  * cell k in 0..4, which = 0 for h, 1 for c.  Valid after an aarmvs_sweep call;
- * returns a device pointer to [B,hid_k,H_k,W_k] or NULL. */
+ * returns a device pointer to [B,H_k,W_k,hid_k] (NHWC: the workspace keeps the U-Net
+ * tensors channel-innermost) or NULL. */
 float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int plane_parity,
                         int cell, int which);
 

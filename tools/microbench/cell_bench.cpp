@@ -1,6 +1,6 @@
 // Diagnostic harness: times the ConvLSTM cell kernels at the headline geometry
-// (1600x1184) for the library's tile configs and experimental variants (CellDef
-// specialisations >= 10 defined here).  Not shipped.
+// (1600x1184, NHWC inputs of random values) for the library's configs, the other buffer
+// mode and the ablations.  Not shipped.
 #include "../../aa-rmvsnet_amd/csrc/convlstm.hip"
 
 #include <cstdio>
@@ -70,29 +70,28 @@ int main() {
   };
   const double fl0 = 2.0 * 9 * 48 * 64 * HW, fl1 = 2.0 * 9 * 32 * 64 * HW / 4, fl3 = 2.0 * 9 * 48 * 64 * HW / 4,
                fl4 = 2.0 * 9 * 40 * 32 * HW;
-  run("cell0 f32 (TH4 NT1)", [&] { return run_cell<0>(args(0, 1), 256, K_CELL0, 0); }, fl0);
   auto h3 = [&](CellArgs a) { a.wpk = reinterpret_cast<const float*>(wh); return a; };
-  run("cell0 h3", [&] { return run_cell_h3<0>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell1 h3", [&] { return run_cell_h3<1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
-  run("cell3 h3", [&] { return run_cell_h3<3>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
-  run("cell4 h3", [&] { return run_cell_h3<4>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
-  run("cell0 h3 single-buffered", [&] { return run_cell_h3<0, 1, 8, 1, 0, 0>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell1 h3 double-buffered", [&] { return run_cell_h3<1, 1, 8, 1, 0, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
-  run("cell3 h3 single-buffered", [&] { return run_cell_h3<3, 1, 8, 1, 0, 0>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
-  run("cell4 h3 double-buffered", [&] { return run_cell_h3<4, 1, 8, 1, 0, 1>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
-  run("cell0 h3 pipelined frags (8)", [&] { return run_cell_h3<0, 1, 8, 1, 8>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell1 h3 pipelined frags (8)", [&] { return run_cell_h3<1, 1, 8, 1, 8>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
-  run("cell3 h3 pipelined frags (8)", [&] { return run_cell_h3<3, 1, 8, 1, 8>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
-  run("cell4 h3 pipelined frags (8)", [&] { return run_cell_h3<4, 1, 8, 1, 8>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
-  run("cell0 h3 NHWC staging", [&] { return run_cell_h3<0, 1, 8, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell1 h3 NHWC staging", [&] { return run_cell_h3<1, 1, 8, 2>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
-  run("cell3 h3 NHWC staging", [&] { return run_cell_h3<3, 1, 8, 2>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
-  run("cell4 h3 NHWC staging", [&] { return run_cell_h3<4, 1, 8, 2>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
-  run("cell4 h3 NHWC staging, DB", [&] { return run_cell_h3<4, 1, 8, 2, 0, 1>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
-  run("cell0 h3 NHWC no MFMA", [&] { return run_cell_h3<0, 1, 8, 2, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell0 h3 no MFMA (1)", [&] { return run_cell_h3<0, 1, 8, 1, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell0 h3 no staging (2)", [&] { return run_cell_h3<0, 1, 8, 1, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell0 h3 MFMA only (6)", [&] { return run_cell_h3<0, 1, 8, 1, 6>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell0 h3 skeleton (7)", [&] { return run_cell_h3<0, 1, 8, 1, 7>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 DB0 PIPE0", [&] { return run_cell_h3<0, 1, 8, 0, 0, 0>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 DB0 PIPE1", [&] { return run_cell_h3<0, 1, 8, 0, 0, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 DB1 PIPE0", [&] { return run_cell_h3<0, 1, 8, 0, 1, 0>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 DB1 PIPE1", [&] { return run_cell_h3<0, 1, 8, 0, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell1 h3 DB0 PIPE0", [&] { return run_cell_h3<1, 1, 8, 0, 0, 0>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell1 h3 DB0 PIPE1", [&] { return run_cell_h3<1, 1, 8, 0, 0, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell1 h3 DB1 PIPE0", [&] { return run_cell_h3<1, 1, 8, 0, 1, 0>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell1 h3 DB1 PIPE1", [&] { return run_cell_h3<1, 1, 8, 0, 1, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell3 h3 DB0 PIPE0", [&] { return run_cell_h3<3, 1, 8, 0, 0, 0>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+  run("cell3 h3 DB0 PIPE1", [&] { return run_cell_h3<3, 1, 8, 0, 0, 1>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+  run("cell3 h3 DB1 PIPE0", [&] { return run_cell_h3<3, 1, 8, 0, 1, 0>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+  run("cell3 h3 DB1 PIPE1", [&] { return run_cell_h3<3, 1, 8, 0, 1, 1>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+  run("cell4 h3 DB0 PIPE0", [&] { return run_cell_h3<4, 1, 8, 0, 0, 0>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+  run("cell4 h3 DB0 PIPE1", [&] { return run_cell_h3<4, 1, 8, 0, 0, 1>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+  run("cell4 h3 DB1 PIPE0", [&] { return run_cell_h3<4, 1, 8, 0, 1, 0>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+  run("cell4 h3 DB1 PIPE1", [&] { return run_cell_h3<4, 1, 8, 0, 1, 1>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+  run("cell0 h3 no MFMA (1)", [&] { return run_cell_h3<0, 1, 8, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 no staging (2)", [&] { return run_cell_h3<0, 1, 8, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 MFMA only (6)", [&] { return run_cell_h3<0, 1, 8, 6>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 skeleton (7)", [&] { return run_cell_h3<0, 1, 8, 7>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell4 h3 no MFMA (1)", [&] { return run_cell_h3<4, 1, 8, 1>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+  run("cell4 h3 MFMA only (6)", [&] { return run_cell_h3<4, 1, 8, 6>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
   return 0;
 }

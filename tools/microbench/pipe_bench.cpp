@@ -79,8 +79,12 @@ int main(int argc, char** argv) {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     printf("%-36s %8.3f ms  %7.0f GB/s algorithmic\n", name, ms / R, bytes / (ms / R) / 1e6);
   };
-  run("cost_x", cost_x_kernel, dim3(tiles_x * ((H + kXRows - 1) / kXRows), B), 2 * kXRows * kTileW,
-      128.0 * (nsrc + 2) * HW);
+  const dim3 gx(tiles_x * ((H + kXRows - 1) / kXRows), B);
+  const double bx = 128.0 * (nsrc + 2) * HW;
+  run("cost_x", cost_x_kernel<0>, gx, 2 * kXRows * kTileW, bx);
+  run("cost_x pair sample_pos (1)", cost_x_kernel<1>, gx, 2 * kXRows * kTileW, bx);
+  run("cost_x pair omega (2)", cost_x_kernel<2>, gx, 2 * kXRows * kTileW, bx);
+  run("cost_x pair both (3)", cost_x_kernel<3>, gx, 2 * kXRows * kTileW, bx);
   const dim3 gc(tiles_x * ((H + kTileH - 1) / kTileH) * nsrc, 1, B);
   const double bc = (128.0 * (nsrc + 1) + 16.0 * nsrc) * HW;
   run("omega_conv", omega_conv_kernel<0>, gc, kTileThreads, bc);
