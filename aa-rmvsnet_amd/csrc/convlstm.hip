@@ -610,34 +610,27 @@ __global__ void __launch_bounds__(256) deconv_kernel(const float* __restrict__ i
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int co = 0; co < 16; ++co) o[q][co] = 0.f;
-    const float4* i00 = reinterpret_cast<const float4*>(ib + (size_t)p * 16);
-    const float4* i01 = i00 + 4;
-    const float4* i10 = i00 + 4 * Wi;
-    const float4* i11 = i10 + 4;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    // one input channel per iteration (its 144 weights are scalar loads; unrolling the
+    // channel loop spills them)
+    const float* i00 = ib + (size_t)p * 16;
 #pragma unroll 1
-    for (int c4 = 0; c4 < 4; ++c4) {
-      const float4 a00 = i00[c4], a01 = hx ? i01[c4] : z4, a10 = hy ? i10[c4] : z4,
-                   a11 = (hx && hy) ? i11[c4] : z4;
-      const float f00[4] = {a00.x, a00.y, a00.z, a00.w}, f01[4] = {a01.x, a01.y, a01.z, a01.w};
-      const float f10[4] = {a10.x, a10.y, a10.z, a10.w}, f11[4] = {a11.x, a11.y, a11.z, a11.w};
+    for (int ci = 0; ci < 16; ++ci) {
+      const float v00 = i00[ci];
+      const float v01 = hx ? i00[16 + ci] : 0.f;
+      const float v10 = hy ? i00[(size_t)Wi * 16 + ci] : 0.f;
+      const float v11 = (hx && hy) ? i00[(size_t)Wi * 16 + 16 + ci] : 0.f;
+      const float* wc = w + ci * 16 * 9;   // [ci][co][ky][kx]
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int ci = 4 * c4 + u;
-        const float v00 = f00[u], v01 = f01[u], v10 = f10[u], v11 = f11[u];
-        const float* wc = w + ci * 16 * 9;   // [ci][co][ky][kx]
-#pragma unroll
-        for (int co = 0; co < 16; ++co) {
-          const float* k = wc + co * 9;
-          // out(2iy,2ix): (ky,kx)=(1,1) from (iy,ix)
-          o[0][co] = fmaf(v00, k[4], o[0][co]);
-          // out(2iy,2ix+1): kx=2 from ix, kx=0 from ix+1 (ky=1)
-          o[1][co] = fmaf(v00, k[5], fmaf(v01, k[3], o[1][co]));
-          // out(2iy+1,2ix): ky=2 from iy, ky=0 from iy+1 (kx=1)
-          o[2][co] = fmaf(v00, k[7], fmaf(v10, k[1], o[2][co]));
-          // out(2iy+1,2ix+1)
-          o[3][co] = fmaf(v00, k[8], fmaf(v01, k[6], fmaf(v10, k[2], fmaf(v11, k[0], o[3][co]))));
-        }
+      for (int co = 0; co < 16; ++co) {
+        const float* k = wc + co * 9;
+        // out(2iy,2ix): (ky,kx)=(1,1) from (iy,ix)
+        o[0][co] = fmaf(v00, k[4], o[0][co]);
+        // out(2iy,2ix+1): kx=2 from ix, kx=0 from ix+1 (ky=1)
+        o[1][co] = fmaf(v00, k[5], fmaf(v01, k[3], o[1][co]));
+        // out(2iy+1,2ix): ky=2 from iy, ky=0 from iy+1 (kx=1)
+        o[2][co] = fmaf(v00, k[7], fmaf(v10, k[1], o[2][co]));
+        // out(2iy+1,2ix+1)
+        o[3][co] = fmaf(v00, k[8], fmaf(v01, k[6], fmaf(v10, k[2], fmaf(v11, k[0], o[3][co]))));
       }
     }
 #pragma unroll
