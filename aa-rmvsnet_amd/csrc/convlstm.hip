@@ -587,68 +587,99 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
 
 // ---------------------------------------------------------------------------
 // deConvGnReLU's transposed conv (module.py:281): ConvTranspose2d(16,16,3,s2,p1,op1).
-// One thread per input pixel produces its 2x2 output quad (uniform weight taps),
-// plus GroupNorm(2,16) partial sums (the GN+ReLU itself is fused into the
-// consuming cell's input staging).  NHWC in and out: a pixel's 16 channels are 64 B.
+// One thread per input pixel produces its 2x2 output quad (uniform weight taps), plus
+// GroupNorm(2,16) partial sums (the GN+ReLU itself is fused into the consuming cell's
+// input staging).  A block takes a 256-pixel segment of an input row: the segment and
+// the one below (+ the right neighbour) are staged in LDS from contiguous NHWC runs
+// (channel stride 17: conflict-free per-channel reads), and each output row segment is
+// assembled in LDS and written back as one contiguous run.
 // ---------------------------------------------------------------------------
+constexpr int kDcTW = 256;    // input pixels per block
+constexpr int kDcOut = 20;    // LDS floats per output pixel (16 + 4 pad: 2-way writes)
 __global__ void __launch_bounds__(256) deconv_kernel(const float* __restrict__ in,
                                                      const float* __restrict__ w,
                                                      const float* __restrict__ bias, int Hi,
                                                      int Wi, float* __restrict__ out,
                                                      double* __restrict__ stats) {
+  __shared__ float tin[2][kDcTW + 1][17];
+  __shared__ __attribute__((aligned(16))) float tout[2 * kDcTW * kDcOut];
   __shared__ float red[4 * 4];
-  const int b = blockIdx.y;
-  const int HWi = Hi * Wi, Ho = 2 * Hi, Wo = 2 * Wi;
-  const float* ib = in + (size_t)b * 16 * HWi;
-  float* ob = out + (size_t)b * 16 * Ho * Wo;
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int Wo = 2 * Wi;
+  const float* ib = in + (size_t)b * 16 * Hi * Wi;
+  float* ob = out + (size_t)b * 16 * 4 * Hi * Wi;
+  const int segs = (Wi + kDcTW - 1) / kDcTW;
   float part[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HWi; p += gridDim.x * blockDim.x) {
-    const int iy = p / Wi, ix = p % Wi;
-    const bool hy = iy + 1 < Hi, hx = ix + 1 < Wi;
+  for (int t = blockIdx.x; t < Hi * segs; t += gridDim.x) {
+    const int iy = t / segs, x0 = (t % segs) * kDcTW, n = min(kDcTW, Wi - x0);
+    __syncthreads();   // the previous segment's LDS reads are done
+    for (int i = tid; i < 2 * (kDcTW + 1) * 4; i += 256) {
+      const int r = i / ((kDcTW + 1) * 4), rem = i % ((kDcTW + 1) * 4);
+      const int px = rem >> 2, c4 = rem & 3;
+      const int gy = iy + r, gx = x0 + px;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);   // zero padding past the image
+      if (px <= n && gy < Hi && gx < Wi)
+        v = *reinterpret_cast<const float4*>(ib + ((size_t)gy * Wi + gx) * 16 + 4 * c4);
+      float* d = &tin[r][px][4 * c4];
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
+    __syncthreads();
+    const int lp = tid;
     float o[4][16];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int co = 0; co < 16; ++co) o[q][co] = 0.f;
-    // one input channel per iteration (its 144 weights are scalar loads; unrolling the
-    // channel loop spills them)
-    const float* i00 = ib + (size_t)p * 16;
+    if (lp < n) {
+      // one input channel per iteration (its 144 weights are scalar loads)
 #pragma unroll 1
-    for (int ci = 0; ci < 16; ++ci) {
-      const float v00 = i00[ci];
-      const float v01 = hx ? i00[16 + ci] : 0.f;
-      const float v10 = hy ? i00[(size_t)Wi * 16 + ci] : 0.f;
-      const float v11 = (hx && hy) ? i00[(size_t)Wi * 16 + 16 + ci] : 0.f;
-      const float* wc = w + ci * 16 * 9;   // [ci][co][ky][kx]
+      for (int ci = 0; ci < 16; ++ci) {
+        const float v00 = tin[0][lp][ci], v01 = tin[0][lp + 1][ci];
+        const float v10 = tin[1][lp][ci], v11 = tin[1][lp + 1][ci];
+        const float* wc = w + ci * 16 * 9;   // [ci][co][ky][kx]
 #pragma unroll
-      for (int co = 0; co < 16; ++co) {
-        const float* k = wc + co * 9;
-        // out(2iy,2ix): (ky,kx)=(1,1) from (iy,ix)
-        o[0][co] = fmaf(v00, k[4], o[0][co]);
-        // out(2iy,2ix+1): kx=2 from ix, kx=0 from ix+1 (ky=1)
-        o[1][co] = fmaf(v00, k[5], fmaf(v01, k[3], o[1][co]));
-        // out(2iy+1,2ix): ky=2 from iy, ky=0 from iy+1 (kx=1)
-        o[2][co] = fmaf(v00, k[7], fmaf(v10, k[1], o[2][co]));
-        // out(2iy+1,2ix+1)
-        o[3][co] = fmaf(v00, k[8], fmaf(v01, k[6], fmaf(v10, k[2], fmaf(v11, k[0], o[3][co]))));
+        for (int co = 0; co < 16; ++co) {
+          const float* k = wc + co * 9;
+          // out(2iy,2ix): (ky,kx)=(1,1) from (iy,ix)
+          o[0][co] = fmaf(v00, k[4], o[0][co]);
+          // out(2iy,2ix+1): kx=2 from ix, kx=0 from ix+1 (ky=1)
+          o[1][co] = fmaf(v00, k[5], fmaf(v01, k[3], o[1][co]));
+          // out(2iy+1,2ix): ky=2 from iy, ky=0 from iy+1 (kx=1)
+          o[2][co] = fmaf(v00, k[7], fmaf(v10, k[1], o[2][co]));
+          // out(2iy+1,2ix+1)
+          o[3][co] = fmaf(v00, k[8], fmaf(v01, k[6], fmaf(v10, k[2], fmaf(v11, k[0], o[3][co]))));
+        }
       }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int oy = 2 * iy + (q >> 1), ox = 2 * ix + (q & 1);
-      float4* op = reinterpret_cast<float4*>(ob + ((size_t)oy * Wo + ox) * 16);
+    for (int ry = 0; ry < 2; ++ry) {
+      if (lp < n) {
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        float r[4];
+        for (int dxo = 0; dxo < 2; ++dxo) {
+          float4* d = reinterpret_cast<float4*>(&tout[(2 * lp + dxo) * kDcOut]);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int co = 4 * c4 + u;
-          r[u] = o[q][co] + bias[co];
-          part[(co >> 3) * 2] += r[u];
-          part[(co >> 3) * 2 + 1] += r[u] * r[u];
+          for (int c4 = 0; c4 < 4; ++c4) {
+            float r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int co = 4 * c4 + u;
+              r[u] = o[2 * ry + dxo][co] + bias[co];
+              part[(co >> 3) * 2] += r[u];
+              part[(co >> 3) * 2 + 1] += r[u] * r[u];
+            }
+            d[c4] = make_float4(r[0], r[1], r[2], r[3]);
+          }
         }
-        op[c4] = make_float4(r[0], r[1], r[2], r[3]);
       }
+      __syncthreads();
+      // output row 2 iy + ry, pixels 2 x0 .. 2 (x0 + n) - 1: one contiguous run
+      float4* orow = reinterpret_cast<float4*>(ob + ((size_t)(2 * iy + ry) * Wo + 2 * x0) * 16);
+      for (int j = tid; j < 2 * n * 4; j += 256)
+        orow[j] = *reinterpret_cast<const float4*>(&tout[(j >> 2) * kDcOut + 4 * (j & 3)]);
+      __syncthreads();
     }
   }
   block_sum<4>(part, red);
@@ -812,7 +843,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
   {
     const int Hi = H / 4, Wi = W / 4;
-    const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 8 * cu));
+    const int blocks = std::max(1, std::min(Hi * ((Wi + kDcTW - 1) / kDcTW), 4 * cu));
     for (int b = 0; b < B; ++b) {
       double* st = ws.reg_stats + reg_stat_index(b, 0, 0);
       ProfScope ps(s, K_DECONV0);
@@ -840,7 +871,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // deconv_1: h3' (H/2) -> u1 (H) + GN stats
   {
     const int Hi = H / 2, Wi = W / 2;
-    const int blocks = std::max(1, std::min((Hi * Wi + 255) / 256, 8 * cu));
+    const int blocks = std::max(1, std::min(Hi * ((Wi + kDcTW - 1) / kDcTW), 4 * cu));
     for (int b = 0; b < B; ++b) {
       double* st = ws.reg_stats + reg_stat_index(b, 1, 0);
       ProfScope ps(s, K_DECONV1);
