@@ -46,6 +46,10 @@ const ParamLayout& param_layout() {
     pk += 4 * 5 * 64 * 8 / 2;   // halves -> floats
     l.owb_scale_off = pk;
     pk += 64;
+    for (int k = 0; k < 2; ++k) {
+      l.dct_off[k] = pk;
+      pk += 16 * 9 * 16;
+    }
     l.raw_total = raw;
     l.pk_total = pk;
     return l;
@@ -276,6 +280,20 @@ __global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __r
   }
 }
 
+// deconv weights [ci][co][ky][kx] (ConvTranspose2d) -> [ci][tap][co]: the 16 output
+// channels of one (ci, tap) are contiguous, so the deconv's packed FMAs pair adjacent
+// scalar registers
+__global__ void pack_deconv_kernel(const float* __restrict__ raw, float* __restrict__ pk,
+                                   ParamLayout L) {
+  const int k = blockIdx.x;
+  const float* w = raw + L.raw_off[k ? P_D1W : P_D0W];
+  float* d = pk + L.dct_off[k];
+  for (int i = threadIdx.x; i < 16 * 9 * 16; i += blockDim.x) {
+    const int co = i % 16, tap = (i / 16) % 9, ci = i / 144;
+    d[i] = w[(ci * 16 + co) * 9 + tap];
+  }
+}
+
 hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s) {
   const ParamLayout& L = param_layout();
   hipError_t e = hipMemsetAsync(packed, 0, L.pk_total * sizeof(float), s);
@@ -285,6 +303,8 @@ hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s) {
   hipLaunchKernelGGL(pack_cell_h3_kernel, dim3(5), dim3(256), 0, s, raw, packed, L);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(pack_omega_conv_kernel, dim3(1), dim3(256), 0, s, raw, packed, L);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(pack_deconv_kernel, dim3(2), dim3(256), 0, s, raw, packed, L);
   return hipGetLastError();
 }
 

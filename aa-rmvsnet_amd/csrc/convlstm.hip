@@ -639,18 +639,18 @@ __global__ void __launch_bounds__(256) deconv_kernel(const float* __restrict__ i
       for (int ci = 0; ci < 16; ++ci) {
         const float v00 = tin[0][lp][ci], v01 = tin[0][lp + 1][ci];
         const float v10 = tin[1][lp][ci], v11 = tin[1][lp + 1][ci];
-        const float* wc = w + ci * 16 * 9;   // [ci][co][ky][kx]
+        const float* wc = w + ci * 9 * 16;   // [ci][tap][co] (pack_deconv_kernel)
 #pragma unroll
         for (int co = 0; co < 16; ++co) {
-          const float* k = wc + co * 9;
+          auto k = [&](int tap) { return wc[tap * 16 + co]; };
           // out(2iy,2ix): (ky,kx)=(1,1) from (iy,ix)
-          o[0][co] = fmaf(v00, k[4], o[0][co]);
+          o[0][co] = fmaf(v00, k(4), o[0][co]);
           // out(2iy,2ix+1): kx=2 from ix, kx=0 from ix+1 (ky=1)
-          o[1][co] = fmaf(v00, k[5], fmaf(v01, k[3], o[1][co]));
+          o[1][co] = fmaf(v00, k(5), fmaf(v01, k(3), o[1][co]));
           // out(2iy+1,2ix): ky=2 from iy, ky=0 from iy+1 (kx=1)
-          o[2][co] = fmaf(v00, k[7], fmaf(v10, k[1], o[2][co]));
+          o[2][co] = fmaf(v00, k(7), fmaf(v10, k(1), o[2][co]));
           // out(2iy+1,2ix+1)
-          o[3][co] = fmaf(v00, k[8], fmaf(v01, k[6], fmaf(v10, k[2], fmaf(v11, k[0], o[3][co]))));
+          o[3][co] = fmaf(v00, k(8), fmaf(v01, k(6), fmaf(v10, k(2), fmaf(v11, k(0), o[3][co]))));
         }
       }
     }
@@ -848,7 +848,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
       double* st = ws.reg_stats + reg_stat_index(b, 0, 0);
       ProfScope ps(s, K_DECONV0);
       hipLaunchKernelGGL(deconv_kernel, dim3(blocks, 1), dim3(256), 0, s,
-                         ws.h[2][nxt] + (size_t)b * 16 * Hi * Wi, params + L.pk_off[P_D0W],
+                         ws.h[2][nxt] + (size_t)b * 16 * Hi * Wi, params + L.dct_off[0],
                          params + L.pk_off[P_D0B], Hi, Wi, ws.u0 + (size_t)b * 16 * 4 * Hi * Wi,
                          st);
       if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -876,7 +876,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
       double* st = ws.reg_stats + reg_stat_index(b, 1, 0);
       ProfScope ps(s, K_DECONV1);
       hipLaunchKernelGGL(deconv_kernel, dim3(blocks, 1), dim3(256), 0, s,
-                         ws.h[3][nxt] + (size_t)b * 16 * Hi * Wi, params + L.pk_off[P_D1W],
+                         ws.h[3][nxt] + (size_t)b * 16 * Hi * Wi, params + L.dct_off[1],
                          params + L.pk_off[P_D1B], Hi, Wi, ws.u1 + (size_t)b * 16 * 4 * Hi * Wi,
                          st);
       if ((e = hipGetLastError()) != hipSuccess) return e;
