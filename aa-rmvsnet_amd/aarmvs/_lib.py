@@ -36,6 +36,29 @@ class SweepArgs(ctypes.Structure):
     ]
 
 
+MAX_FUSION_SRC = 10
+
+
+def fusion_cam_floats(nsrc: int) -> int:
+    return 18 + 42 * nsrc
+
+
+class FusionArgs(ctypes.Structure):
+    """Mirror of ``aarmvs_fusion_args``."""
+    _fields_ = [
+        ("H", c_int), ("W", c_int), ("nsrc", c_int),
+        ("ref_depth", c_void_p),
+        ("confidence", c_void_p),
+        ("src_depth", c_void_p * MAX_FUSION_SRC),
+        ("cams", c_void_p),
+        ("photo_threshold", ctypes.c_float),
+        ("photo_mask", c_void_p),
+        ("geo_mask", c_void_p),
+        ("final_mask", c_void_p),
+        ("depth_avg", c_void_p),
+    ]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "aarmvs_last_error": (c_char_p, []),
@@ -53,6 +76,7 @@ SIGNATURES = {
     "aarmvs_unet_step": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),
     "aarmvs_softmax_depth": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "aarmvs_fusion_filter": (c_int, [ctypes.POINTER(FusionArgs), c_void_p]),
     "aarmvs_profile_enable": (None, [c_int]),
     "aarmvs_profile_reset": (None, []),
     "aarmvs_profile_kernel_count": (c_int, []),

@@ -1,0 +1,177 @@
+"""Depth-map fusion (the reference's fusion.py) on the HIP library.
+
+``filter_depth_core`` is the per-reference-view core of ``filter_depth``
+(fusion.py:174-220): photometric mask, geometric consistency against every source view
+(``reproject_with_depth`` / ``check_geometric_consistency``, fusion.py:71-133), the
+per-threshold votes, the geometric and final masks and the averaged depth -- one HIP
+launch (``aarmvs_fusion_filter``).  ``fuse_points`` back-projects the kept pixels to world
+points (fusion.py:235-246), and the file helpers read/write the formats the fusion step
+consumes: PFM maps (datasets/data_io.py:9-74), cam files (fusion.py:27-42), pair files
+(fusion.py:57-68), and a binary PLY writer for the point cloud.
+Depth maps must be CUDA float32 tensors; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+import sys
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import AarmvsError, check, lib
+
+
+def pack_cameras(ref_cam, src_cams) -> np.ndarray:
+    """float32 matrices exactly as numpy forms them in fusion.py:71-108 (float32 inverses
+    and float32 products), packed for ``aarmvs_fusion_filter`` (include/aarmvs.h)."""
+    K_ref = np.asarray(ref_cam[0], np.float32)
+    E_ref = np.asarray(ref_cam[1], np.float32)
+    parts = [np.linalg.inv(K_ref).ravel(), K_ref.ravel()]
+    for K, E in src_cams:
+        K = np.asarray(K, np.float32)
+        E = np.asarray(E, np.float32)
+        parts += [K.ravel(), np.linalg.inv(K).ravel(),
+                  np.matmul(E, np.linalg.inv(E_ref))[:3].ravel(),
+                  np.matmul(E_ref, np.linalg.inv(E))[:3].ravel()]
+    out = np.concatenate(parts).astype(np.float32)
+    assert out.size == _lib.fusion_cam_floats(len(src_cams))
+    return np.ascontiguousarray(out)
+
+
+def filter_depth_core(ref_depth: torch.Tensor, confidence: torch.Tensor, ref_cam, src_depths,
+                      src_cams, photo_threshold: float):
+    """(photo_mask, geo_mask, final_mask [H,W] bool, depth_est_averaged [H,W] float64)."""
+    nsrc = len(src_depths)
+    if not 1 <= nsrc <= _lib.MAX_FUSION_SRC:
+        raise AarmvsError(f"aarmvs: fusion needs 1..{_lib.MAX_FUSION_SRC} source views, got {nsrc}")
+    maps = [ref_depth, confidence, *src_depths]
+    for t in maps:
+        if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32):
+            raise AarmvsError("aarmvs: fusion depth maps / confidence must be CUDA float32 tensors")
+        if t.shape != ref_depth.shape or t.dim() != 2:
+            raise AarmvsError("aarmvs: fusion maps must all be [H,W] of the same size")
+    maps = [t.contiguous() for t in maps]
+    H, W = ref_depth.shape
+    dev = ref_depth.device
+    cams = pack_cameras(ref_cam, src_cams)
+    photo = torch.empty(H, W, dtype=torch.uint8, device=dev)
+    geo = torch.empty_like(photo)
+    final = torch.empty_like(photo)
+    avg = torch.empty(H, W, dtype=torch.float64, device=dev)
+    a = _lib.FusionArgs()
+    a.H, a.W, a.nsrc = H, W, nsrc
+    a.ref_depth = maps[0].data_ptr()
+    a.confidence = maps[1].data_ptr()
+    for i, t in enumerate(maps[2:]):
+        a.src_depth[i] = t.data_ptr()
+    a.cams = cams.ctypes.data
+    a.photo_threshold = float(np.float32(photo_threshold))
+    a.photo_mask, a.geo_mask, a.final_mask = photo.data_ptr(), geo.data_ptr(), final.data_ptr()
+    a.depth_avg = avg.data_ptr()
+    check(lib().aarmvs_fusion_filter(ctypes.byref(a), torch.cuda.current_stream().cuda_stream),
+          "fusion_filter")
+    return photo.bool(), geo.bool(), final.bool(), avg
+
+
+def fuse_points(depth_est_averaged, final_mask, ref_cam, ref_img=None):
+    """World points (float32 [n,3]) and colours (uint8 [n,3] or None) of the kept pixels
+    (fusion.py:235-246), host numpy."""
+    depth = depth_est_averaged.cpu().numpy() if isinstance(depth_est_averaged, torch.Tensor) else depth_est_averaged
+    valid = final_mask.cpu().numpy() if isinstance(final_mask, torch.Tensor) else final_mask
+    K, E = (np.asarray(m, np.float32) for m in ref_cam)
+    height, width = depth.shape[:2]
+    x, y = np.meshgrid(np.arange(0, width), np.arange(0, height))
+    x, y, d = x[valid], y[valid], depth[valid]
+    xyz_ref = np.matmul(np.linalg.inv(K), np.vstack((x, y, np.ones_like(x))) * d)
+    xyz_world = np.matmul(np.linalg.inv(E), np.vstack((xyz_ref, np.ones_like(x))))[:3]
+    colors = None if ref_img is None else (np.asarray(ref_img)[valid] * 255).astype(np.uint8)
+    return xyz_world.transpose((1, 0)).astype(np.float32), colors
+
+
+# ---------------------------------------------------------------------------------
+# file formats
+# ---------------------------------------------------------------------------------
+def read_pfm(filename):
+    """(data float32 [H,W] or [H,W,3], scale), rows bottom-up in the file (data_io.py:9-45)."""
+    with open(filename, "rb") as f:
+        header = f.readline().decode("utf-8").rstrip()
+        if header not in ("PF", "Pf"):
+            raise ValueError("Not a PFM file.")
+        m = re.match(r"^(\d+)\s(\d+)\s$", f.readline().decode("utf-8"))
+        if not m:
+            raise ValueError("Malformed PFM header.")
+        width, height = map(int, m.groups())
+        scale = float(f.readline().rstrip())
+        endian = "<" if scale < 0 else ">"
+        data = np.fromfile(f, endian + "f")
+    shape = (height, width, 3) if header == "PF" else (height, width)
+    return np.flipud(np.reshape(data, shape)), abs(scale)
+
+
+def save_pfm(filename, image, scale=1):
+    """data_io.py:48-74: float32 [H,W] / [H,W,1] / [H,W,3], native byte order."""
+    if image.dtype != np.float32:
+        raise ValueError("Image dtype must be float32.")
+    if image.ndim == 3 and image.shape[2] == 3:
+        color = True
+    elif image.ndim == 2 or (image.ndim == 3 and image.shape[2] == 1):
+        color = False
+    else:
+        raise ValueError("Image must have H x W x 3, H x W x 1 or H x W dimensions.")
+    image = np.flipud(image)
+    endian = image.dtype.byteorder
+    if endian == "<" or (endian == "=" and sys.byteorder == "little"):
+        scale = -scale
+    with open(filename, "wb") as f:
+        f.write(b"PF\n" if color else b"Pf\n")
+        f.write(f"{image.shape[1]} {image.shape[0]}\n".encode("utf-8"))
+        f.write(("%f\n" % scale).encode("utf-8"))
+        np.ascontiguousarray(image).tofile(f)
+
+
+def read_camera_parameters(filename, scale=1.0, index=0, flag=0):
+    """(intrinsics float32 3x3, extrinsics float32 4x4) of a cam.txt, intrinsics scaled and
+    shifted for the resized / cropped image (fusion.py:27-42)."""
+    with open(filename) as f:
+        lines = [line.rstrip() for line in f.readlines()]
+    extrinsics = np.array(" ".join(lines[1:5]).split(), dtype=np.float32).reshape((4, 4))
+    intrinsics = np.array(" ".join(lines[7:10]).split(), dtype=np.float32).reshape((3, 3))
+    intrinsics[:2, :] *= scale
+    if flag == 0:
+        intrinsics[0, 2] -= index
+    else:
+        intrinsics[1, 2] -= index
+    return intrinsics, extrinsics
+
+
+def read_pair_file(filename):
+    """[(ref_view, [src_view, ...]), ...] (fusion.py:57-68)."""
+    data = []
+    with open(filename) as f:
+        num_viewpoint = int(f.readline())
+        for _ in range(num_viewpoint):
+            ref_view = int(f.readline().rstrip())
+            src_views = [int(x) for x in f.readline().rstrip().split()[1::2]]
+            data.append((ref_view, src_views))
+    return data
+
+
+def write_ply(filename, xyz, rgb=None):
+    """Binary little-endian PLY of float32 x, y, z (+ uint8 red, green, blue) vertices."""
+    xyz = np.asarray(xyz, np.float32)
+    n = xyz.shape[0]
+    fields = [("x", "<f4"), ("y", "<f4"), ("z", "<f4")]
+    if rgb is not None:
+        fields += [("red", "u1"), ("green", "u1"), ("blue", "u1")]
+    v = np.empty(n, dtype=fields)
+    v["x"], v["y"], v["z"] = xyz[:, 0], xyz[:, 1], xyz[:, 2]
+    if rgb is not None:
+        rgb = np.asarray(rgb, np.uint8)
+        v["red"], v["green"], v["blue"] = rgb[:, 0], rgb[:, 1], rgb[:, 2]
+    props = "".join(f"property {'float' if t == '<f4' else 'uchar'} {name}\n" for name, t in fields)
+    header = f"ply\nformat binary_little_endian 1.0\nelement vertex {n}\n{props}end_header\n"
+    with open(filename, "wb") as f:
+        f.write(header.encode("ascii"))
+        f.write(v.tobytes())

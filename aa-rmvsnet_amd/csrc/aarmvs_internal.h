@@ -116,6 +116,8 @@ struct CostArgs {
 // plane d (omega_conv + omega_stats<1> + <2>).  The statistics of a plane must be zero
 // before its omega_next and are cleared by the caller once its cost_x has run.
 // NCHW <-> NHWC copy of a [B][C][HW] / [B][HW][C] fp32 tensor (API edges only)
+// depth-map fusion core (fusion.hip)
+hipError_t launch_fusion_filter(const aarmvs_fusion_args* a, hipStream_t s);
 hipError_t launch_layout(const float* in, float* out, int B, int C, int HW, bool to_nhwc,
                          hipStream_t s);
 hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s);
@@ -141,7 +143,7 @@ int cu_count();
 // stream around each kernel.  Off by default; costs nothing when off.
 // ---------------------------------------------------------------------------
 enum KernelId : int {
-  K_COST_X, K_OMEGA_CONV, K_OMEGA1, K_OMEGA2,
+  K_COST_X, K_OMEGA_CONV, K_FUSION, K_OMEGA1, K_OMEGA2,
   K_CELL0, K_CELL1, K_CELL2, K_CELL3, K_CELL4,
   K_DECONV0, K_DECONV1, K_HEAD_WTA, K_FINALIZE, K_SOFTMAX, K_WARP, K_TO_C8,
   K_COUNT

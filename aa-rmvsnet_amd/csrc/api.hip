@@ -75,7 +75,7 @@ static double g_prof_ms[K_COUNT];
 static long long g_prof_n[K_COUNT];
 
 static const char* kKernelNames[K_COUNT] = {
-    "cost_x", "omega_conv", "omega_stats1", "omega_stats2",
+    "cost_x", "omega_conv", "fusion", "omega_stats1", "omega_stats2",
     "lstm_cell0", "lstm_cell1", "lstm_cell2", "lstm_cell3", "lstm_cell4",
     "deconv0", "deconv1", "head_wta", "finalize", "softmax_depth", "homo_warp", "to_c8"};
 
@@ -546,6 +546,19 @@ int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
       hipSuccess)
     return hip_fail(e, "unet_step: head");
   return AARMVS_OK;
+}
+
+int aarmvs_fusion_filter(const aarmvs_fusion_args* a, hipStream_t stream) {
+  if (!a) return fail(AARMVS_ERR_INVALID, "fusion_filter: null args");
+  if (a->H < 1 || a->W < 1 || a->nsrc < 1 || a->nsrc > AARMVS_MAX_FUSION_SRC)
+    return fail(AARMVS_ERR_INVALID, "fusion_filter: need H, W >= 1 and 1 <= nsrc <= 10");
+  if (!a->ref_depth || !a->confidence || !a->cams || !a->photo_mask || !a->geo_mask ||
+      !a->final_mask || !a->depth_avg)
+    return fail(AARMVS_ERR_INVALID, "fusion_filter: null pointer argument");
+  for (int v = 0; v < a->nsrc; ++v)
+    if (!a->src_depth[v]) return fail(AARMVS_ERR_INVALID, "fusion_filter: null src_depth pointer");
+  hipError_t e = launch_fusion_filter(a, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "fusion_filter");
 }
 
 int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW, hipStream_t stream) {

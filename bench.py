@@ -155,6 +155,46 @@ def cpu_baseline(feats, proj, dv, P, planes: int):
                             f"{W}x{H}, {dt:.1f} s, torch CPU threads={torch.get_num_threads()}")
 
 
+def fusion_bench(H: int, W: int, nsrc: int, dev, cpu_leg: bool, reps: int = 10):
+    """The depth-map fusion core (aarmvs.fusion.filter_depth_core, fusion.py:174-220) on one
+    reference view with nsrc source views at the sweep's resolution: GPU time per view with
+    hipEvents, HBM roofline on its algorithmic bytes ((19 + 4 nsrc) B per reference pixel:
+    depth + confidence + one depth read per source view + three masks + the float64
+    average), and the CPU oracle on a 2-source-view sample of the same maps."""
+    from aarmvs import fusion
+    from oracle import fusion_oracle as fo
+    depths, cams, conf = fo.synthetic_views(H, W, nsrc, seed=7)
+    t = [torch.from_numpy(d).to(dev) for d in depths]
+    c = torch.from_numpy(conf).to(dev)
+    run = lambda: fusion.filter_depth_core(t[0], c, cams[0], t[1:], cams[1:], 0.35)  # noqa: E731
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        out = run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    px = H * W
+    bytes_ = (19.0 + 4.0 * nsrc) * px
+    ach = bytes_ / (ms / 1e3) / 1e9
+    res = dict(metric="fusion ref-view pixels/s (nsrc source views each)", value=round(px / (ms / 1e3), 1),
+               ms_per_view=round(ms, 4), H=H, W=W, nsrc=nsrc, achieved_gbs=round(ach, 1),
+               peak_gbs=HBM_PEAK_GBS, frac=round(ach / HBM_PEAK_GBS, 4),
+               geo_mask_mean=round(float(out[1].float().mean()), 4))
+    if cpu_leg:
+        k = 2
+        t0 = time.perf_counter()
+        fo.filter_depth_core(depths[0], conf, cams[0], depths[1:1 + k], cams[1:1 + k], 0.35)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = dict(value=round(px * k / nsrc / dt, 1), unit="ref-view pixels/s",
+                                   cores=1, kind="port",
+                                   sample=f"oracle/fusion_oracle.py filter_depth_core, {k} of {nsrc} "
+                                          f"source views ({dt:.1f} s), scaled to {nsrc}")
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -169,6 +209,8 @@ def main():
                     help="run the omega pipeline on the main stream (no second stream)")
     ap.add_argument("--high-priority", action="store_true",
                     help="run the sweep's main stream at high priority (aux stream normal)")
+    ap.add_argument("--no-fusion", action="store_true",
+                    help="skip the depth-map fusion measurement (the next §8 row)")
     ap.add_argument("--planes", type=int, default=0,
                     help="profiling aid: sweep only the first P depth planes (0 = all D); "
                          "per-launch figures are unchanged, the headline value is not comparable")
@@ -269,6 +311,10 @@ def main():
         parity = dict(sample_planes=planes, cost_max_abs_err=cost_err, depth_rel_l1=rl1)
         cpu["value"] = round(cpu["value"], 1)
 
+    fusion_res = None
+    if rank == 0 and world == 1 and not args.no_fusion:
+        fusion_res = fusion_bench(H, W, 10, dev, cpu_leg=not args.no_cpu)
+
     if rank == 0:
         line = {
             "metric": "depth-hypotheses/sec (ref-views x H x W x D / s)",
@@ -288,6 +334,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,
+            "fusion": fusion_res,
             "kernels": {k: {kk: vv for kk, vv in v.items() if kk != "per_launch"}
                         for k, v in kernels.items()},
         }

@@ -131,6 +131,35 @@ int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
                          hipStream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Depth-map fusion core of one reference view (fusion.py:71-220, the per-view part of
+ * filter_depth after file I/O): for every reference pixel the geometric consistency
+ * against each source view's depth map (reproject_with_depth, check_geometric_consistency)
+ * and filter_depth's photometric mask, per-threshold votes, geometric mask and averaged
+ * depth.  Depth maps and confidence are device [H,W] float32 (all views the same size);
+ * `cams` is HOST memory, AARMVS_FUSION_CAM_FLOATS(nsrc) float32 values as numpy forms
+ * them in the reference (float32 inverses and products): inv(K_ref) 3x3, K_ref 3x3, then
+ * per source view K 3x3, inv(K) 3x3, (E_src inv(E_ref))[:3] 3x4, (E_ref inv(E_src))[:3]
+ * 3x4, row-major (aarmvs/fusion.py packs them).  Outputs (device): three [H,W] uint8
+ * masks (photo, geo, final) and the [H,W] float64 averaged depth.  1 <= nsrc <=
+ * AARMVS_MAX_FUSION_SRC (the reference indexes its mask list up to 10 source views).
+ * ------------------------------------------------------------------------- */
+#define AARMVS_MAX_FUSION_SRC 10
+#define AARMVS_FUSION_CAM_FLOATS(nsrc) (18 + 42 * (nsrc))
+typedef struct aarmvs_fusion_args {
+  int H, W, nsrc;
+  const float* ref_depth;                          /* [H,W]                 */
+  const float* confidence;                         /* [H,W]                 */
+  const float* src_depth[AARMVS_MAX_FUSION_SRC];   /* nsrc x [H,W]          */
+  const float* cams;                               /* host, see above       */
+  float photo_threshold;                           /* 0.35 DTU, 0.2 T&T     */
+  unsigned char* photo_mask;                       /* [H,W] out             */
+  unsigned char* geo_mask;                         /* [H,W] out             */
+  unsigned char* final_mask;                       /* [H,W] out             */
+  double* depth_avg;                               /* [H,W] out             */
+} aarmvs_fusion_args;
+int aarmvs_fusion_filter(const aarmvs_fusion_args* args, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Opt-in per-kernel timing (a diagnostic, not part of the reference interface).
  * When enabled, every launch made by the entry points above is bracketed by
  * hipEvents on its stream; aarmvs_profile_read synchronises on the recorded

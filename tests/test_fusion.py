@@ -1,0 +1,111 @@
+"""Depth-map fusion (fusion.py) -- the oracle's known answers, the file formats, and (GPU)
+the HIP filter against the oracle.
+
+cv2 and plyfile are not installed in this image and the reference ships no fusion
+fixtures: the cv2.remap restatement is checked against known answers of OpenCV's
+published INTER_LINEAR algorithm (1/32-px coordinates, table weights, zero border), not
+against cv2 itself (parity unpinned for that step)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "aa-rmvsnet_amd"))
+
+from oracle import fusion_oracle as fo  # noqa: E402
+from aarmvs import fusion  # noqa: E402
+
+
+def test_remap_known_answers():
+    src = np.arange(12, dtype=np.float32).reshape(3, 4)
+    mx = np.array([[0, 1, 2.5, 3, -1, 0.5]], np.float32)
+    my = np.array([[0, 1, 0, 2, 0, 0.25]], np.float32)
+    out = fo.remap_linear(src, mx, my)
+    # integer points read the pixel; (2.5, 0) averages 2 and 3; (3, 2) = 11 (right tap outside,
+    # weight 0); (-1, 0): all taps outside but the right one, weight 0 -> 0; (0.5, 0.25)
+    # bilinear with 1/32 weights
+    want = [0.0, 5.0, 2.5, 11.0, 0.0, 0.75 * (0.5 * 0 + 0.5 * 1) + 0.25 * (0.5 * 4 + 0.5 * 5)]
+    np.testing.assert_allclose(out[0], np.array(want, np.float32), rtol=0, atol=1e-6)
+    # coordinates are rounded to 1/32 px (half to even): 0.015625 = 0.5/32 -> 0
+    out = fo.remap_linear(src, np.array([[0.015625, 0.046875]], np.float32), np.zeros((1, 2), np.float32))
+    np.testing.assert_array_equal(out[0], np.array([0.0, 2 / 32], np.float32))
+    # non-finite coordinates read the border value
+    out = fo.remap_linear(src, np.array([[np.inf, np.nan]], np.float32), np.zeros((1, 2), np.float32))
+    np.testing.assert_array_equal(out[0], np.zeros(2, np.float32))
+
+
+def test_filter_core_on_a_consistent_scene():
+    depths, cams, conf = fo.synthetic_views(48, 64, 4, seed=3)
+    photo, geo, final, avg = fo.filter_depth_core(depths[0], conf, cams[0], depths[1:], cams[1:], 0.35)
+    assert photo.dtype == bool and geo.dtype == bool and avg.dtype == np.float64
+    np.testing.assert_array_equal(final, photo & geo)
+    assert geo.mean() > 0.6          # the views see one surface
+    good = geo & (depths[0] > 0)
+    rel = np.abs(avg[good] - depths[0][good]) / depths[0][good]
+    assert np.median(rel) < 2e-3     # averaged with consistent reprojections
+
+
+def test_pfm_cam_pair_roundtrip(tmp_path):
+    img = np.random.default_rng(0).random((5, 7)).astype(np.float32)
+    fusion.save_pfm(str(tmp_path / "d.pfm"), img)
+    back, scale = fusion.read_pfm(str(tmp_path / "d.pfm"))
+    np.testing.assert_array_equal(back, img)
+    assert scale == 1.0
+    rgb = np.random.default_rng(1).random((4, 3, 3)).astype(np.float32)
+    fusion.save_pfm(str(tmp_path / "c.pfm"), rgb)
+    np.testing.assert_array_equal(fusion.read_pfm(str(tmp_path / "c.pfm"))[0], rgb)
+    # a cam.txt in the DTU / MVSNet layout (extrinsic, 4 rows; intrinsic, 3 rows; depth range)
+    cam = ("extrinsic\n1 0 0 10\n0 1 0 20\n0 0 1 30\n0 0 0 1\n\nintrinsic\n"
+           "361.54 0 82.9\n0 360.4 66.4\n0 0 1\n\n425 2.5\n")
+    (tmp_path / "00000000_cam.txt").write_text(cam)
+    K, E = fusion.read_camera_parameters(str(tmp_path / "00000000_cam.txt"), scale=2.0, index=3, flag=0)
+    assert K.dtype == np.float32 and E.dtype == np.float32
+    np.testing.assert_allclose(E[:3, 3], [10, 20, 30])
+    np.testing.assert_allclose(K[0], np.array([361.54 * 2, 0, 82.9 * 2 - 3], np.float32))
+    (tmp_path / "pair.txt").write_text("2\n0\n3 1 2.5 2 1.0 5 0.3\n1\n1 0 9.0\n")
+    assert fusion.read_pair_file(str(tmp_path / "pair.txt")) == [(0, [1, 2, 5]), (1, [0])]
+    xyz = np.arange(12, dtype=np.float32).reshape(4, 3)
+    fusion.write_ply(str(tmp_path / "p.ply"), xyz, np.full((4, 3), 7, np.uint8))
+    raw = (tmp_path / "p.ply").read_bytes()
+    head, body = raw.split(b"end_header\n", 1)
+    assert b"element vertex 4" in head and len(body) == 4 * 15
+
+
+def test_camera_pack_layout():
+    _, cams, _ = fo.synthetic_views(8, 8, 3)
+    p = fusion.pack_cameras(cams[0], cams[1:])
+    assert p.dtype == np.float32 and p.size == 18 + 42 * 3
+    np.testing.assert_array_equal(p[:9], np.linalg.inv(cams[0][0]).ravel())
+    np.testing.assert_array_equal(p[18 + 18:18 + 30], np.matmul(cams[1][1], np.linalg.inv(cams[0][1]))[:3].ravel())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,nsrc,seed", [(96, 128, 10, 0), (75, 101, 4, 1), (40, 52, 1, 2)])
+def test_gpu_filter_matches_oracle(H, W, nsrc, seed):
+    import torch
+    depths, cams, conf = fo.synthetic_views(H, W, nsrc, seed=seed)
+    photo, geo, final, avg = fo.filter_depth_core(depths[0], conf, cams[0], depths[1:], cams[1:], 0.35)
+    dev = torch.device("cuda")
+    t = [torch.from_numpy(d).to(dev) for d in depths]
+    g = fusion.filter_depth_core(t[0], torch.from_numpy(conf).to(dev), cams[0], t[1:], cams[1:], 0.35)
+    gp, gg, gf, ga = (x.cpu().numpy() for x in g)
+    np.testing.assert_array_equal(gp, photo)
+    # masks are threshold tests on float64/float32 chains whose last bits differ by summation
+    # order (numpy's BLAS vs an fma chain): allow a handful of boundary pixels
+    assert (gg != geo).mean() <= 2e-3
+    assert (gf != final).mean() <= 2e-3
+    same = gg == geo
+    np.testing.assert_allclose(ga[same], avg[same], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_filter_rejects_bad_input():
+    import torch
+    from aarmvs._lib import AarmvsError
+    depths, cams, conf = fo.synthetic_views(16, 16, 2)
+    with pytest.raises(AarmvsError):
+        fusion.filter_depth_core(torch.from_numpy(depths[0]), torch.from_numpy(conf), cams[0],
+                                 [torch.from_numpy(d) for d in depths[1:]], cams[1:], 0.35)
