@@ -833,8 +833,19 @@ __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
   load_omega(a, P, o);
   const float4* t1 = a.t1_next + ((size_t)b * a.nsrc + v) * HW;
   float part[2] = {0.f, 0.f};
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
-    const float4 q = t1[p];
+  // four independent 16-B loads in flight per thread per iteration
+  const int gstride = gridDim.x * blockDim.x;
+  for (int p0 = blockIdx.x * blockDim.x + threadIdx.x; p0 < HW; p0 += 4 * gstride) {
+    float4 qs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + u * gstride;
+      qs[u] = p < HW ? t1[p] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+    if (p0 + u * gstride >= HW) break;
+    const float4 q = qs[u];
     const float t[4] = {q.x, q.y, q.z, q.w};
     float aa[4], t2[4];
     gn_relu4(t, gs[0], o.g0w, o.g0b, true, aa);
@@ -850,6 +861,7 @@ __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
     }
     part[0] += (r[0] + r[1]) + (r[2] + r[3]);
     part[1] += (r[0] * r[0] + r[1] * r[1]) + (r[2] * r[2] + r[3] * r[3]);
+    }
   }
   block_sum<2>(part, red);
   if (threadIdx.x == 0) stat_add(a.st_next + st_index(b, v, STAGE, a.nsrc), part[0], part[1]);
@@ -940,7 +952,7 @@ hipError_t launch_omega_next(const CostArgs& ca, const SweepGeom& g, const Works
   // GN #1 / #2 statistics of plane d
   const int HW = g.H * g.W;
   const int pblk =
-      std::max(1, std::min((HW + 255) / 256, 2 * g.cu_count / std::max(1, g.B * g.nsrc) + 1));
+      std::max(1, std::min((HW + 1023) / 1024, 8 * g.cu_count / std::max(1, g.B * g.nsrc) + 1));
   {
     ProfScope ps(s, K_OMEGA1);
     hipLaunchKernelGGL(omega_stats_kernel<1>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a, a.params);
