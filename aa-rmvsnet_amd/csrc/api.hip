@@ -427,7 +427,15 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   // statistics cleared" (main -> aux, before omega of plane p + 2, which reuses the
   // buffers of parity p).
   hipStream_t aux = (a->aux_stream && a->aux_stream != stream) ? a->aux_stream : nullptr;
-  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // main[2], aux[2], fork/join
+  // Overlap mode: by default omega(d+1) starts as soon as cost_x(d-1) released its buffers
+  // (beside plane d-1's regulariser step and plane d's cost slice).  AARMVS_OVERLAP=costx
+  // runs it beside cost_x(d) only (the regulariser step waits for it, so the whole-CU
+  // ConvLSTM blocks never queue behind omega blocks): measured 888 vs 904 M hyp/s (single
+  // stream 885), so not the default.
+  const char* ov_env = std::getenv("AARMVS_OVERLAP");
+  const bool ov_all = !(ov_env && std::strcmp(ov_env, "costx") == 0);
+  hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // main[2], aux[2], fork/join, start[2]
   auto destroy_events = [&] {
     for (hipEvent_t& x : ev)
       if (x) (void)hipEventDestroy(x), x = nullptr;
@@ -442,6 +450,7 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         return sweep_fail(e, "sweep: event create");
   hipEvent_t* ev_main = ev;
   hipEvent_t* ev_aux = ev + 2;
+  hipEvent_t* ev_start = ev + 5;
   hipStream_t os = aux ? aux : stream;   // the omega pipeline's stream
 
   if (a->d_begin == 0) {
@@ -477,9 +486,13 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   for (int d = a->d_begin; d < a->d_end; ++d) {
     const bool last = d == a->d_end - 1;
     // omega pipeline of plane d + 1; its buffers were last read by cost_x(d - 1)
+    if (aux && !ov_all && (e = hipEventRecord(ev_start[d & 1], stream)) != hipSuccess)
+      return sweep_fail(e, "sweep: event record");
     if (d + 1 < a->D) {
-      if (aux && d - 1 >= a->d_begin &&
+      if (aux && ov_all && d - 1 >= a->d_begin &&
           (e = hipStreamWaitEvent(aux, ev_main[(d - 1) & 1], 0)) != hipSuccess)
+        return sweep_fail(e, "sweep: event wait");
+      if (aux && !ov_all && (e = hipStreamWaitEvent(aux, ev_start[d & 1], 0)) != hipSuccess)
         return sweep_fail(e, "sweep: event wait");
       if ((e = launch_omega_next(ca, g, ws, d + 1, os)) != hipSuccess)
         return sweep_fail(e, "sweep: omega pipeline");
@@ -498,6 +511,9 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
       return sweep_fail(e, "sweep: stats clear");
     if (aux && (e = hipEventRecord(ev_main[d & 1], stream)) != hipSuccess)
       return sweep_fail(e, "sweep: event record");
+    if (aux && !ov_all && d + 1 < a->D &&
+        (e = hipStreamWaitEvent(stream, ev_aux[(d + 1) & 1], 0)) != hipSuccess)
+      return sweep_fail(e, "sweep: event wait");
     if (last && a->slice_out) {
       e = launch_layout(ws.x, a->slice_out, a->B, kC, a->H * a->W, false, stream);
       if (e != hipSuccess) return sweep_fail(e, "sweep: slice copy");
