@@ -252,12 +252,12 @@ __device__ __forceinline__ size_t st_index(int b, int v, int k, int nsrc) {
   return (((size_t)b * nsrc + v) * 3 + k) * kSlots * 2;
 }
 
-// Tiles are 32 pixels wide, 8 rows (one thread per pixel).
-constexpr int kTileW = 32, kTileH = 8, kTileThreads = kTileW * kTileH;
+// omega_conv tiles are 32 pixels wide, 16 rows (one thread per pixel).
+constexpr int kTileW = 32, kTileH = 16, kTileThreads = kTileW * kTileH;
 constexpr int kTileWaves = kTileThreads / 64;
 constexpr int kCHH = kTileH + 2, kCHW = kTileW + 2;   // omega_conv haloed tile
 constexpr int kCRing = 2 * kCHW + 2 * kTileH;         // its halo-only (ring) pixels
-constexpr int kCBoxPx = 448;    // omega_conv LDS source box: 32-B pixels (one chunk)
+constexpr int kCBoxPx = 1024;   // omega_conv LDS source box: 32-B pixels (one chunk)
 static_assert(kCRing <= kTileThreads, "one ring pixel per thread at most");
 
 // XCD-aware tile order: blocks are dealt to the 8 XCDs round-robin, so XCD k takes the
