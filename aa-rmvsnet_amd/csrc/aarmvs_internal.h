@@ -52,7 +52,7 @@ struct ParamLayout {
   size_t h3_off[5];         // split-fp16 cell weights (hi then lo halves), in floats
   size_t h3_scale_off;      // 5 floats: 1 / (power-of-two weight scale) per cell
   size_t ow0t_off;          // omega conv3x3 weights as [tap][ci][co] (1,152 floats)
-  size_t owb_off;           // omega conv3x3 as split-fp16 MFMA B fragments [chunk][5][64 lanes][8]
+  size_t owb_off;           // omega conv3x3 off-centre taps as split-fp16 MFMA B fragments [chunk][2][64 lanes][8]
   size_t owb_scale_off;     // 1 float: 1 / (power-of-two scale of those fragments)
   size_t dct_off[2];        // deconv_0/1 weights as [ci][tap][co] (2,304 floats each)
   size_t raw_total;

@@ -43,7 +43,7 @@ const ParamLayout& param_layout() {
     l.ow0t_off = pk;
     pk += 4 * 32 * 9;
     l.owb_off = pk;
-    pk += 4 * 5 * 64 * 8 / 2;   // halves -> floats
+    pk += 4 * 2 * 64 * 8 / 2;   // halves -> floats
     l.owb_scale_off = pk;
     pk += 64;
     for (int k = 0; k < 2; ++k) {
@@ -237,11 +237,11 @@ __global__ void __launch_bounds__(256) pack_cell_h3_kernel(const float* __restri
 
 // omega conv3x3 32->4 weights [co][ci][tap] -> [tap][ci][co]: the 16 weights of one
 // (tap, 4-channel group) are contiguous (scalar loads in the VALU form of the conv)
-// and -> split-fp16 B fragments of v_mfma_f32_16x16x32_f16 for omega_conv's MFMA conv:
-// per 8-channel chunk c, K = [a_hi taps 0..8 | a_lo taps 0..8] x 8 channels (k8 group
-// q = 9 s + tap, 18 groups, padded to 20 = 5 MFMAs of K 32), N = 16 columns
-// n = co + 4 ws (ws: weight hi / lo part; columns 8..15 zero).  Lane l of MFMA j holds
-// B[k8 group 4 j + l / 16][n = l % 16] (8 halves).  A power-of-two scale keeps the
+// and -> split-fp16 B fragments of v_mfma_f32_16x16x32_f16 for omega_conv's MFMA conv
+// (the eight off-centre taps): per 8-channel chunk c and N tile k, column n = 4 u + co
+// (tap slot u = 4 k + n / 4: taps 0..3, 5..8), k8 group g = lane / 16 against the A
+// groups [sq hi | sq lo | sq hi | sq lo]: W hi for g < 2, W lo for g >= 2.  Lane l of
+// fragment (c, k) holds B[8 g .. 8 g + 7][n = l % 16].  A power-of-two scale keeps the
 // weights in fp16's normal range (undone in the kernel's epilogue).
 __global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __restrict__ pk,
                                        ParamLayout L) {
@@ -266,17 +266,12 @@ __global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __r
   const float sc = ldexpf(1.0f, e);
   if (threadIdx.x == 0) pk[L.owb_scale_off] = ldexpf(1.0f, -e);
   _Float16* b = reinterpret_cast<_Float16*>(pk + L.owb_off);
-  for (int i = threadIdx.x; i < 4 * 5 * 64 * 8; i += blockDim.x) {
-    const int ci8 = i & 7, lane = (i >> 3) & 63, j = (i >> 9) % 5, c = (i >> 9) / 5;
-    const int q = 4 * j + (lane >> 4), n = lane & 15;
-    float v = 0.f;
-    if (q < 18 && n < 8) {
-      const int tap = q % 9, co = n & 3;
-      const float x = w[(co * 32 + 8 * c + ci8) * 9 + tap] * sc;
-      const _Float16 xh = (_Float16)x;
-      v = (n < 4) ? (float)xh : (float)(_Float16)(x - (float)xh);
-    }
-    b[i] = (_Float16)v;
+  for (int i = threadIdx.x; i < 4 * 2 * 64 * 8; i += blockDim.x) {
+    const int ci8 = i & 7, lane = (i >> 3) & 63, k = (i >> 9) & 1, c = i >> 10;
+    const int n = lane & 15, g = lane >> 4, u = 4 * k + n / 4, tap = u < 4 ? u : u + 1, co = n & 3;
+    const float x = w[(co * 32 + 8 * c + ci8) * 9 + tap] * sc;
+    const _Float16 xh = (_Float16)x;
+    b[i] = g < 2 ? xh : (_Float16)(x - (float)xh);
   }
 }
 

@@ -550,15 +550,22 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-// split-fp16 sq image (MFMA A operand): channels 4h..4h+3 of pixel p as fp16 hi parts in
-// the hi plane and fp16(v - hi) in the lo plane, [plane][pixel][8 channels]
+// split-fp16 sq image (MFMA A operand), 32 B per pixel: slot 0 the fp16 hi parts of the
+// 8 channels, slot 1 fp16(v - hi), the slots swapped when bit 3 of p is set (img_slot's
+// swizzle); channels 4h..4h+3 are halves 4h..4h+3 of each slot.  v is stored x 2^-4
+// (exact) so that |difference| up to 1024 stays in fp16 range.
+constexpr float kSqScale = 0.0625f;
 __device__ __forceinline__ void sq_st16(_Float16* img, uint32_t p, int h, float4 v) {
-  constexpr uint32_t NHP = kCHH * kCHW;
+  v.x *= kSqScale;
+  v.y *= kSqScale;
+  v.z *= kSqScale;
+  v.w *= kSqScale;
   const half4 hi = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
   const half4 lo = {(_Float16)(v.x - (float)hi.x), (_Float16)(v.y - (float)hi.y),
                     (_Float16)(v.z - (float)hi.z), (_Float16)(v.w - (float)hi.w)};
-  *reinterpret_cast<half4*>(img + p * 8u + 4u * (uint32_t)h) = hi;
-  *reinterpret_cast<half4*>(img + NHP * 8u + p * 8u + 4u * (uint32_t)h) = lo;
+  const uint32_t sw = (p >> 3) & 1u;
+  *reinterpret_cast<half4*>(img + p * 16u + 8u * sw + 4u * (uint32_t)h) = hi;
+  *reinterpret_cast<half4*>(img + p * 16u + 8u * (sw ^ 1u) + 4u * (uint32_t)h) = lo;
 }
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -580,23 +587,30 @@ __device__ __forceinline__ void dma_wait() {
 // A box past kCBoxPx pixels is sampled from global memory instead.
 // ABL: ablation bits for the diagnostic harness only (tools/microbench/pipe_bench.cpp;
 // the library instantiates ABL = 0): 1 no conv, 2 no squared differences, 4 no box
-// loads, 8 conv tap loop rolled, 16 the conv on the matrix cores: an implicit GEMM per
-// chunk, M = 16 pixels of a tile row, K = 9 taps x 8 channels x {sq hi, sq lo} (split
-// fp16 sq image), N = 4 output channels x {w hi, w lo}, v_mfma_f32_16x16x32_f16 (all four
-// split products, fp32 accumulation).  Measured slower (0.90 vs 0.74 ms per plane): the
-// A fragments re-read every pixel once per tap from LDS, 1 KiB per MFMA, which saturates
-// the LDS at 16 cycles per MFMA on four SIMDs; the parity tests pass on it.
+// loads, 8 conv tap loop rolled, 16 the eight off-centre taps on the matrix cores: per
+// chunk a GEMM y[q][tap, co] += sq[q][8 ch] x W[8 ch][tap, co] over the 612 haloed
+// pixels q (M tiles of 16, N = 8 taps x 4 co = 2 tiles of 16, v_mfma_f32_16x16x32_f16
+// with K = [sq hi | sq lo | sq hi | sq lo] x [W hi | W hi | W lo | W lo]: the four split
+// products), accumulated over the chunks in registers; then out[p] = sum over taps of
+// y[p + tap offset][tap] through LDS (two 16-column rounds); the centre tap stays a VALU
+// fmaf chain on the thread's own sq.  Parity-green but slower: 1.18 vs 0.73 ms per plane
+// (the accumulators need 3 waves per SIMD: 8 waves per CU at 16-row tiles), and 1.59 vs
+// 1.29 ms at 12-row tiles where both fit 12 waves per CU: the kernel is bound by block
+// latency (the chunk pipeline's DMA waits and barriers), not by the conv's VALU issue.
 template <int ABL = 0>
-__global__ void __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ void __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu((ABL & 16) ? 3 : 4)))
 omega_conv_kernel(PipeArgs a,
                                                                   const float* __restrict__ P,
                                                                   const float* __restrict__ Rel) {
   constexpr int NHP = kCHH * kCHW;                                      // haloed tile pixels
   constexpr int NB = (2 * kCBoxPx + kTileThreads - 1) / kTileThreads;   // box pieces per thread
   constexpr int NR = (2 * NHP + kTileThreads - 1) / kTileThreads;       // ref pieces per thread
-  __shared__ __attribute__((aligned(16))) float box[(kCBoxPx + 1) * 8];
-  __shared__ __attribute__((aligned(16))) float rt[NHP * 8];
-  __shared__ __attribute__((aligned(16))) float sqt[NHP * 8];
+  // one LDS array: source box | reference tile | sq tile (the MFMA epilogue's y image
+  // reuses the box and reference space)
+  __shared__ __attribute__((aligned(16))) float smem[(kCBoxPx + 1) * 8 + 2 * NHP * 8];
+  float* const box = smem;
+  float* const rt = smem + (kCBoxPx + 1) * 8;
+  float* const sqt = rt + NHP * 8;
   __shared__ int red[kTileWaves][4];
   __shared__ float wsum[kTileWaves][2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -692,24 +706,20 @@ omega_conv_kernel(PipeArgs a,
   };
   const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]
   const float* __restrict__ b0 = P + a.off_ob0;
-  // MFMA conv: this lane's A rows (pixel i = lane & 15 of the wave's four 16-pixel row
-  // tiles) and k8 groups (q = 4 j + lane / 16 of MFMA j: plane q / 9, tap q % 9; the two
-  // padding groups re-read group 17 against zero weights)
+  // MFMA conv: M tiles t = wave + 8 i of the haloed tile (rows 16 t .. 16 t + 15 in
+  // haloed-pixel order; the last tile's rows past NHP re-read pixel NHP - 1 and are
+  // dropped), this lane's A row and slot (k8 group lane / 16: hi, lo, hi, lo)
   constexpr bool MF = (ABL & 16) != 0;
-  _Float16* sqh = reinterpret_cast<_Float16*>(sqt);   // [hi plane | lo plane][NHP][8]
+  constexpr int MT = (NHP + 15) / 16, MTW = (MT + kTileWaves - 1) / kTileWaves;
+  _Float16* sqh = reinterpret_cast<_Float16*>(sqt);
   const half8* __restrict__ owb = reinterpret_cast<const half8*>(P + a.off_owb);
-  uint32_t mrow[4], koff[5];
+  auto arow = [&](int i) {
+    const uint32_t q = (uint32_t)min(16 * (wave + kTileWaves * i) + (lane & 15), NHP - 1);
+    return q * 32u + 16u * (((uint32_t)(lane >> 4) & 1u) ^ ((q >> 3) & 1u));
+  };
+  floatx4 acc[MTW][2];
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
-    mrow[t] = (uint32_t)(((2 * wave + (t >> 1) + 1) * kCHW + 16 * (t & 1) + (lane & 15) + 1) * 16);
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const int q = min(4 * j + (lane >> 4), 17), tap = q % 9;
-    koff[j] = (uint32_t)((q / 9) * NHP * 16 + ((tap / 3 - 1) * kCHW + (tap % 3 - 1)) * 16);
-  }
-  floatx4 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MTW; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   stage(0);
   dma_wait();
@@ -720,13 +730,26 @@ omega_conv_kernel(PipeArgs a,
 #pragma unroll
     for (int h = 0; h < 2 && !(ABL & 2); ++h) {
       const float4 so = sqdiff4(sample(to, c, h), img_ld(rt, own_hp, h));
-      if (MF) sq_st16(sqh, own_hp, h, so);
-      else img_st(sqt, own_hp, h, so);
+      if constexpr (MF) {
+        sq_st16(sqh, own_hp, h, so);
+        // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel
+        const float qq[4] = {so.x, so.y, so.z, so.w};
+        const float* wt = w0t + (4 * kC + 8 * c + 4 * h) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int co = 0; co < 4; ++co) o4[co] = fmaf(qq[j], wt[j * 4 + co], o4[co]);
+      } else {
+        img_st(sqt, own_hp, h, so);
+      }
       if (has_ring) {
         const float4 sr = sqdiff4(sample(tr, c, h), img_ld(rt, ring_hp, h));
         if (MF) sq_st16(sqh, ring_hp, h, sr);
         else img_st(sqt, ring_hp, h, sr);
       }
+      // MFMA conv: keep the halves' gathers from being hoisted together (their registers
+      // would be live alongside the accumulators)
+      if constexpr (MF) __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();   // sq visible; this chunk's box / reference reads are done
     if (c < 3) stage(c + 1);
@@ -745,14 +768,13 @@ omega_conv_kernel(PipeArgs a,
     // (0.72 vs 0.82 ms per plane at the headline geometry with a rolled loop)
     if constexpr (ABL & 1) {
     } else if constexpr (MF) {
+      const half8 bf0 = owb[(c * 2 + 0) * 64 + lane], bf1 = owb[(c * 2 + 1) * 64 + lane];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        const half8 bf = owb[(c * 5 + j) * 64 + lane];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const half8 af = *reinterpret_cast<const half8*>(
-              reinterpret_cast<const char*>(sqh) + mrow[t] + koff[j]);
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc[t], 0, 0, 0);
+      for (int i = 0; i < MTW; ++i) {
+        if (wave + kTileWaves * i < MT) {
+          const half8 af = *reinterpret_cast<const half8*>(reinterpret_cast<const char*>(sqh) + arow(i));
+          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf0, acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf1, acc[i][1], 0, 0, 0);
         }
       }
     } else if constexpr ((ABL & 8) != 0) {
@@ -768,27 +790,41 @@ omega_conv_kernel(PipeArgs a,
     }
   }
   if constexpr (MF) {
-    // D[row = 4 (lane / 16) + r][col = lane % 16] of row tile t -> LDS [pixel][8] (cols
-    // 0..3: x w_hi, 4..7: x w_lo), then every thread sums its own pixel's parts.  The box
-    // image is free: its last reads were chunk 3's sq phase.
-    float* dt = box;
-    if ((lane & 15) < 8) {
+    // y image [haloed pixel][20 floats] over the box and reference space (last read in
+    // chunk 3's sq phase): D[row = 4 (lane / 16) + r][col = lane % 16] of tile t, column
+    // n = 4 (tap slot) + co; N tile k holds tap slots 4k .. 4k + 3 (taps 0..3, 5..8)
+    constexpr int YS = 20;
+    static_assert(NHP * YS <= (kCBoxPx + 1) * 8 + NHP * 8, "y image fits the box + reference space");
+    float* const y = smem;
+    float g4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+    for (int k = 0; k < 2; ++k) {
+      if (k) __syncthreads();   // round 0's gathers are done
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int px = (2 * wave + (t >> 1)) * kTileW + 16 * (t & 1) + 4 * (lane >> 4) + r;
-          dt[px * 8 + (lane & 15)] = acc[t][r];
+      for (int i = 0; i < MTW; ++i) {
+        if (wave + kTileWaves * i < MT) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = 16 * (wave + kTileWaves * i) + 4 * (lane >> 4) + r;
+            if (q < NHP) y[q * YS + (lane & 15)] = acc[i][k][r];
+          }
         }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int tap = 4 * k + u < 4 ? 4 * k + u : 4 * k + u + 1;
+        const uint32_t q = own_hp + (uint32_t)((tap / 3 - 1) * kCHW + (tap % 3 - 1));
+        const float4 yv = *reinterpret_cast<const float4*>(y + q * YS + 4 * u);
+        g4[0] += yv.x;
+        g4[1] += yv.y;
+        g4[2] += yv.z;
+        g4[3] += yv.w;
+      }
     }
-    __syncthreads();
-    const float4 d0 = *reinterpret_cast<const float4*>(&dt[tid * 8]);
-    const float4 d1 = *reinterpret_cast<const float4*>(&dt[tid * 8 + 4]);
-    const float isc = P[a.off_owb_scale];
-    o4[0] = (d0.x + d1.x) * isc;
-    o4[1] = (d0.y + d1.y) * isc;
-    o4[2] = (d0.z + d1.z) * isc;
-    o4[3] = (d0.w + d1.w) * isc;
+    const float isc = P[a.off_owb_scale] * (1.0f / kSqScale);
+#pragma unroll
+    for (int co = 0; co < 4; ++co) o4[co] = fmaf(g4[co], isc, o4[co]);
   }
   float ps = 0.f, pss = 0.f;
   if (inside) {
@@ -817,6 +853,9 @@ omega_conv_kernel(PipeArgs a,
     stat_add(a.st_next + st_index(b, v, 0, nsrc), s0, s1);
   }
 }
+
+// the library's omega_conv variant (0: VALU conv)
+constexpr int kOmegaConvAbl = 0;
 
 // GN #STAGE (1 or 2) partial sums of the omega chain on t1 (plane d_next).
 template <int STAGE>
@@ -945,7 +984,7 @@ hipError_t launch_omega_next(const CostArgs& ca, const SweepGeom& g, const Works
   {
     const int ntiles = ((g.W + kTileW - 1) / kTileW) * ((g.H + kTileH - 1) / kTileH);
     ProfScope ps(s, K_OMEGA_CONV);
-    hipLaunchKernelGGL(omega_conv_kernel<0>, dim3(ntiles * g.nsrc, 1, g.B), dim3(kTileThreads), 0, s, a,
+    hipLaunchKernelGGL(omega_conv_kernel<kOmegaConvAbl>, dim3(ntiles * g.nsrc, 1, g.B), dim3(kTileThreads), 0, s, a,
                        a.params, a.rel);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

@@ -200,3 +200,34 @@ def test_two_stream_schedule_is_bit_identical():
         assert torch.equal(a[k], b[k]), k
     assert torch.equal(a["cost"], cost)
     assert torch.equal(a["depth"], c["depth"]) and torch.equal(a["conf"], c["conf"])
+
+
+def test_sweep_with_points_behind_a_source_camera_matches_oracle():
+    """A source projection whose z row is mixed with its x row (z' = z - x / (W/2) in
+    pixel units): z' changes sign across the image, so omega_conv sees tiles with every
+    corner in front (the corner-box path), tiles straddling z' = 0 and tiles wholly
+    behind (both on the per-pixel box path), and positions far outside the image."""
+    from oracle import sweep_oracle as orc
+    from aarmvs import ops
+    B, N, H, W, D = 1, 3, 64, 160, 4
+    sc = syn.scene(B, N, H, W, D, seed=23)
+    proj = torch.from_numpy(sc["proj_matrices"]).clone()
+    M = torch.eye(4)
+    M[2, 0] = -1.0 / (W / 2)
+    proj[:, 2] = M @ proj[:, 2]
+    rel = ops.relative_projection(proj[:, 2], proj[:, 0])[0].numpy()
+    ys, xs = np.mgrid[0:H, 0:W].astype(np.float32)
+    zs = [(rel[2, 0] * xs + rel[2, 1] * ys + rel[2, 2]) * d + rel[2, 3]
+          for d in sc["depth_values"][0]]
+    neg = float(np.mean(np.stack(zs) <= 0))
+    assert 0.1 < neg < 0.9, neg
+    P = {k: torch.from_numpy(v) for k, v in syn.sweep_weights(6).items()}
+    feats = torch.from_numpy(sc["features"])
+    ref = orc.sweep(feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+                    [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]), P)
+    sw = ops.DepthSweep({k: v.to(DEV) for k, v in P.items()}, DEV)
+    fd = feats.to(DEV)
+    out = sw(fd[0], [fd[v] for v in range(1, N)], proj[:, 0], [proj[:, v] for v in range(1, N)],
+             torch.from_numpy(sc["depth_values"]), want_cost=True)
+    np.testing.assert_allclose(out["cost"].cpu().numpy(), ref["cost"].numpy(), atol=1e-4, rtol=1e-4)
+    assert rel_l1(out["depth"].cpu().numpy(), ref["depth"].numpy()) <= 1e-3

@@ -93,7 +93,7 @@ int main(int argc, char** argv) {
   run("omega_conv no box loads (4)", omega_conv_kernel<4>, gc, kTileThreads, bc);
   run("omega_conv no sq/box (6)", omega_conv_kernel<6>, gc, kTileThreads, bc);
   run("omega_conv skeleton (7)", omega_conv_kernel<7>, gc, kTileThreads, bc);
-  run("omega_conv MFMA conv (16)", omega_conv_kernel<16>, gc, kTileThreads, bc);
+  run("omega_conv MFMA off-centre taps (16)", omega_conv_kernel<16>, gc, kTileThreads, bc);
   run("omega_conv conv rolled (8)", omega_conv_kernel<8>, gc, kTileThreads, bc);
   a0.box_cap = 64;
   run("omega_conv (box cap 64: global gathers)", omega_conv_kernel<0>, gc, kTileThreads, bc);
