@@ -378,6 +378,11 @@ static int check_geom(int B, int H, int W, int nsrc) {
                 "H and W must be positive multiples of 4 (two 2x2 pools + two stride-2 deconvs)");
   if (nsrc < 1 || nsrc > AARMVS_MAX_SRC)
     return fail(AARMVS_ERR_INVALID, "nsrc must be in [1, AARMVS_MAX_SRC]");
+  // the pipeline kernels address one view's 32-channel image with 32-bit byte offsets and
+  // the per-view maps with 32-bit element indices
+  const long long hw = (long long)H * W;
+  if (hw * 128 >= (1ll << 32) || (long long)B * (nsrc + 1) * hw >= (1ll << 31))
+    return fail(AARMVS_ERR_INVALID, "H x W (x B x views) too large for 32-bit image offsets");
   return AARMVS_OK;
 }
 

@@ -368,7 +368,9 @@ __device__ __forceinline__ TapP tap_p(const TapF& t, bool valid, int H, int W, b
     const float xf = t.xf + (float)(k & 1), yf = t.yf + (float)(k >> 1);
     const bool ok = valid && (xf > -1.0f) && (xf < (float)W) && (yf > -1.0f) && (yf < (float)H);
     const int xi = ok ? (int)xf : bx.x0, yi = ok ? (int)yf : bx.y0;
-    const uint32_t p = lds ? (uint32_t)((yi - bx.y0) * bx.nx + (xi - bx.x0)) : (uint32_t)(yi * W + xi);
+    // 24-bit multiplies (full rate): coordinates and extents are < 2^24
+    const uint32_t p = lds ? __umul24((uint32_t)(yi - bx.y0), (uint32_t)bx.nx) + (uint32_t)(xi - bx.x0)
+                           : __umul24((uint32_t)yi, (uint32_t)W) + (uint32_t)xi;
     o.pix[k] = ok ? p : zpix;
   }
   return o;
@@ -468,8 +470,13 @@ __global__ void __launch_bounds__(2 * kXRows * kTileW) cost_x_kernel(PipeArgs a,
   for (int vp = 0; vp < AARMVS_MAX_SRC; vp += 2) {
     if ((XV & 2) && vp < nsrc) {
       const int vm = min(vp + h, nsrc - 1);
-      const float w = omega_weight(a.t1_prev[((size_t)b * nsrc + vm) * HW + p], gs[vm], o);
-      if (a.omega_out && vp + h < nsrc) a.omega_out[((size_t)(vp + h) * a.B + b) * HW + p] = w;
+      // 32-bit element offsets (B * nsrc * HW < 2^31, checked on the host): a wave-uniform
+      // base (scalar) plus this lane's view step
+      const uint32_t p32 = (uint32_t)p, hw = (uint32_t)HW;
+      const float w = omega_weight(
+          a.t1_prev[(uint32_t)(b * nsrc + vp) * hw + (uint32_t)(vm - vp) * hw + p32], gs[vm], o);
+      if (a.omega_out && vp + h < nsrc)
+        a.omega_out[(uint32_t)(vp * a.B + b) * hw + (uint32_t)(h * a.B) * hw + p32] = w;
       const float ws = swap_pair(w);
       wv[vp] = h ? ws : w;
       if (vp + 1 < AARMVS_MAX_SRC) wv[vp + 1] = h ? w : ws;
@@ -674,7 +681,8 @@ omega_conv_kernel(PipeArgs a,
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int i = tid + j * kTileThreads, p = i >> 1, r = box_row(p, bx.nx, mg);
-    const uint32_t gp = (uint32_t)((bx.y0 + r) * W + bx.x0 + (p - r * bx.nx));
+    const uint32_t gp = __umul24((uint32_t)(bx.y0 + r), (uint32_t)W) + (uint32_t)bx.x0 +
+                        ((uint32_t)p - __umul24((uint32_t)r, (uint32_t)bx.nx));
     boff[j] = gp * 32u + 16u * (uint32_t)img_half((uint32_t)p, i & 1);
   }
 #pragma unroll
@@ -682,7 +690,7 @@ omega_conv_kernel(PipeArgs a,
     const int i = tid + j * kTileThreads, hp = i >> 1, py = hp / kCHW;
     const int y = y0 - 1 + py, x = x0 - 1 + (hp - py * kCHW);
     roff[j] = (y >= 0 && y < H && x >= 0 && x < W)
-                  ? (uint32_t)(y * W + x) * 32u + 16u * (uint32_t)img_half((uint32_t)hp, i & 1)
+                  ? (__umul24((uint32_t)y, (uint32_t)W) + (uint32_t)x) * 32u + 16u * (uint32_t)img_half((uint32_t)hp, i & 1)
                   : fbytes;   // zero padding
   }
   auto stage = [&](int c) {
