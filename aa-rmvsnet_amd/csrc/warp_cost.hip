@@ -429,10 +429,13 @@ __device__ __forceinline__ void sample_pos_pair(const float* __restrict__ m, flo
 // XV: bit 2 (the library's) the omega weights split over the lane pair (view v by lane
 // v & 1, swapped by DPP) and computed before the view loop: 0.46 vs 0.50 ms per plane;
 // bit 1 (microbenchmark variant) the sampling position split over the pair as well
-// (sample_pos_pair): no further gain.
+// (sample_pos_pair): no further gain; bits 4 / 8 (microbenchmark) 5 / 6 waves per SIMD
+// instead of 4: 0.485 / 0.578 ms (6 spills) vs 0.482 ms, so occupancy is not the limit
+// (the measured HBM traffic, 2.1 GB per plane, is close to the algorithmic 1.94 GB).
 constexpr int kXRows = 8;
 template <int XV = 0>
-__global__ void __launch_bounds__(2 * kXRows * kTileW) cost_x_kernel(PipeArgs a,
+__global__ void __launch_bounds__(2 * kXRows * kTileW)
+__attribute__((amdgpu_waves_per_eu((XV & 8) ? 6 : (XV & 4) ? 5 : 4))) cost_x_kernel(PipeArgs a,
                                                               const float* __restrict__ P,
                                                               const float* __restrict__ Rel) {
   __shared__ GnStat gs[AARMVS_MAX_SRC][3];

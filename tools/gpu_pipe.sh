@@ -1,4 +1,4 @@
 #!/bin/bash
+# pipeline microbenchmark only (omega_conv / cost_x variants)
 source tools/gpu_round.sh
-run pytest_gpu 900 python -m pytest tests -m gpu -q -x
-run pipe_bench 200 ./tools/microbench/pipe_bench
+run pipe_bench 120 ./tools/microbench/pipe_bench

@@ -85,6 +85,8 @@ int main(int argc, char** argv) {
   run("cost_x pair sample_pos (1)", cost_x_kernel<1>, gx, 2 * kXRows * kTileW, bx);
   run("cost_x pair omega (2)", cost_x_kernel<2>, gx, 2 * kXRows * kTileW, bx);
   run("cost_x pair both (3)", cost_x_kernel<3>, gx, 2 * kXRows * kTileW, bx);
+  run("cost_x pair omega, 5 waves/SIMD (6)", cost_x_kernel<6>, gx, 2 * kXRows * kTileW, bx);
+  run("cost_x pair omega, 6 waves/SIMD (10)", cost_x_kernel<10>, gx, 2 * kXRows * kTileW, bx);
   const dim3 gc(tiles_x * ((H + kTileH - 1) / kTileH) * nsrc, 1, B);
   const double bc = (128.0 * (nsrc + 1) + 16.0 * nsrc) * HW;
   run("omega_conv", omega_conv_kernel<0>, gc, kTileThreads, bc);
