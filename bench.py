@@ -19,7 +19,10 @@ Also reported on the same JSON line:
                 of the reference, pinned to fixtures made by running the reference) timed
                 on this host's cores on a bounded sample (the first planes of the same
                 workload), rank 0 at N=1 only;
-  parity        HIP vs the oracle on that sample (cost max|err|, depth rel-L1).
+  parity        HIP vs the oracle on that sample (cost max|err|, depth rel-L1);
+  fusion        the depth-map fusion core (§8f-2) at the same resolution;
+  e2e           the end-to-end models.EMVSNet eval forward on images (FeatNet in PyTorch
+                + the sweep) at the same config, reported beside the headline (§8d).
 """
 from __future__ import annotations
 
@@ -195,6 +198,41 @@ def fusion_bench(H: int, W: int, nsrc: int, dev, cpu_leg: bool, reps: int = 10):
     return res
 
 
+def e2e_bench(N: int, H: int, W: int, D: int, B: int, dev, reps: int = 2):
+    """End-to-end figure (reported beside the headline): the drop-in
+    `models.EMVSNet` eval forward (drmvsnet.py:255-345) on images, FeatNet (PyTorch on the
+    GPU) for all N views plus the HIP sweep, random-init weights; FeatNet alone is timed
+    too.  Wall time with the device synchronised, `reps` forwards after one warm-up."""
+    from models.drmvsnet import EMVSNet
+    torch.manual_seed(0)
+    model = EMVSNet(D, image_scale=1.0, max_h=H, max_w=W, return_depth=True).to(dev).eval()
+    g = torch.Generator(device="cpu").manual_seed(0)
+    imgs = torch.randn(B, N, 3, H, W, generator=g).to(dev)
+    sc = syn.scene(B, N, H, W, D, seed=0)
+    proj = torch.from_numpy(sc["proj_matrices"]).to(dev)
+    dv = torch.from_numpy(sc["depth_values"]).to(dev)
+    with torch.no_grad():
+        out = model(imgs, proj, dv)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = model(imgs, proj, dv)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        views = torch.unbind(imgs, 1)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            feats = [model.feature(v) for v in views]
+        torch.cuda.synchronize()
+        ft = (time.perf_counter() - t0) / reps
+    ok = bool(torch.isfinite(out["depth"]).all())
+    del feats, out, model
+    return dict(metric="end-to-end depth-hypotheses/s (EMVSNet.forward: FeatNet + sweep)",
+                value=round(B * H * W * D / dt, 1), s_per_step=round(dt, 4),
+                featnet_s=round(ft, 4), featnet="PyTorch (MIOpen) fp32, out of the §8 scope",
+                images=f"[{B},{N},3,{H},{W}] ~N(0,1)", depth_finite=ok)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -211,6 +249,8 @@ def main():
                     help="run the sweep's main stream at high priority (aux stream normal)")
     ap.add_argument("--no-fusion", action="store_true",
                     help="skip the depth-map fusion measurement (the next §8 row)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end EMVSNet.forward figure (FeatNet + sweep)")
     ap.add_argument("--planes", type=int, default=0,
                     help="profiling aid: sweep only the first P depth planes (0 = all D); "
                          "per-launch figures are unchanged, the headline value is not comparable")
@@ -315,6 +355,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_fusion:
         fusion_res = fusion_bench(H, W, 10, dev, cpu_leg=not args.no_cpu)
 
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = e2e_bench(N, H, W, D, B, dev)
+
     if rank == 0:
         line = {
             "metric": "depth-hypotheses/sec (ref-views x H x W x D / s)",
@@ -335,6 +379,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "fusion": fusion_res,
+            "e2e": e2e,
             "kernels": {k: {kk: vv for kk, vv in v.items() if kk != "per_launch"}
                         for k, v in kernels.items()},
         }
