@@ -145,6 +145,27 @@ def test_larger_views_and_batch_match_oracle():
     assert rel_l1(out["depth"].cpu().numpy(), ref["depth"].numpy()) <= 1e-3
 
 
+@pytest.mark.parametrize("shape", [(1, 3, 52, 84, 3), (1, 2, 4, 4, 2), (1, 3, 4, 132, 3)])
+def test_ragged_and_minimum_sizes_match_oracle(shape):
+    """H, W multiples of 4 (the U-Net's two 2x pools, drmvsnet.py:148-150) but not of the
+    16x32 pixel tile: partial tiles, the 4x4 minimum (level-2 maps are 1x1), a 4-row strip."""
+    from oracle import sweep_oracle as orc
+    B, N, H, W, D = shape
+    sc = syn.scene(B, N, H, W, D, seed=H * 1000 + W)
+    P = {k: torch.from_numpy(v) for k, v in syn.sweep_weights(7).items()}
+    feats = torch.from_numpy(sc["features"])
+    proj = torch.from_numpy(sc["proj_matrices"])
+    ref = orc.sweep(feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+                    [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]), P)
+    from aarmvs import ops
+    sw = ops.DepthSweep({k: v.to(DEV) for k, v in P.items()}, DEV)
+    fd = feats.to(DEV)
+    out = sw(fd[0], [fd[v] for v in range(1, N)], proj[:, 0], [proj[:, v] for v in range(1, N)],
+             torch.from_numpy(sc["depth_values"]), want_cost=True)
+    np.testing.assert_allclose(out["cost"].cpu().numpy(), ref["cost"].numpy(), atol=1e-4, rtol=1e-4)
+    assert rel_l1(out["depth"].cpu().numpy(), ref["depth"].numpy()) <= 1e-3
+
+
 def test_rejects_cpu_tensors_and_bad_shapes():
     from aarmvs import ops
     from aarmvs._lib import AarmvsError
