@@ -223,6 +223,36 @@ def test_two_stream_schedule_is_bit_identical():
     assert torch.equal(a["depth"], c["depth"]) and torch.equal(a["conf"], c["conf"])
 
 
+def test_full_size_properties():
+    """BASELINE's full frame (1600x1184, N=7) at D=3, where the oracle is too slow: the
+    two-stream and single-stream schedules and a continued d_range must agree bit for bit,
+    and the WTA depth must be one of the hypotheses (drmvsnet.py:324-339)."""
+    from aarmvs import ops
+    B, N, H, W, D = 1, 7, 1184, 1600, 3
+    sc = syn.scene(B, N, H, W, D, seed=77)
+    feats = torch.from_numpy(sc["features"]).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    dv = torch.from_numpy(sc["depth_values"])
+    args = (feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+            [proj[:, v] for v in range(1, N)], dv)
+    P = P_of(5)
+    a = ops.DepthSweep(P, DEV, overlap=True)(*args, want_cost=True)
+    b = ops.DepthSweep(P, DEV, overlap=False)(*args, want_cost=True)
+    sw = ops.DepthSweep(P, DEV, overlap=True)
+    cost = torch.empty(B, D, H, W, device=DEV)
+    sw(*args, d_range=(0, 1), cost_out=cost)
+    c = sw(*args, d_range=(1, D), cost_out=cost)
+    for k in ("cost", "depth", "conf"):
+        assert torch.equal(a[k], b[k]), k
+    assert torch.equal(a["cost"], cost)
+    assert torch.equal(a["depth"], c["depth"]) and torch.equal(a["conf"], c["conf"])
+    assert torch.isfinite(a["cost"]).all()
+    depth = a["depth"].cpu()
+    # 0 is the initial depth map (drmvsnet.py:301), kept where every exp(cost) underflows
+    hyp = torch.cat([torch.zeros(B, 1), dv.to(depth.dtype)], 1).view(B, D + 1, 1, 1)
+    assert (depth.unsqueeze(1) == hyp).any(dim=1).all()
+
+
 def test_sweep_with_points_behind_a_source_camera_matches_oracle():
     """A source projection whose z row is mixed with its x row (z' = z - x / (W/2) in
     pixel units): z' changes sign across the image, so omega_conv sees tiles with every
