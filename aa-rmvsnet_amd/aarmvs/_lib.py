@@ -76,6 +76,11 @@ SIGNATURES = {
     "aarmvs_unet_step": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),
     "aarmvs_softmax_depth": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "aarmvs_cost_slice": (c_int, [c_void_p, ctypes.POINTER(c_void_p), c_void_p, c_void_p, c_void_p,
+                                  c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                  c_void_p]),
+    "aarmvs_wta_update": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                  c_void_p]),
     "aarmvs_fusion_filter": (c_int, [ctypes.POINTER(FusionArgs), c_void_p]),
     "aarmvs_profile_enable": (None, [c_int]),
     "aarmvs_profile_reset": (None, []),

@@ -35,6 +35,11 @@ def _require_device(*ts: torch.Tensor) -> None:
             raise AarmvsError(f"aarmvs: expected float32 tensors, got {t.dtype}")
 
 
+def _check_proj(p: torch.Tensor, B: int, what: str) -> None:
+    if tuple(p.shape) != (B, 4, 4):
+        raise AarmvsError(f"aarmvs: {what} must be [B={B},4,4], got {tuple(p.shape)}")
+
+
 def relative_projection(src_proj: torch.Tensor, ref_proj: torch.Tensor) -> torch.Tensor:
     """rows 0..2 of src_proj @ inverse(ref_proj) (module.py:16-18), [B,3,4] fp32.
 
@@ -98,6 +103,24 @@ def softmax_depth(cost: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def wta_update(cost: torch.Tensor, depth_d: torch.Tensor, max_prob: torch.Tensor,
+               depth_map: torch.Tensor, exp_sum: torch.Tensor) -> None:
+    """In-place online WTA update of one plane (aarmvs_wta_update, drmvsnet.py:324-334):
+    cost/max_prob/depth_map/exp_sum [B,H,W] fp32 device tensors, depth_d [B]."""
+    ts = (cost, max_prob, depth_map, exp_sum)
+    _require_device(*ts)
+    B = cost.shape[0]
+    for t in ts:
+        if t.shape != cost.shape or not t.is_contiguous():
+            raise AarmvsError("aarmvs: wta_update needs contiguous tensors of one [B,H,W] shape")
+    dep = depth_d.reshape(-1).to(cost.device, torch.float32).contiguous()
+    if dep.numel() != B:
+        raise AarmvsError(f"aarmvs: depth_d must hold B={B} values")
+    check(lib().aarmvs_wta_update(cost.data_ptr(), dep.data_ptr(), max_prob.data_ptr(),
+                                  depth_map.data_ptr(), exp_sum.data_ptr(), B, cost[0].numel(),
+                                  _stream()), "wta_update")
+
+
 class DepthSweep:
     """Runs EMVSNet's depth loop (drmvsnet.py:273-291 / :306-342) on the HIP library.
 
@@ -137,28 +160,50 @@ class DepthSweep:
             self._ws[key] = ws
         return ws
 
+    def relative(self, ref_proj, src_projs, B: int) -> torch.Tensor:
+        """[nsrc,B,12] device tensor of rows 0..2 of src_proj @ inv(ref_proj) per source view
+        (module.py:16-18): one host round trip, reusable across d_range calls."""
+        _check_proj(ref_proj, B, "ref_proj")
+        for sp in src_projs:
+            _check_proj(sp, B, "src_proj")
+        rel = torch.stack([relative_projection(sp, ref_proj) for sp in src_projs])  # [nsrc,B,3,4]
+        return rel.reshape(len(src_projs), B, 12).to(self.device).contiguous()
+
     def __call__(self, ref_fea, src_feas, ref_proj, src_projs, depth_values, *,
-                 want_depth=True, want_cost=False, d_range=None, debug=False, cost_out=None):
+                 want_depth=True, want_cost=False, d_range=None, debug=False, cost_out=None,
+                 rel=None):
         """Returns dict(depth, conf, cost, slice, omega) (entries None when not requested).
 
         ``d_range=(d0, d1)`` runs planes d0..d1-1 only (d0 == 0 resets the hidden state;
         later ranges continue from the state the previous call left in the workspace).
         ``cost_out`` is an optional caller-owned [B,D,H,W] buffer for the regulariser output.
+        ``rel`` is an optional precomputed ``self.relative(ref_proj, src_projs, B)``.
         """
         ref = ref_fea.contiguous()
         srcs = [s.contiguous() for s in src_feas]
         _require_device(ref, *srcs)
+        if ref.dim() != 4:
+            raise AarmvsError(f"aarmvs: ref_fea must be [B,C,H,W], got {tuple(ref.shape)}")
         B, C, H, W = ref.shape
         nsrc = len(srcs)
         if nsrc < 1 or nsrc > _lib.MAX_SRC:
             raise AarmvsError(f"aarmvs: need 1..{_lib.MAX_SRC} source views, got {nsrc}")
+        if len(src_projs) != nsrc:
+            raise AarmvsError(f"aarmvs: {nsrc} source features but {len(src_projs)} projections")
         for s in srcs:
             if s.shape != ref.shape:
                 raise AarmvsError("aarmvs: source features must match the reference feature shape")
+        # the kernels index depth_values[b * D + d] and rel[v][b]: reject mismatches here
+        if depth_values.dim() != 2 or depth_values.shape[0] != B or depth_values.shape[1] < 1:
+            raise AarmvsError(f"aarmvs: depth_values must be [B={B},D], got {tuple(depth_values.shape)}")
         dv = depth_values.to(ref.device, torch.float32).contiguous()
         D = dv.shape[1]
-        rel = torch.stack([relative_projection(sp, ref_proj) for sp in src_projs])  # [nsrc,B,3,4]
-        rel = rel.reshape(nsrc, B, 12).to(ref.device).contiguous()
+        if d_range is not None and not (0 <= d_range[0] < d_range[1] <= D):
+            raise AarmvsError(f"aarmvs: bad d_range {d_range} for D={D}")
+        if rel is None:
+            rel = self.relative(ref_proj, src_projs, B)
+        elif tuple(rel.shape) != (nsrc, B, 12) or not rel.is_cuda:
+            raise AarmvsError(f"aarmvs: rel must be a device [nsrc={nsrc},B={B},12] tensor")
         ws = self.workspace(B, H, W, nsrc)
         out = {"depth": None, "conf": None, "cost": None, "slice": None, "omega": None}
         if want_depth:
@@ -212,6 +257,68 @@ class DepthSweep:
         """Copies of the regulariser's (h, c) per cell as left for the plane of `parity`."""
         return [[self.state(B, H, W, nsrc, parity, k, 0).contiguous().clone(),
                  self.state(B, H, W, nsrc, parity, k, 1).contiguous().clone()] for k in range(5)]
+
+    def _region(self, B, H, W, nsrc):
+        """(byte offset, bytes) of the workspace's contiguous state region (h ping-pong + c of
+        every cell; include/aarmvs.h aarmvs_state_ptr)."""
+        ws = self.workspace(B, H, W, nsrc)
+        L = lib()
+        begin = L.aarmvs_state_ptr(ws.data_ptr(), B, H, W, nsrc, 0, 0, 0)
+        end = L.aarmvs_state_ptr(ws.data_ptr(), B, H, W, nsrc, 0, 4, 1)
+        if not begin or not end:
+            raise AarmvsError("aarmvs: bad state query")
+        end += B * 8 * H * W * 4   # cell 4's c: [B,H,W,8]
+        return begin - ws.data_ptr(), end - begin
+
+    def snapshot_region(self, B, H, W, nsrc) -> torch.Tensor:
+        """One device copy of the whole regulariser state region (raw bytes)."""
+        off, n = self._region(B, H, W, nsrc)
+        return self.workspace(B, H, W, nsrc)[off: off + n].clone()
+
+    def region_states(self, snap: torch.Tensor, B, H, W, nsrc, parity):
+        """(h, c) per cell, NCHW views into a snapshot_region copy, as left for the plane of
+        `parity`."""
+        ws = self.workspace(B, H, W, nsrc)
+        off, _ = self._region(B, H, W, nsrc)
+        L = lib()
+        out = []
+        for k in range(5):
+            hid, sc = (16, 16, 16, 16, 8)[k], (1, 2, 4, 2, 1)[k]
+            n = B * hid * (H // sc) * (W // sc) * 4
+            pair = []
+            for which in (0, 1):
+                p = L.aarmvs_state_ptr(ws.data_ptr(), B, H, W, nsrc, parity, k, which)
+                o = p - ws.data_ptr() - off
+                pair.append(snap[o: o + n].view(torch.float32).view(
+                    B, H // sc, W // sc, hid).permute(0, 3, 1, 2))
+            out.append(pair)
+        return out
+
+    def cost_slice(self, ref_fea, src_feas, ref_proj, src_projs, depth, want_omega=False):
+        """One plane's cost slice x [B,32,H,W] (aarmvs_cost_slice; drmvsnet.py:307-319) at
+        depth [B]; returns (x, omega [nsrc,B,H,W] or None).  Uses this object's workspace."""
+        ref = ref_fea.contiguous()
+        srcs = [s.contiguous() for s in src_feas]
+        _require_device(ref, *srcs)
+        B, C, H, W = ref.shape
+        nsrc = len(srcs)
+        if nsrc < 1 or nsrc > _lib.MAX_SRC or len(src_projs) != nsrc:
+            raise AarmvsError(f"aarmvs: need 1..{_lib.MAX_SRC} source views with projections")
+        for s in srcs:
+            if s.shape != ref.shape:
+                raise AarmvsError("aarmvs: source features must match the reference feature shape")
+        dep = depth.reshape(-1).to(ref.device, torch.float32).contiguous()
+        if dep.numel() != B:
+            raise AarmvsError(f"aarmvs: depth must hold B={B} values")
+        rel = self.relative(ref_proj, src_projs, B)
+        ws = self.workspace(B, H, W, nsrc)
+        x = torch.empty(B, C, H, W, device=ref.device)
+        om = torch.empty(nsrc, B, H, W, device=ref.device) if want_omega else None
+        ptrs = (ctypes.c_void_p * nsrc)(*[s.data_ptr() for s in srcs])
+        check(lib().aarmvs_cost_slice(ref.data_ptr(), ptrs, rel.data_ptr(), dep.data_ptr(),
+                                      self.packed.data_ptr(), B, C, H, W, nsrc, ws.data_ptr(),
+                                      x.data_ptr(), _ptr(om), _stream()), "cost_slice")
+        return x, om
 
     def unet_step(self, x: torch.Tensor, step: int, nsrc: int = 1) -> torch.Tensor:
         _require_device(x)

@@ -66,6 +66,8 @@ const ParamLayout& param_layout();
 struct Workspace {
   double* omega_stats[2]; // per plane parity: [B][nsrc][3][kSlots][2] omega GN statistics
   double* reg_stats;      // [B][2 deconvs][2 groups][kSlots][2] U-Net GN statistics
+  unsigned* xbound;       // float bits of an upper bound on |x| (cost slice) for this sweep:
+                          // 8 max|feature|^2 (to_c8) or max|x| (unet_step); cell 0's fp16 range
   float* max_prob;        // [B,HW]
   float* exp_sum;         // [B,HW]
   float* depth;           // [B,HW]
@@ -118,9 +120,13 @@ struct CostArgs {
 // NCHW <-> NHWC copy of a [B][C][HW] / [B][HW][C] fp32 tensor (API edges only)
 // depth-map fusion core (fusion.hip)
 hipError_t launch_fusion_filter(const aarmvs_fusion_args* a, hipStream_t s);
+// xmax (optional, to_nhwc only): atomic max of |in| as float bits
 hipError_t launch_layout(const float* in, float* out, int B, int C, int HW, bool to_nhwc,
-                         hipStream_t s);
-hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s);
+                         hipStream_t s, unsigned* xmax = nullptr);
+// xbound (optional): atomic max of 8 max|src|^2 as float bits, an upper bound on the cost
+// slice's |x| (|warp - ref| <= 2 max|feature|, (1 + w) <= 2)
+hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s,
+                        unsigned* xbound = nullptr);
 hipError_t launch_cost_x(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d,
                          float* omega_out, hipStream_t s);
 hipError_t launch_omega_next(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d,
@@ -131,6 +137,8 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
 hipError_t launch_head_wta(const float* params, const SweepGeom& g, const Workspace& ws,
                            int parity, const float* depth_values, int d, float* cost_out,
                            bool wta, hipStream_t s);
+hipError_t launch_wta_update(const float* cost, const float* depth_d, float* max_prob,
+                             float* depth, float* exp_sum, int B, int HW, hipStream_t s);
 hipError_t launch_finalize(const SweepGeom& g, const Workspace& ws, float* depth_out,
                            float* conf_out, hipStream_t s);
 hipError_t launch_softmax_depth(const float* cost, float* prob, int B, int D, int HW,

@@ -142,6 +142,7 @@ Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
   ws.omega_stats[0] = reinterpret_cast<double*>(take(ws.omega_stats_bytes));
   ws.omega_stats[1] = reinterpret_cast<double*>(take(ws.omega_stats_bytes));
   ws.reg_stats = reinterpret_cast<double*>(take(ws.reg_stats_bytes));
+  ws.xbound = reinterpret_cast<unsigned*>(take(sizeof(unsigned)));
   ws.stats_bytes = off - stats_begin;
   const size_t wta_begin = off;
   ws.max_prob = reinterpret_cast<float*>(take(B * HW * 4));
@@ -434,20 +435,29 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   // stream 885), so not the default.
   const char* ov_env = std::getenv("AARMVS_OVERLAP");
   const bool ov_all = !(ov_env && std::strcmp(ov_env, "costx") == 0);
-  hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  // main[2], aux[2], fork/join, start[2]
-  auto destroy_events = [&] {
-    for (hipEvent_t& x : ev)
-      if (x) (void)hipEventDestroy(x), x = nullptr;
+  // main[2], aux[2], fork/join, start[2]: a per-thread, per-device set reused across calls
+  // (a training forward makes one call per plane).  Events are only recorded/waited on the
+  // caller's streams, and a record overwrites the previous one, so reuse is safe.
+  struct EventSet {
+    int dev = -1;
+    hipEvent_t ev[7] = {};
   };
-  auto sweep_fail = [&](hipError_t err, const char* where) {
-    destroy_events();
-    return hip_fail(err, where);
-  };
-  if (aux)
-    for (hipEvent_t& x : ev)
-      if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
-        return sweep_fail(e, "sweep: event create");
+  static thread_local EventSet evs;
+  hipEvent_t* ev = evs.ev;
+  auto sweep_fail = [&](hipError_t err, const char* where) { return hip_fail(err, where); };
+  if (aux) {
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return sweep_fail(e, "sweep: get device");
+    if (evs.dev != dev) {
+      for (hipEvent_t& x : evs.ev)
+        if (x) (void)hipEventDestroy(x), x = nullptr;
+      evs.dev = -1;
+      for (hipEvent_t& x : evs.ev)
+        if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
+          return sweep_fail(e, "sweep: event create");
+      evs.dev = dev;
+    }
+  }
   hipEvent_t* ev_main = ev;
   hipEvent_t* ev_aux = ev + 2;
   hipEvent_t* ev_start = ev + 5;
@@ -464,10 +474,12 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
       return sweep_fail(e, "sweep: stats init");
     // c8 copies of the features for the pipeline
     const int HW = a->H * a->W;
-    if ((e = launch_to_c8(a->ref_fea, ws.feat8[0], a->B, HW, stream)) != hipSuccess)
+    // (each copy also folds 8 max|feature|^2 into ws.xbound: cell 0's fp16 range guard)
+    if ((e = launch_to_c8(a->ref_fea, ws.feat8[0], a->B, HW, stream, ws.xbound)) != hipSuccess)
       return sweep_fail(e, "sweep: c8 copy");
     for (int v = 0; v < a->nsrc; ++v)
-      if ((e = launch_to_c8(a->src_fea[v], ws.feat8[1 + v], a->B, HW, stream)) != hipSuccess)
+      if ((e = launch_to_c8(a->src_fea[v], ws.feat8[1 + v], a->B, HW, stream, ws.xbound)) !=
+          hipSuccess)
         return sweep_fail(e, "sweep: c8 copy");
   }
   if (aux) {   // fork: the aux stream starts after everything enqueued on `stream` so far
@@ -533,8 +545,53 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     if ((e = launch_finalize(g, ws, a->depth_out, a->conf_out, stream)) != hipSuccess)
       return sweep_fail(e, "sweep: finalize");
   }
-  destroy_events();
   return AARMVS_OK;
+}
+
+int aarmvs_cost_slice(const float* ref_fea, const float* const* src_fea, const float* rel_proj,
+                      const float* depth_d, const void* packed_params, int B, int C, int H, int W,
+                      int nsrc, void* workspace, float* slice_out, float* omega_out,
+                      hipStream_t stream) {
+  int rc = check_geom(B, H, W, nsrc);
+  if (rc) return rc;
+  if (C != kC) return fail(AARMVS_ERR_INVALID, "cost_slice: feature channels C must be 32");
+  if (!ref_fea || !src_fea || !rel_proj || !depth_d || !packed_params || !workspace || !slice_out)
+    return fail(AARMVS_ERR_INVALID, "cost_slice: null pointer argument");
+  for (int v = 0; v < nsrc; ++v)
+    if (!src_fea[v]) return fail(AARMVS_ERR_INVALID, "cost_slice: null src_fea pointer");
+  // one plane of the sweep's cost-slice pipeline (D = 1, depth_values = depth_d [B,1])
+  SweepGeom g{B, H, W, nsrc, 1, cu_count()};
+  Workspace ws = carve_workspace(workspace, B, H, W, nsrc);
+  CostArgs ca{};
+  ca.ref = ref_fea;
+  for (int v = 0; v < nsrc; ++v) ca.src[v] = src_fea[v];
+  ca.rel = rel_proj;
+  ca.depth_values = depth_d;
+  ca.params = static_cast<const float*>(packed_params);
+  hipError_t e;
+  const int HW = H * W;
+  if ((e = hipMemsetAsync(ws.omega_stats[0], 0, ws.omega_stats_bytes, stream)) != hipSuccess)
+    return hip_fail(e, "cost_slice: stats init");
+  if ((e = launch_to_c8(ref_fea, ws.feat8[0], B, HW, stream)) != hipSuccess)
+    return hip_fail(e, "cost_slice: c8 copy");
+  for (int v = 0; v < nsrc; ++v)
+    if ((e = launch_to_c8(src_fea[v], ws.feat8[1 + v], B, HW, stream)) != hipSuccess)
+      return hip_fail(e, "cost_slice: c8 copy");
+  if ((e = launch_omega_next(ca, g, ws, 0, stream)) != hipSuccess)
+    return hip_fail(e, "cost_slice: omega pipeline");
+  if ((e = launch_cost_x(ca, g, ws, 0, omega_out, stream)) != hipSuccess)
+    return hip_fail(e, "cost_slice: cost slice");
+  if ((e = launch_layout(ws.x, slice_out, B, kC, HW, false, stream)) != hipSuccess)
+    return hip_fail(e, "cost_slice: slice copy");
+  return AARMVS_OK;
+}
+
+int aarmvs_wta_update(const float* cost, const float* depth_d, float* max_prob, float* depth_map,
+                      float* exp_sum, int B, int HW, hipStream_t stream) {
+  if (!cost || !depth_d || !max_prob || !depth_map || !exp_sum || B < 1 || HW < 1)
+    return fail(AARMVS_ERR_INVALID, "wta_update: bad arguments");
+  hipError_t e = launch_wta_update(cost, depth_d, max_prob, depth_map, exp_sum, B, HW, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "wta_update");
 }
 
 int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
@@ -552,8 +609,11 @@ int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
     return hip_fail(e, "unet_step: state init");
   if ((e = hipMemsetAsync(ws.reg_stats, 0, ws.reg_stats_bytes, stream)) != hipSuccess)
     return hip_fail(e, "unet_step: stats reset");
-  // the workspace's slice buffer holds x as NHWC, like the sweep's cost slice
-  if ((e = launch_layout(x, ws.x, B, kC, H * W, true, stream)) != hipSuccess)
+  // the workspace's slice buffer holds x as NHWC, like the sweep's cost slice; max|x| goes
+  // to ws.xbound (cell 0's fp16 range guard)
+  if ((e = hipMemsetAsync(ws.xbound, 0, sizeof(unsigned), stream)) != hipSuccess)
+    return hip_fail(e, "unet_step: bound reset");
+  if ((e = launch_layout(x, ws.x, B, kC, H * W, true, stream, ws.xbound)) != hipSuccess)
     return hip_fail(e, "unet_step: x layout");
   if ((e = launch_unet_step(ws.x, params, g, ws, step & 1, stream)) != hipSuccess)
     return hip_fail(e, "unet_step");

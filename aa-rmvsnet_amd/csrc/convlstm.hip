@@ -42,8 +42,22 @@ struct CellArgs {
   float* c;
   const float* wpk;     // packed A operands [K/2][MT][64]
   const float* bias;    // [4*hid]
+  const unsigned* xbound;   // cell 0: float bits of a bound on |x| (fp16 range guard), or null
   int B, H, W;          // cell resolution
 };
+
+// fp16 range guard of cell 0's input (the cost slice x = -sum (1 + w) sq / nsrc is
+// unbounded, unlike h, pooled h and the GroupNorm outputs of the other parts): x is staged
+// as x 2^-e and the partial sums of the x chunks are rescaled by 2^e (exact) before the h
+// chunk is accumulated, with e >= 0 the smallest exponent that keeps bound 2^-e <= 2^15
+// (fp16's largest finite is 65504).  e = 0 whenever |x| <= 32768: bit-identical to no guard.
+__device__ __forceinline__ int xguard_exp(const unsigned* xb) {
+  if (!xb) return 0;
+  const float bound = __uint_as_float(*xb);
+  if (bound <= 32768.0f) return 0;
+  const int k = ilogbf(bound);   // 2^k <= bound < 2^(k+1); INT_MAX for inf
+  return k >= 134 ? 120 : k - 14;
+}
 
 constexpr int kMaxParts = 3;
 
@@ -153,6 +167,7 @@ struct H3PixStager {
   static_assert(NI <= 32, "item mask holds 32 items");
   float val[NI][8][4];   // [item][channel][POOL window: fine (2y,2x) (2y,2x+1) (2y+1,2x) (2y+1,2x+1)]
   uint32_t in_mask;      // bit j: item j is an in-image pixel of valid channels
+  float xs = 1.0f;       // cell 0: 2^-e of the fp16 range guard (xguard_exp), applied to x
 
   template <int CH>
   __device__ __forceinline__ void load(const CellArgs& a, int b, int y0, int x0, int tid) {
@@ -214,6 +229,7 @@ struct H3PixStager {
             x = fmaxf(val[j][k][0] * gn[lc] + gn[16 + lc], 0.0f);
           } else {
             x = val[j][k][0];
+            if constexpr (KIND == 0 && C::chunk_part(CH) == 0) x *= xs;
           }
           v[k] = in ? x : 0.0f;
         }
@@ -227,6 +243,18 @@ struct H3PixStager {
     }
   }
 };
+
+// Before the MFMAs of chunk CH: undo cell 0's x guard scale on the x chunks' partial sums
+// (CH is the first chunk past the x part).
+template <class C, int KIND, int CH>
+__device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], float xr) {
+  if constexpr (KIND == 0 && CH > 0 && C::chunk_part(CH) != 0 && C::chunk_part(CH - 1) == 0) {
+#pragma unroll
+    for (int m = 0; m < C::MT; ++m)
+#pragma unroll
+      for (int r = 0; r < C::RW; ++r) acc[m][r] *= xr;
+  }
+}
 
 // One input chunk's MFMAs: 9 taps x MT m-tiles x RW rows x 3 split products.  PIPE: the
 // A/B fragments of tap t+1 are read from LDS into a second register set before tap t's
@@ -402,6 +430,9 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     x0 = (rem % tiles_x) * C::TW;
   };
   H3PixStager<KIND, RW, WAVES> st;
+  const int xe = KIND == 0 ? xguard_exp(a.xbound) : 0;
+  st.xs = ldexpf(1.0f, -xe);
+  const float xr = ldexpf(1.0f, xe);
   int tile = blockIdx.x;
   if (tile < ntiles && !(ABL & 2)) {
     int b, y0, x0;
@@ -437,6 +468,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
         st.template load<0>(a, nb, ny0, nx0, tid);
       }
       if (CH == 0) cell_c_load<C>(a, b, yw, x0 + col, hi, cst);
+      xguard_rescale<C, KIND, CH>(acc, xr);
       if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
     };
     chunk(std::integral_constant<int, 0>{});
@@ -498,6 +530,9 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
   int tile = blockIdx.x;
   if (tile >= ntiles) return;   // whole block
   H3PixStager<KIND, RW, WAVES> st;
+  const int xe = KIND == 0 ? xguard_exp(a.xbound) : 0;
+  st.xs = ldexpf(1.0f, -xe);
+  const float xr = ldexpf(1.0f, xe);
   int b, y0, x0;
   coords(tile, b, y0, x0);
   if (!(ABL & 2)) st.template load<0>(a, b, y0, x0, tid);
@@ -533,6 +568,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
       constexpr int AC = A_NEXT ? CH + 2 - NCHK : CH + 2;
       const char* cur = inb + 2 * par * PB;
       char* oth = inb + 2 * (par ^ 1) * PB;
+      xguard_rescale<C, KIND, CH>(acc, xr);
       if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0>(acc, wl_hi, wl_lo, cur, cur + PB, wave, lane);
       if (!(ABL & 2)) {
         if (!F_NEXT || next < ntiles) st.template store<F>(oth, oth + PB, gn, tid, 0, W);
@@ -695,6 +731,46 @@ __global__ void __launch_bounds__(256) deconv_kernel(const float* __restrict__ i
 // ---------------------------------------------------------------------------
 constexpr int kHeadTH = 8, kHeadTW = 32;
 
+// drmvsnet.py:324-334 for one pixel: p = exp(cost) (no max-subtraction), strict-< flag,
+// the arithmetic select of max_prob and depth, exp_sum += p -- op for op (contract off)
+__device__ __forceinline__ void wta_select(float cost, float dv, float& max_prob, float& depth,
+                                           float& exp_sum) {
+#pragma clang fp contract(off)
+  const float pr = expf(cost);
+  const float mp = max_prob;
+  const float f = (mp < pr) ? 1.0f : 0.0f;
+  max_prob = __fadd_rn(__fmul_rn(f, pr), __fmul_rn(1.0f - f, mp));
+  depth = __fadd_rn(__fmul_rn(f, dv), __fmul_rn(1.0f - f, depth));
+  exp_sum = __fadd_rn(exp_sum, pr);
+}
+
+// aarmvs_wta_update: the online WTA of one plane on a caller-given cost slice [B,HW]
+__global__ void __launch_bounds__(256) wta_update_kernel(const float* __restrict__ cost,
+                                                         const float* __restrict__ depth_d,
+                                                         float* __restrict__ max_prob,
+                                                         float* __restrict__ depth,
+                                                         float* __restrict__ exp_sum, int HW) {
+  const int b = blockIdx.y;
+  const float dv = depth_d[b];
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
+    const size_t q = (size_t)b * HW + p;
+    float mp = max_prob[q], dp = depth[q], es = exp_sum[q];
+    wta_select(cost[q], dv, mp, dp, es);
+    max_prob[q] = mp;
+    depth[q] = dp;
+    exp_sum[q] = es;
+  }
+}
+
+hipError_t launch_wta_update(const float* cost, const float* depth_d, float* max_prob,
+                             float* depth, float* exp_sum, int B, int HW, hipStream_t s) {
+  const int blocks = std::max(1, std::min((HW + 255) / 256, 4096));
+  ProfScope ps(s, K_HEAD_WTA);
+  hipLaunchKernelGGL(wta_update_kernel, dim3(blocks, B), dim3(256), 0, s, cost, depth_d, max_prob,
+                     depth, exp_sum, HW);
+  return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__ h4,
                                                        const float* __restrict__ w,
                                                        const float* __restrict__ bias, int H,
@@ -740,14 +816,12 @@ __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__
   const float cost = acc + bias[0];
   if (cost_out) cost_out[((size_t)b * D + d) * HW + p] = cost;
   if (wta) {
-    const float dv = dvals[b * D + d];
     const size_t q = (size_t)b * HW + p;
-    const float pr = expf(cost);
-    const float mp = max_prob[q];
-    const float f = (mp < pr) ? 1.0f : 0.0f;
-    max_prob[q] = __fadd_rn(__fmul_rn(f, pr), __fmul_rn(1.0f - f, mp));
-    depth[q] = __fadd_rn(__fmul_rn(f, dv), __fmul_rn(1.0f - f, depth[q]));
-    exp_sum[q] = __fadd_rn(exp_sum[q], pr);
+    float mp = max_prob[q], dp = depth[q], es = exp_sum[q];
+    wta_select(cost, dvals[b * D + d], mp, dp, es);
+    max_prob[q] = mp;
+    depth[q] = dp;
+    exp_sum[q] = es;
   }
 }
 
@@ -782,24 +856,37 @@ __global__ void __launch_bounds__(256) softmax_depth_kernel(const float* __restr
 // one thread per (b, pixel), all channels.
 __global__ void __launch_bounds__(256) layout_kernel(const float* __restrict__ in,
                                                      float* __restrict__ out, int C, int HW,
-                                                     int to_nhwc) {
+                                                     int to_nhwc, unsigned* __restrict__ xmax) {
   const int b = blockIdx.y;
   const float* ib = in + (size_t)b * C * HW;
   float* ob = out + (size_t)b * C * HW;
+  float mx = 0.f;
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x)
     for (int c = 0; c < C; ++c) {
-      if (to_nhwc)
-        ob[(size_t)p * C + c] = ib[(size_t)c * HW + p];
-      else
+      if (to_nhwc) {
+        const float v = ib[(size_t)c * HW + p];
+        ob[(size_t)p * C + c] = v;
+        const float av = fabsf(v);
+        mx = (av > mx || av != av) ? av : mx;
+      } else {
         ob[(size_t)c * HW + p] = ib[(size_t)p * C + c];
+      }
     }
+  if (xmax) {   // |x| bound for cell 0's fp16 range guard (one atomic per wave)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float q = __shfl_xor(mx, o, 64);
+      mx = (q > mx || q != q) ? q : mx;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(xmax, __float_as_uint(mx != mx ? INFINITY : mx));
+  }
 }
 
 hipError_t launch_layout(const float* in, float* out, int B, int C, int HW, bool to_nhwc,
-                         hipStream_t s) {
+                         hipStream_t s, unsigned* xmax) {
   const int blocks = std::max(1, std::min((HW + 255) / 256, 4096));
   hipLaunchKernelGGL(layout_kernel, dim3(blocks, B), dim3(256), 0, s, in, out, C, HW,
-                     to_nhwc ? 1 : 0);
+                     to_nhwc ? 1 : 0, to_nhwc ? xmax : nullptr);
   return hipGetLastError();
 }
 
@@ -829,6 +916,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // cell 0: [x, h0] @ H
   CellArgs a0 = cell(0, {{x, 32, SRC_PLAIN, nullptr, nullptr, nullptr},
                          {ws.h[0][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
+  a0.xbound = ws.xbound;
   if ((e = run_cell_h3<0>(a0, params + L.h3_scale_off + 0, cu, K_CELL0, s)) != hipSuccess) return e;
   // cell 1: [maxpool(h0'), h1] @ H/2
   CellArgs a1 = cell(1, {{ws.h[0][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},

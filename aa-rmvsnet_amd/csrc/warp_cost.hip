@@ -1018,18 +1018,39 @@ hipError_t launch_omega_next(const CostArgs& ca, const SweepGeom& g, const Works
 // NCHW [B][32][HW] -> c8 [B][4][HW][8] (once per sweep): four 8-channel chunk images of
 // 32-B pixels.  64 pixels per block through LDS: coalesced reads and 16-B writes.
 __global__ void __launch_bounds__(256) nchw_to_c8_kernel(const float* __restrict__ src,
-                                                         float* __restrict__ dst, int HW) {
+                                                         float* __restrict__ dst, int HW,
+                                                         unsigned* __restrict__ xbound) {
   __shared__ float t[kC][65];
+  __shared__ float wmax[4];
   const int b = blockIdx.y, p0 = blockIdx.x * 64;
   const float* s = src + (size_t)b * kC * HW;
   float4* d = reinterpret_cast<float4*>(dst + (size_t)b * kC * HW);
   const int px = threadIdx.x & 63;
+  float mx = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = (threadIdx.x >> 6) + 4 * j;
-    t[c][px] = p0 + px < HW ? s[(size_t)c * HW + p0 + px] : 0.f;
+    const float v = p0 + px < HW ? s[(size_t)c * HW + p0 + px] : 0.f;
+    t[c][px] = v;
+    // NaN-propagating max of |v| (a NaN feature forces the largest fp16 guard scale)
+    const float av = fabsf(v);
+    mx = (av > mx || av != av) ? av : mx;
+  }
+  if (xbound) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float q = __shfl_xor(mx, o, 64);
+      mx = (q > mx || q != q) ? q : mx;
+    }
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
   }
   __syncthreads();
+  if (xbound && threadIdx.x == 0) {
+    float m = 0.f;
+    for (int w = 0; w < 4; ++w) m = (wmax[w] > m || wmax[w] != wmax[w]) ? wmax[w] : m;
+    const float bound = 8.0f * m * m;   // non-negative: float bits order like unsigned
+    atomicMax(xbound, __float_as_uint(bound != bound ? INFINITY : bound));
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int idx = threadIdx.x + 256 * j, ch = idx >> 7, q = (idx & 127) >> 1, h = idx & 1;
@@ -1040,9 +1061,11 @@ __global__ void __launch_bounds__(256) nchw_to_c8_kernel(const float* __restrict
   }
 }
 
-hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s) {
+hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s,
+                        unsigned* xbound) {
   ProfScope ps(s, K_TO_C8);
-  hipLaunchKernelGGL(nchw_to_c8_kernel, dim3((HW + 63) / 64, B), dim3(256), 0, s, src, dst, HW);
+  hipLaunchKernelGGL(nchw_to_c8_kernel, dim3((HW + 63) / 64, B), dim3(256), 0, s, src, dst, HW,
+                     xbound);
   return hipGetLastError();
 }
 

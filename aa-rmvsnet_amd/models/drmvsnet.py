@@ -179,14 +179,26 @@ class EvidentialUnavailable(nn.Module):
         return None, None
 
 
-# sweep parameters in the library's raw-blob order (include/aarmvs.h)
+# sweep parameters in the library's raw-blob order (include/aarmvs.h).  Looked up by
+# walking attributes, not named_parameters(): nn.DataParallel replicas (train.py:173,
+# eval.py:77) hold their parameter copies as plain attributes and expose none.
 def _sweep_params(model: "EMVSNet"):
-    sd = dict(model.named_parameters())
-    return [sd[k] for k in _ops.SWEEP_KEYS]
+    out = []
+    for key in _ops.SWEEP_KEYS:
+        obj = model
+        for part in key.split("."):
+            obj = getattr(obj, part)
+        out.append(obj)
+    return out
 
 
 class _SweepTrain(torch.autograd.Function):
-    """cost volume [B,D,H,W] of the sweep; backward = reverse-plane recompute (BPTT)."""
+    """cost volume [B,D,H,W] of the sweep; backward = reverse-plane recompute (BPTT).
+
+    The forward is one HIP call per plane, snapshotting the regulariser state (one copy of
+    the workspace's state region) before each plane after the first; the snapshots are
+    saved with save_for_backward, so autograd frees them after the backward and a second
+    backward through a freed graph raises autograd's own error, as for any PyTorch op."""
 
     @staticmethod
     def forward(ctx, model, sweep, ref_proj, src_projs, depth_values, ref, *rest):
@@ -195,16 +207,18 @@ class _SweepTrain(torch.autograd.Function):
         B, C, H, W = ref.shape
         D = depth_values.shape[1]
         cost = torch.empty(B, D, H, W, device=ref.device)
-        states = []
+        rel = sweep.relative(ref_proj, src_projs, B)   # once per forward (no per-plane sync)
+        snaps = []
         for d in range(D):
             if d > 0:
-                states.append(sweep.snapshot_state(B, H, W, nsrc, d & 1))
+                snaps.append(sweep.snapshot_region(B, H, W, nsrc))
             sweep(ref, srcs, ref_proj, src_projs, depth_values, want_depth=False,
-                  cost_out=cost, d_range=(d, d + 1))
+                  cost_out=cost, d_range=(d, d + 1), rel=rel)
         ctx.model = model
-        ctx.states = states
+        ctx.sweep = sweep
+        ctx.geom = (B, H, W, nsrc)
         ctx.meta = (ref_proj, src_projs, depth_values, nsrc)
-        ctx.save_for_backward(ref, *srcs)
+        ctx.save_for_backward(ref, *srcs, *snaps)
         return cost
 
     @staticmethod
@@ -213,6 +227,10 @@ class _SweepTrain(torch.autograd.Function):
         ref_proj, src_projs, depth_values, nsrc = ctx.meta
         saved = ctx.saved_tensors
         ref, srcs = saved[0], list(saved[1:1 + nsrc])
+        B, H, W, _ = ctx.geom
+        snaps = saved[1 + nsrc:]
+        # planes d >= 1 start from the state plane d-1 left, in parity (d & 1)'s h buffers
+        states = [ctx.sweep.region_states(s, B, H, W, nsrc, (i + 1) & 1) for i, s in enumerate(snaps)]
         params = _sweep_params(model)
         D = depth_values.shape[1]
         g_ref = torch.zeros_like(ref)
@@ -224,7 +242,8 @@ class _SweepTrain(torch.autograd.Function):
             srcs_l = [s.detach().requires_grad_(True) for s in srcs]
             for d in reversed(range(D)):
                 if d > 0:
-                    hidden = [[t.detach().requires_grad_(True) for t in hc] for hc in ctx.states[d - 1]]
+                    hidden = [[t.detach().contiguous().requires_grad_(True) for t in hc]
+                              for hc in states[d - 1]]
                     flat_hidden = [t for hc in hidden for t in hc]
                 else:
                     hidden, flat_hidden = None, []
@@ -253,7 +272,6 @@ class _SweepTrain(torch.autograd.Function):
                     g_state = [[gh[2 * k] if gh[2 * k] is not None else torch.zeros_like(hidden[k][0]),
                                 gh[2 * k + 1] if gh[2 * k + 1] is not None else torch.zeros_like(hidden[k][1])]
                                for k in range(len(hidden))]
-        ctx.states = None
         return (None, None, None, None, None, g_ref, *g_srcs, *g_params)
 
 

@@ -139,23 +139,48 @@ def make_inputs(cfg, B, seed, device):
     return feats, proj, dv, feats.to(device)
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def real_weights():
+    """The reference's model_dtu_v2 omega/regulariser tensors, as committed in
+    tests/golden/real_weights_sweep.npz (read from the checkpoint with weights_only=True by
+    tests/golden/make_golden.py)."""
+    g = np.load(os.path.join(ROOT, "tests", "golden", "real_weights_sweep.npz"), allow_pickle=False)
+    return {k[2:]: g[k] for k in g.files if k.startswith("w:")}
+
+
 def cpu_baseline(feats, proj, dv, P, planes: int):
-    """Time the CPU oracle on the first `planes` planes of the same inputs."""
+    """SURVEY §8d's CPU baseline: the CPU restatement (oracle/sweep_oracle.py with its
+    F.grid_sample warp, the reference's own ATen kernels; measured beside the imported
+    reference in profiles/r02_cpu_restatement_vs_reference.json) on this host's cores, one
+    warm-up plane then `planes` timed planes of the same inputs.  Returns the oracle's
+    output over planes 0..planes (the parity leg) and the baseline record."""
     from oracle import sweep_oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     threads = max(1, min(threads, os.cpu_count() or 1))
     torch.set_num_threads(threads)
     N = feats.shape[0]
     B, _, H, W = feats.shape[1:]
-    t0 = time.perf_counter()
+    times = []
     ref = orc.sweep(feats[0], list(feats[1:]), proj[:, 0], list(proj[:, 1:].unbind(1)),
-                    dv[:, :planes], P, want_volume=True)
-    dt = time.perf_counter() - t0
+                    dv[:, :planes + 1], P, want_volume=True, fast=True, plane_times=times)
+    dt = sum(times[1:])   # plane 0 is the warm-up
     hyp = B * H * W * planes
     return ref, dict(value=hyp / dt, unit="depth-hypotheses/s", cores=torch.get_num_threads(),
-                     kind="port",
-                     sample=f"oracle/sweep_oracle.py, first {planes} of D planes, B={B}, N={N}, "
-                            f"{W}x{H}, {dt:.1f} s, torch CPU threads={torch.get_num_threads()}")
+                     kind="port", cpu=cpu_model(), s_per_plane=round(dt / planes, 3),
+                     sample=f"oracle/sweep_oracle.py (fast: F.grid_sample warp), 1 warm-up plane + "
+                            f"{planes} timed planes of D, B={B}, N={N}, {W}x{H}, model_dtu_v2 weights, "
+                            f"{dt:.1f} s timed, torch CPU threads={torch.get_num_threads()}, "
+                            f"CPU: {cpu_model()}")
 
 
 def fusion_bench(H: int, W: int, nsrc: int, dev, cpu_leg: bool, reps: int = 10):
@@ -233,6 +258,42 @@ def e2e_bench(N: int, H: int, W: int, D: int, B: int, dev, reps: int = 2):
                 images=f"[{B},{N},3,{H},{W}] ~N(0,1)", depth_finite=ok)
 
 
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: start N rank processes (one per GPU, the torchrun
+    environment set by hand) from this parent, which never initialises the GPU
+    (torch.cuda.device_count() does not, on this image), and exit with the worst code."""
+    import signal
+    import socket
+    import subprocess
+    visible = torch.cuda.device_count()
+    if n > visible:
+        print(f"bench.py: --gpus {n} but only {visible} GPU(s) are visible", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:   # a failed rank would leave the others waiting at a barrier: stop them
+        time.sleep(0.5)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or (code if code > 0 else 128 - code)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -240,7 +301,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default=DEFAULT_CONFIG, choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=1, help="reference views per GPU per step")
-    ap.add_argument("--cpu-planes", type=int, default=2)
+    ap.add_argument("--cpu-planes", type=int, default=8,
+                    help="CPU baseline: timed planes after one warm-up plane (SURVEY 8d: 8)")
+    ap.add_argument("--random-weights", action="store_true",
+                    help="random-init sweep weights instead of the reference's model_dtu_v2")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
@@ -256,7 +320,13 @@ def main():
                          "per-launch figures are unchanged, the headline value is not comparable")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     rank, local, world = env()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched",
+              file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     init_process_group(dev)
@@ -265,7 +335,8 @@ def main():
     if args.planes:
         cfg["D"] = min(cfg["D"], args.planes)
     N, H, W, D, B = cfg["N"], cfg["H"], cfg["W"], cfg["D"], args.batch
-    P = {k: torch.from_numpy(v) for k, v in syn.sweep_weights(1).items()}
+    wts = syn.sweep_weights(1) if args.random_weights else real_weights()
+    P = {k: torch.from_numpy(v) for k, v in wts.items()}
     feats_h, proj, dv, feats = make_inputs(cfg, B, seed=rank, device=dev)
     sweep = ops.DepthSweep({k: v.to(dev) for k, v in P.items()}, dev, overlap=not args.no_overlap)
     if args.high_priority:
@@ -340,15 +411,15 @@ def main():
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        planes = max(1, min(args.cpu_planes, D))
+        planes = max(1, min(args.cpu_planes, D - 1))
         orc_out, cpu = cpu_baseline(feats_h, proj, dv, P, planes)
-        g = sweep(ref, srcs, proj[:, 0], src_proj, dv[:, :planes].contiguous(), want_depth=True,
+        g = sweep(ref, srcs, proj[:, 0], src_proj, dv[:, :planes + 1].contiguous(), want_depth=True,
                   want_cost=True)
         torch.cuda.synchronize()
         cost_err = float((g["cost"].cpu() - orc_out["cost"]).abs().max())
         dref = orc_out["depth"]
         rl1 = float((g["depth"].cpu() - dref).abs().sum() / dref.abs().sum())
-        parity = dict(sample_planes=planes, cost_max_abs_err=cost_err, depth_rel_l1=rl1)
+        parity = dict(sample_planes=planes + 1, cost_max_abs_err=cost_err, depth_rel_l1=rl1)
         cpu["value"] = round(cpu["value"], 1)
 
     fusion_res = None
@@ -372,7 +443,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded numpy features ~N(0,1), SURVEY 8d cameras, random-init weights)",
+            "data": "synthetic (seeded numpy features ~N(0,1), SURVEY 8d cameras, "
+                    + ("random-init weights)" if args.random_weights else "model_dtu_v2 weights)"),
             "config": {"workload": args.config, "ref_views_per_gpu": B, "views": N, "H": H, "W": W,
                        "D": D, "global_batch": B * world, "parallelism": f"ref-view shard x{world}"},
             "roofline": roofline,

@@ -126,6 +126,30 @@ int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
                      const void* packed_params, void* workspace, float* cost_out,
                      hipStream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * One plane's cost slice (SURVEY §8b aarmvs_cost_slice): replaces, for one depth
+ * hypothesis per batch element, drmvsnet.py:307-319 -- homo_warping_depthwise x nsrc
+ * (module.py:6-38), (warp - ref)^2, InterViewAAModule (drmvsnet.py:27-38) and the
+ * weighted accumulation -- giving x = -(sum_v (1 + w_v) sq_v) / nsrc.
+ * src_fea is a HOST array of nsrc device pointers [B,C,H,W]; rel_proj [nsrc][B][12]
+ * (as for aarmvs_sweep); depth_d [B].  slice_out [B,32,H,W]; omega_out [nsrc,B,H,W]
+ * (the omega weights w_v) or NULL.  `workspace` is an aarmvs_sweep_workspace_bytes
+ * buffer used as scratch: a sweep in progress in the same workspace is invalidated.
+ * ------------------------------------------------------------------------- */
+int aarmvs_cost_slice(const float* ref_fea, const float* const* src_fea, const float* rel_proj,
+                      const float* depth_d, const void* packed_params, int B, int C, int H, int W,
+                      int nsrc, void* workspace, float* slice_out, float* omega_out,
+                      hipStream_t stream);
+
+/* Online winner-take-all update of one plane (SURVEY §8b aarmvs_wta_update;
+ * drmvsnet.py:324-334): p = exp(cost) without max-subtraction, flag = max_prob < p
+ * (strict: the first plane wins ties), max_prob/depth_map updated by the reference's
+ * arithmetic select, exp_sum += p.  cost, max_prob, depth_map, exp_sum [B,HW];
+ * depth_d [B].  Start from max_prob = depth_map = exp_sum = 0 (drmvsnet.py:301-304);
+ * the confidence is max_prob / exp_sum after the last plane (:339). */
+int aarmvs_wta_update(const float* cost, const float* depth_d, float* max_prob, float* depth_map,
+                      float* exp_sum, int B, int HW, hipStream_t stream);
+
 /* softmax over the depth axis of cost [B,D,H,W] (drmvsnet.py:291/:342). */
 int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
                          hipStream_t stream);

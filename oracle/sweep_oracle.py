@@ -97,10 +97,21 @@ def bilinear_zeros(src: torch.Tensor, gx: torch.Tensor, gy: torch.Tensor) -> tor
     return acc
 
 
-def homo_warp(src_fea: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor) -> torch.Tensor:
-    """homo_warping_depthwise (module.py:6-38) for a precomputed rel = src@inv(ref)."""
+def homo_warp(src_fea: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor,
+              fast: bool = False) -> torch.Tensor:
+    """homo_warping_depthwise (module.py:6-38) for a precomputed rel = src@inv(ref).
+
+    ``fast`` samples with ``F.grid_sample`` itself (the reference's own call,
+    module.py:36-37, align_corners=False as torch>=1.3 defaults) instead of the explicit
+    gather: the same ATen kernel the reference runs, used by the CPU timing baseline
+    (bench.py) so that it costs what the reference costs.
+    """
     H, W = src_fea.shape[2:]
     gx, gy = homography_grid(rel, depth, H, W)
+    if fast:
+        grid = torch.stack((gx, gy), dim=3)
+        return F.grid_sample(src_fea.float(), grid, mode="bilinear", padding_mode="zeros",
+                             align_corners=False)
     return bilinear_zeros(src_fea.float(), gx, gy)
 
 
@@ -133,11 +144,11 @@ def omega_weight(sq: torch.Tensor, P: dict) -> torch.Tensor:
     return torch.sigmoid(F.conv2d(r, P[k + "2.weight"], P[k + "2.bias"]))
 
 
-def cost_slice(ref_fea, src_feas, rels, depth, P) -> torch.Tensor:
+def cost_slice(ref_fea, src_feas, rels, depth, P, fast: bool = False) -> torch.Tensor:
     """-(sum_v (1+w_v)(warp_v-ref)^2)/(N-1), drmvsnet.py:307-319 (sign folded in)."""
     acc = None
     for src, rel in zip(src_feas, rels):
-        sq = (homo_warp(src, rel, depth) - ref_fea).pow(2)
+        sq = (homo_warp(src, rel, depth, fast) - ref_fea).pow(2)
         w = omega_weight(sq, P)
         term = (w + 1) * sq
         acc = term if acc is None else acc + term
@@ -189,12 +200,15 @@ def unet_step(x, state, P):
 # ----------------------------------------------------------------------------------
 @torch.no_grad()
 def sweep(ref_fea, src_feas, ref_proj, src_projs, depth_values, P, planes=None,
-          want_volume=True):
+          want_volume=True, fast=False, plane_times=None):
     """EMVSNet.forward's depth loop on precomputed features.
 
     Returns dict(depth [B,H,W], conf [B,H,W], cost [B,D,H,W] or None,
-    prob [B,D,H,W] or None).  ``planes`` limits the loop (CPU-baseline sampling).
+    prob [B,D,H,W] or None).  ``planes`` limits the loop (CPU-baseline sampling);
+    ``fast`` warps with F.grid_sample (see homo_warp); ``plane_times``, if a list,
+    receives each plane's wall seconds.
     """
+    import time
     P = {k: v.float() for k, v in P.items()}
     B, C, H, W = ref_fea.shape
     rels = [relative_projection(sp, ref_proj) for sp in src_projs]
@@ -205,8 +219,9 @@ def sweep(ref_fea, src_feas, ref_proj, src_projs, depth_values, P, planes=None,
     exp_sum = torch.zeros(B, H, W)
     costs = []
     for d in range(D):
+        t0 = time.perf_counter()
         dv = depth_values[:, d].float()
-        x = cost_slice(ref_fea.float(), [s.float() for s in src_feas], rels, dv, P)
+        x = cost_slice(ref_fea.float(), [s.float() for s in src_feas], rels, dv, P, fast)
         cost, state = unet_step(x, state, P)
         if want_volume:
             costs.append(cost)
@@ -215,6 +230,8 @@ def sweep(ref_fea, src_feas, ref_proj, src_projs, depth_values, P, planes=None,
         max_prob = flag * prob + (1 - flag) * max_prob          # :328 arithmetic select (NaN-faithful)
         depth_img = flag * dv.view(B, 1, 1).expand(B, H, W) + (1 - flag) * depth_img
         exp_sum = exp_sum + prob                                # :334
+        if plane_times is not None:
+            plane_times.append(time.perf_counter() - t0)
     out = {"depth": depth_img, "conf": max_prob / exp_sum, "cost": None, "prob": None}
     if want_volume:
         vol = torch.stack(costs, 1).squeeze(2)

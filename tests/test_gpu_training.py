@@ -1,0 +1,164 @@
+"""GPU tests of the training path (configs[3]: DTU training 640x512, N=3, D=192, DDP):
+BPTT through the HIP sweep at the full 640x512 frame over a truncated D against CPU
+autograd of the oracle, nn.DataParallel replicas (train.py:173, eval.py:77), and a
+world-2 DDP step (gloo, two processes on the one device) whose gradients must equal the
+hand-averaged per-rank gradients.
+
+Gradient tolerance: 1e-4 of max(the gradient's own scale, 1e-3 x the largest), as in
+test_gpu_models.py (fp32 atomics and reassociation in the backward).
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from conftest import ROOT
+from aarmvs import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+
+def _model(D, H, W, wseed):
+    from models import EMVSNet
+    m = EMVSNet(disparity_level=D, image_scale=1.0, max_h=H, max_w=W, return_depth=False)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    wts = syn.init_weights(shapes, seed=wseed)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in wts.items()}, strict=True)
+    m.feature = nn.Identity()
+    return m.to(DEV)
+
+
+def _oracle_grads(feats, proj, dv, P_cpu, R):
+    """CPU autograd of the oracle's fp32 restatement (F.grid_sample warp)."""
+    from oracle import sweep_oracle as orc
+    N, B, C, H, W = feats.shape
+    fc = feats.clone().requires_grad_(True)
+    rels = [orc.relative_projection(proj[:, v], proj[:, 0]) for v in range(1, N)]
+    state = orc.init_state(B, H, W)
+    costs = []
+    for d in range(dv.shape[1]):
+        x = orc.cost_slice(fc[0], [fc[v] for v in range(1, N)], rels, dv[:, d], P_cpu, fast=True)
+        cost, state = orc.unet_step(x, state, P_cpu)
+        costs.append(cost)
+    prob = torch.softmax(torch.stack(costs, 1).squeeze(2), dim=1)
+    (prob * R).sum().backward()
+    return prob.detach(), fc.grad
+
+
+def _check_param_grads(m, P_cpu):
+    gmax = max(float(p.grad.abs().max()) for p in P_cpu.values())
+    for k, p in m.named_parameters():
+        if k not in P_cpu:
+            continue
+        gr = P_cpu[k].grad.numpy()
+        if k == "cost_regularization.conv_0.bias":   # true gradient 0 (softmax over D)
+            assert abs(float(p.grad)) < 1e-4 * gmax and abs(float(gr)) < 1e-4 * gmax
+            continue
+        tol = 1e-4 * max(np.abs(gr).max(), 1e-3 * gmax)
+        np.testing.assert_allclose(p.grad.cpu().numpy(), gr, atol=tol, err_msg=k)
+
+
+def test_config4_full_frame_training_backward_matches_cpu_autograd():
+    """640x512, N=3 (configs[3]) over the first 4 of D=192's hypotheses."""
+    B, N, H, W, D = 1, 3, 512, 640, 4
+    sc = syn.scene(B, N, H, W, 192, seed=404)
+    dv = torch.from_numpy(sc["depth_values"][:, :D].copy())
+    m = _model(D, H, W, 8)
+    P_cpu = {k: v.detach().cpu().clone().requires_grad_(True)
+             for k, v in m.named_parameters() if k in syn.SWEEP_SHAPES}
+    feats = torch.from_numpy(sc["features"])
+    proj = torch.from_numpy(sc["proj_matrices"])
+    R = torch.randn(B, D, H, W, generator=torch.Generator().manual_seed(3))
+    prob_c, gref = _oracle_grads(feats, proj, dv, P_cpu, R)
+
+    imgs = torch.from_numpy(np.moveaxis(sc["features"], 0, 1).copy()).to(DEV).requires_grad_(True)
+    prob, _, _ = m(imgs, proj.to(DEV), dv.to(DEV))
+    np.testing.assert_allclose(prob.detach().cpu().numpy(), prob_c.numpy(), atol=1e-5)
+    (prob * R.to(DEV)).sum().backward()
+    gi = imgs.grad.cpu().numpy()
+    gref = np.moveaxis(gref.numpy(), 0, 1)
+    np.testing.assert_allclose(gi, gref, atol=1e-4 * np.abs(gref).max())
+    _check_param_grads(m, P_cpu)
+
+
+def test_second_backward_through_freed_graph_raises():
+    """The saved plane states are freed by the first backward (save_for_backward), so a second
+    backward raises autograd's own error; with retain_graph=True it runs and repeats."""
+    B, N, H, W, D = 1, 3, 16, 24, 3
+    sc = syn.scene(B, N, H, W, D, seed=5)
+    m = _model(D, H, W, 2)
+    imgs = torch.from_numpy(np.moveaxis(sc["features"], 0, 1).copy()).to(DEV).requires_grad_(True)
+    proj = torch.from_numpy(sc["proj_matrices"]).to(DEV)
+    dv = torch.from_numpy(sc["depth_values"]).to(DEV)
+    prob, _, _ = m(imgs, proj, dv)
+    loss = (prob * torch.arange(D, device=DEV).view(1, D, 1, 1)).sum()
+    loss.backward(retain_graph=True)
+    g1 = imgs.grad.clone()
+    imgs.grad = None
+    loss.backward()
+    assert torch.equal(g1, imgs.grad)
+    with pytest.raises(RuntimeError):
+        loss.backward()
+
+
+def test_dataparallel_replica_runs_the_hip_sweep():
+    """nn.DataParallel's replicas hold parameters as plain attributes (named_parameters() is
+    empty): the sweep finds them by attribute, forward and backward."""
+    from torch.nn.parallel import replicate
+    B, N, H, W, D = 1, 3, 32, 48, 4
+    sc = syn.scene(B, N, H, W, D, seed=31)
+    m = _model(D, H, W, 3)
+    imgs = torch.from_numpy(np.moveaxis(sc["features"], 0, 1).copy()).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"]).to(DEV)
+    dv = torch.from_numpy(sc["depth_values"]).to(DEV)
+    rep = replicate(m, [0])[0]
+    assert len(list(rep.named_parameters())) == 0
+    prob_r, _, _ = rep(imgs, proj, dv)
+    prob_m, _, _ = m(imgs, proj, dv)
+    assert torch.equal(prob_r, prob_m)
+    prob_r.sum().backward()   # gradients flow back to the original parameters
+    assert m.cost_regularization.cell_list[0].conv.weight.grad is not None
+    m.return_depth = True
+    rep = replicate(m, [0])[0]
+    with torch.no_grad():
+        assert torch.equal(rep(imgs, proj, dv)["depth"], m(imgs, proj, dv)["depth"])
+
+
+def test_ddp_world2_gradients_equal_hand_averaged():
+    """Two processes on the one device, gloo (RCCL refuses two ranks on one GPU): DDP over
+    EMVSNet's HIP training path (_SweepTrain) averages the gradients of the two ranks."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = os.path.join(ROOT, "tests", "ddp_worker.py")
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+        assert p.returncode == 0, out[-3000:]
+    for out in outs:
+        assert "DDP_OK" in out, out[-3000:]

@@ -95,3 +95,31 @@ def test_sweep_refuses_cpu_tensors():
     m = EMVSNet(disparity_level=4, image_scale=1.0, max_h=16, max_w=16, return_depth=True)
     with pytest.raises(AarmvsError):
         m(torch.zeros(1, 2, 3, 16, 16), torch.eye(4).expand(1, 2, 4, 4), torch.ones(1, 4))
+
+
+def test_sweep_params_found_on_dataparallel_style_replicas():
+    """nn.DataParallel replicas (train.py:173) hold parameters as plain attributes, with an
+    empty named_parameters(): the sweep's parameter lookup walks attributes instead."""
+    from models.drmvsnet import EMVSNet, _sweep_params
+    from aarmvs.ops import SWEEP_KEYS
+    m = EMVSNet(8, image_scale=1.0, max_h=16, max_w=16)
+    rep = m._replicate_for_data_parallel()
+    mods = dict(m.named_modules())
+    reps = {"": rep}
+    for name, mod in m.named_modules():          # mimic torch.nn.parallel.replicate
+        if name:
+            parent, _, leaf = name.rpartition(".")
+            r = mod._replicate_for_data_parallel()
+            reps[name] = r
+            reps[parent]._modules[leaf] = r
+    copies = {}
+    for name, mod in mods.items():
+        for pn, p in mod._parameters.items():
+            t = p.detach().clone() * 1.0
+            copies[(name + "." + pn).lstrip(".")] = t
+            setattr(reps[name], pn, t)
+    assert len(list(rep.named_parameters())) == 0
+    got = _sweep_params(rep)
+    assert [t is copies[k] for k, t in zip(SWEEP_KEYS, got)] == [True] * len(SWEEP_KEYS)
+    assert [a is b for a, b in zip(_sweep_params(m), [dict(m.named_parameters())[k] for k in SWEEP_KEYS])] \
+        == [True] * len(SWEEP_KEYS)

@@ -111,3 +111,40 @@ def test_config1_matches_reference():
     p = out["prob"].numpy()
     np.testing.assert_allclose(p[:, :, ::8, ::8], g["prob_sub"], atol=1e-5)
     np.testing.assert_allclose(p.mean(axis=(2, 3)), g["prob_plane_mean"], atol=1e-6)
+
+
+def test_fast_warp_matches_reference_and_gather():
+    """The timing restatement's warp (F.grid_sample, the reference's own call) against the
+    warp fixture, and bit-for-bit against the oracle's explicit gather."""
+    g = load("warp.npz")
+    B, N, H, W, C = (int(x) for x in g["shape"])
+    sc = syn.scene(B, N, H, W, D=4, seed=int(g["seed"]), C=C)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    feats = torch.from_numpy(sc["features"])
+    for v in range(1, N):
+        rel = orc.relative_projection(proj[:, v], proj[:, 0])
+        for d in range(4):
+            dep = torch.from_numpy(g["depths"][:, d])
+            fast = orc.homo_warp(feats[v], rel, dep, fast=True)
+            np.testing.assert_allclose(fast.numpy(), g["out"][v - 1, d], atol=1e-5, rtol=0)
+            np.testing.assert_allclose(fast.numpy(), orc.homo_warp(feats[v], rel, dep).numpy(),
+                                       atol=1e-6, rtol=0)
+
+
+def test_fast_sweep_matches_real_weight_fixture():
+    """The fast sweep with the reference's real model_dtu_v2 weights (real_weights_sweep.npz)."""
+    g = load("real_weights_sweep.npz")
+    B, N, H, W, D = (int(x) for x in g["shape"])
+    sc = syn.scene(B, N, H, W, D, seed=int(g["seed"]))
+    assert syn.array_digest(sc["features"], sc["proj_matrices"], sc["depth_values"]) == str(g["digest"])
+    P = {k[2:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("w:")}
+    feats = torch.from_numpy(sc["features"])
+    proj = torch.from_numpy(sc["proj_matrices"])
+    times = []
+    out = orc.sweep(feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+                    [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]), P,
+                    fast=True, plane_times=times)
+    assert len(times) == D
+    assert rel_l1(out["depth"].numpy(), g["depth"]) <= 1e-3
+    np.testing.assert_allclose(out["conf"].numpy(), g["conf"], atol=1e-4)
+    np.testing.assert_allclose(out["prob"].numpy()[:, :, ::4, ::4], g["prob_sub"], atol=1e-5)
