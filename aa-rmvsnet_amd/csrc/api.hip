@@ -493,7 +493,10 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     if (aux && (e = hipEventRecord(ev_aux[0], aux)) != hipSuccess)
       return sweep_fail(e, "sweep: event record");
   }
-  const bool wta = a->depth_out || a->conf_out;
+  // the WTA images are maintained on every plane, whether or not this call returns depth:
+  // a sweep split into d_range calls gives the same depth/confidence however its earlier
+  // pieces were requested (24 B/px per plane, <0.5% of a plane's time)
+  const bool wta = true;
   const size_t stats_parity_bytes = ws.omega_stats_bytes;
   for (int d = a->d_begin; d < a->d_end; ++d) {
     const bool last = d == a->d_end - 1;
@@ -541,7 +544,7 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         (e = hipStreamWaitEvent(stream, ev[4], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: join");
   }
-  if (wta && a->d_end == a->D) {
+  if ((a->depth_out || a->conf_out) && a->d_end == a->D) {
     if ((e = launch_finalize(g, ws, a->depth_out, a->conf_out, stream)) != hipSuccess)
       return sweep_fail(e, "sweep: finalize");
   }

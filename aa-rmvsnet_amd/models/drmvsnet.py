@@ -23,9 +23,14 @@ What runs where:
   planes in reverse and recomputes each one with this module's PyTorch blocks on the
   device (HIP warp + its HIP bilinear-scatter backward), i.e. truncation-free BPTT by
   per-plane recomputation.
-* The evidential head (evidential/models.py) is outside this build's scope
-  (SURVEY §8f-3): ``EMVSNet.evidential`` is a placeholder whose outputs are ``None``;
-  assign a module with the reference's ``forward(prob_volume, depth_values)`` to enable it.
+* The evidential head (evidential/models.py) is this package's PyTorch
+  restatement ``evidential.models.EvidentialModule``, attached by default with the
+  reference's 221 ``evidential.*`` keys (311 keys in all, as the reference: its shipped
+  90-key checkpoints do not load strictly; ``evidential=False`` drops the head).
+  It runs on the softmax of the HIP cost volume.  The reference head only works at B == 1
+  and D == 32 and raises elsewhere; here ``EMVSNet.forward`` returns None for
+  its outputs at other shapes (``evidential="strict"`` raises EvidentialShapeError, like
+  the reference), so the sweep's outputs stay usable at every BASELINE config.
 """
 from __future__ import annotations
 
@@ -35,6 +40,8 @@ import torch.nn.functional as F
 
 from aarmvs import ops as _ops
 from aarmvs._lib import AarmvsError
+from evidential.models import EvidentialModule, EvidentialShapeError
+from evidential.models import *  # noqa: F401,F403  (the reference: drmvsnet.py:5)
 
 from .module import *  # noqa: F401,F403  (reference re-exports models.module names)
 from .module import (ConvLSTMCell, convgnrelu, deConvGnReLU, deformconvgnrelu,
@@ -42,11 +49,13 @@ from .module import (ConvLSTMCell, convgnrelu, deConvGnReLU, deformconvgnrelu,
 
 __all__ = [
     "IntraViewAAModule", "InterViewAAModule", "FeatNet", "UNetConvLSTM", "EMVSNet",
-    "mvsnet_cls_loss", "EvidentialUnavailable",
+    "mvsnet_cls_loss", "EvidentialUnavailable", "EvidentialModule", "EvidentialShapeError",
+    "loss_der", "loss_emvsnet", "criterion_uncertainty",
     "homo_warping_depthwise", "ConvLSTMCell", "convgnrelu", "DeformConv2d", "deformconvgnrelu",
     "ResnetBlockGn", "resnet_block_gn", "deConvGnReLU",
 ]
 from .module import DeformConv2d, ResnetBlockGn  # noqa: E402,F401
+from evidential.models import criterion_uncertainty, loss_der, loss_emvsnet  # noqa: E402,F401
 
 
 # ----------------------------------------------------------------------------------
@@ -169,7 +178,7 @@ class UNetConvLSTM(nn.Module):
 
 
 class EvidentialUnavailable(nn.Module):
-    """Stand-in for evidential/models.py:EvidentialModule (out of scope)."""
+    """No evidential head (``EMVSNet(..., evidential=False)``): outputs are None."""
 
     def __init__(self, depth=None):
         super().__init__()
@@ -293,7 +302,8 @@ class _SoftmaxDepth(torch.autograd.Function):
 class EMVSNet(nn.Module):
     """drmvsnet.py:234-345 with the depth loop on libaarmvs (gfx950)."""
 
-    def __init__(self, disparity_level, image_scale=0.25, max_h=960, max_w=480, return_depth=False):
+    def __init__(self, disparity_level, image_scale=0.25, max_h=960, max_w=480, return_depth=False,
+                 evidential=True):
         super().__init__()
         self.feature = FeatNet()
         input_size = (int(max_h * image_scale), int(max_w * image_scale))
@@ -303,7 +313,11 @@ class EMVSNet(nn.Module):
                                                 [(3, 3) for _ in range(num_layers)], num_layers,
                                                 bias=True)
         self.omega = InterViewAAModule(32)
-        self.evidential = EvidentialUnavailable(depth=disparity_level)
+        if evidential:
+            self.evidential = EvidentialModule(depth=disparity_level)
+        else:
+            self.evidential = EvidentialUnavailable(depth=disparity_level)
+        self.evidential_strict = evidential == "strict"
         self.return_depth = return_depth
         self._sweep_cache = None
 
@@ -346,7 +360,9 @@ class EMVSNet(nn.Module):
         self._check_geometry(H, W)
         sweep = self._sweep(ref.device)
         dv = depth_values.float()
-        evidential_on = not isinstance(self.evidential, EvidentialUnavailable)
+        # the reference head runs at B == 1, D == 32 only
+        evidential_on = not isinstance(self.evidential, EvidentialUnavailable) and (
+            self.evidential_strict or (B == 1 and depth_values.shape[1] == 32))
 
         if not self.return_depth:
             params = _sweep_params(self)
@@ -359,7 +375,9 @@ class EMVSNet(nn.Module):
                 cost = sweep(ref, srcs, ref_proj, src_projs, dv, want_depth=False,
                              want_cost=True)["cost"]
             prob = _SoftmaxDepth.apply(cost)
-            evidential, prob_combine = self.evidential(prob, depth_values)
+            evidential, prob_combine = None, None
+            if evidential_on:
+                evidential, prob_combine = self.evidential(prob, depth_values)
             return prob, evidential, prob_combine
 
         out = sweep(ref, srcs, ref_proj, src_projs, dv, want_depth=True, want_cost=evidential_on)

@@ -249,18 +249,71 @@ def gen_ckpt(drm, mod, out):
     out.append("real_weights_sweep.npz")
 
 
+def gen_evidential(drm, mod, out):
+    """The evidential head (evidential/models.py:183-459) and loss_der (:517-558), which the
+    reference's drivers consume (train.py:297-304, eval.py:151-153): the full EMVSNet
+    state_dict layout, the head's outputs in eval and train mode on a softmax volume at its
+    only working shape (B=1, D=32), and loss_der / loss_emvsnet /
+    criterion_uncertainty on the train-mode output."""
+    import json
+    import evidential.models as evm
+    model, _ = make_model(drm, 32, 32, 40, return_depth=False, seed=9, identity_feature=False,
+                          evidential=True)
+    layout = {k: list(v.shape) for k, v in model.state_dict().items()}
+    with open(os.path.join(HERE, "emvsnet_layout.json"), "w") as f:
+        json.dump({"keys": layout}, f, indent=0, sort_keys=True)
+    out.append("emvsnet_layout.json")
+    head = model.evidential
+    rng = np.random.default_rng(77)
+    logits = rng.standard_normal((1, 32, 32, 40)).astype(np.float32) * 2.0
+    dv = syn.depth_hypotheses(32)[None]
+    prob = torch.softmax(t(logits), dim=1)
+    with torch.no_grad():
+        head.eval()
+        ev_e, comb_e = head(prob, t(dv))
+        head.train()
+        ev_t, comb_t = head(prob, t(dv))
+    depth_gt = rng.uniform(400, 960, (1, 32, 40)).astype(np.float32)
+    mask = (rng.uniform(0, 1, (1, 32, 40)) > 0.3).astype(np.float32)
+    outputs = {"probability_volume": prob, "evidential_prediction": ev_t}
+    loss, gamma, evd = evm.loss_der(outputs, t(depth_gt), t(mask), t(dv))
+    u, la, al, be = (ev_t[i:i + 1] for i in range(4))
+    crit = evm.criterion_uncertainty(u, la, al, be, t(depth_gt), t(mask))
+    lem = evm.loss_emvsnet(u, la, al, be, t(depth_gt), t(mask))
+    np.savez_compressed(os.path.join(HERE, "evidential.npz"), logits=logits, depth_values=dv,
+                        ev_eval=ev_e.numpy(), comb_eval=comb_e.numpy(), ev_train=ev_t.numpy(),
+                        comb_train=comb_t.numpy(), depth_gt=depth_gt, mask=mask,
+                        loss_der=loss.numpy(), gamma=gamma.numpy(),
+                        criterion_uncertainty=crit.numpy(), loss_emvsnet=lem.numpy(),
+                        wseed=9, **{"der:" + k: v.numpy() for k, v in evd.items()})
+    out.append("evidential.npz")
+
+
+GENERATORS = (gen_warp, gen_slice_omega, gen_unet, gen_sweeps, gen_config1, gen_e2e, gen_ckpt,
+              gen_evidential)
+
+
 def main():
+    """``make_golden.py [gen_name ...]`` regenerates only the named fixtures (default all);
+    MANIFEST.txt lists every generator's output."""
     torch.manual_seed(0)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     drm, mod = import_reference()
+    only = set(sys.argv[1:])
     out = []
-    for fn in (gen_warp, gen_slice_omega, gen_unet, gen_sweeps, gen_config1, gen_e2e, gen_ckpt):
+    for fn in GENERATORS:
+        if only and fn.__name__ not in only:
+            continue
         fn(drm, mod, out)
         print("wrote", out[-1], flush=True)
-    with open(os.path.join(HERE, "MANIFEST.txt"), "w") as f:
+    manifest = os.path.join(HERE, "MANIFEST.txt")
+    names = [ln.strip() for ln in open(manifest) if ln.strip() and not ln.startswith("#")] \
+        if only and os.path.exists(manifest) else []
+    names += [n for n in out if n not in names]
+    with open(manifest, "w") as f:
         f.write("# generated by tests/golden/make_golden.py from the reference run on CPU\n")
         f.write(f"# torch {torch.__version__}, numpy {np.__version__}\n")
-        for name in out:
+        for name in names:
             f.write(name + "\n")
 
 

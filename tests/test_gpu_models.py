@@ -24,6 +24,11 @@ def load(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 
 
+def close(a, b, rel=1e-4):
+    """within rel x the reference output's largest magnitude (the 3D hourglass in fp32)"""
+    np.testing.assert_allclose(a, b, atol=rel * max(np.abs(b).max(), 1e-30), rtol=0)
+
+
 def rel_l1(a, b):
     return float(np.abs(a - b).sum() / max(np.abs(b).sum(), 1e-30))
 
@@ -58,10 +63,23 @@ def test_emvsnet_end_to_end_with_featnet():
         out = m(imgs, proj, dv)
         assert rel_l1(out["depth"].cpu().numpy(), g["depth"]) <= 1e-3
         np.testing.assert_allclose(out["photometric_confidence"].cpu().numpy(), g["conf"], atol=1e-4)
-        assert out["evidential_prediction"] is None   # head out of scope
+        # the evidential head on the softmax of the HIP cost volume
+        close(out["evidential_prediction"].cpu().numpy(), g["evidential_eval"])
         m.return_depth = False
         prob, ev, comb = m(imgs, proj, dv)
-    np.testing.assert_allclose(prob.cpu().numpy(), g["prob"], atol=1e-4)
+        np.testing.assert_allclose(prob.cpu().numpy(), g["prob"], atol=1e-4)
+        close(ev.cpu().numpy(), g["evidential"])
+        close(comb.cpu().numpy(), g["prob_combine"])
+        m.train()   # BatchNorm batch statistics, as the reference's training step
+        prob_t, ev_t, _ = m(imgs, proj, dv)
+    np.testing.assert_allclose(prob_t.cpu().numpy(), g["prob_train"], atol=1e-4)
+    close(ev_t.cpu().numpy(), g["evidential_train"])
+    # loss_der (train.py:297-304) runs on the drop-in's outputs
+    from evidential.models import loss_der
+    loss, gamma, evd = loss_der({"probability_volume": prob_t, "evidential_prediction": ev_t},
+                                torch.from_numpy(g["depth_gt"]).to(DEV),
+                                torch.from_numpy(g["mask"]).to(DEV), dv)
+    assert torch.isfinite(loss) and gamma.shape == (1, H, W)
 
 
 def test_emvsnet_real_checkpoint_weights():
@@ -72,7 +90,7 @@ def test_emvsnet_real_checkpoint_weights():
     m = EMVSNet(disparity_level=D, image_scale=1.0, max_h=H, max_w=W, return_depth=True)
     sd = {k[2:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("w:")}
     missing = m.load_state_dict(sd, strict=False).missing_keys
-    assert all(k.startswith("feature.") for k in missing)
+    assert all(k.startswith(("feature.", "evidential.")) for k in missing)
     m.feature = nn.Identity()
     m = m.to(DEV).eval()
     sc = syn.scene(B, N, H, W, D, seed=int(g["seed"]))

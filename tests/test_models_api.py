@@ -22,13 +22,22 @@ def load(name):
 
 
 def test_state_dict_matches_checkpoint_layout():
+    """Without the head: the shipped checkpoints' 90 core keys (load strictly).  With it (the
+    default): the reference EMVSNet's full 311-key layout (emvsnet_layout.json)."""
     from models import EMVSNet
     with open(os.path.join(GOLDEN, "ckpt_layout.json")) as f:
         layout = json.load(f)["keys"]
-    m = EMVSNet(disparity_level=48)
+    m = EMVSNet(disparity_level=48, evidential=False)
     sd = {k: list(v.shape) for k, v in m.state_dict().items()}
     assert sd == layout
     assert sum(int(np.prod(s)) for s in sd.values()) == 187203
+    with open(os.path.join(GOLDEN, "emvsnet_layout.json")) as f:
+        full = json.load(f)["keys"]
+    sd = {k: list(v.shape) for k, v in EMVSNet(disparity_level=48).state_dict().items()}
+    assert sd == full and len(sd) == 311
+    assert len([k for k in sd if k.startswith("evidential.")]) == 221
+    n = sum(int(np.prod(s)) for k, s in sd.items() if not k.endswith("num_batches_tracked"))
+    assert n - sum(int(np.prod(s)) for k, s in sd.items() if "running_" in k) == 4494115
 
 
 def _model_with_weights(D, H, W, wseed, return_depth):
@@ -115,6 +124,8 @@ def test_sweep_params_found_on_dataparallel_style_replicas():
     copies = {}
     for name, mod in mods.items():
         for pn, p in mod._parameters.items():
+            if p is None:
+                continue
             t = p.detach().clone() * 1.0
             copies[(name + "." + pn).lstrip(".")] = t
             setattr(reps[name], pn, t)
