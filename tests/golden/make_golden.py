@@ -289,8 +289,48 @@ def gen_evidential(drm, mod, out):
     out.append("evidential.npz")
 
 
+def _reference_datasets():
+    """The reference's ``datasets`` package, loaded by path (the name is also taken by an
+    installed library)."""
+    import importlib.util
+    for name in [m for m in sys.modules if m == "datasets" or m.startswith("datasets.")]:
+        del sys.modules[name]
+    spec = importlib.util.spec_from_file_location(
+        "datasets", os.path.join(REF, "datasets", "__init__.py"),
+        submodule_search_locations=[os.path.join(REF, "datasets")])
+    pkg = importlib.util.module_from_spec(spec)
+    sys.modules["datasets"] = pkg
+    spec.loader.exec_module(pkg)
+    import datasets.dtu_yao as dy  # noqa
+    return dy
+
+
+def gen_datasets(drm, mod, out):
+    """The training loader (datasets/dtu_yao.py) run by the reference on the committed tiny
+    DTU-format tree tests/golden/dtu_mini (synthetic cameras, 64x80 PNGs, 16x20 PFMs):
+    samples with ascending and flipped hypotheses, linear and inverse spacing, fixed range.
+    (The eval loaders import OpenCV, absent here: their camera/hypothesis recipes are
+    checked against known answers in tests/test_datasets.py.)"""
+    dy = _reference_datasets()
+    root = os.path.join(HERE, "dtu_mini")
+    res = {}
+    for tag, kw, idxs in (("lin", {}, (0, 1, 5)),
+                          ("inv", {"inverse_depth": True, "fix_range": True}, (2, 7))):
+        ds = dy.MVSDataset(root, os.path.join(root, "scans.txt"), "train", 3, ndepths=48,
+                           light_idx=3, image_scale=0.25, **kw)
+        res[f"{tag}:n"] = np.array(len(ds))
+        for i in idxs:
+            smp = ds[i]
+            for k, v in smp.items():
+                if k == "name":
+                    v = os.path.relpath(v, root)
+                res[f"{tag}:{i}:{k}"] = np.asarray(v)
+    np.savez_compressed(os.path.join(HERE, "datasets.npz"), **res)
+    out.append("datasets.npz")
+
+
 GENERATORS = (gen_warp, gen_slice_omega, gen_unet, gen_sweeps, gen_config1, gen_e2e, gen_ckpt,
-              gen_evidential)
+              gen_evidential, gen_datasets)
 
 
 def main():

@@ -80,13 +80,13 @@ def test_full_frame_config_matches_oracle(cfg, k):
 
 
 def test_cell0_fp16_range_guard_with_large_features():
-    """Features x40: the cost slice reaches |x| > 65504 (fp16's largest finite), which the
+    """Features x100: the cost slice reaches |x| > 65504 (fp16's largest finite), which the
     split-fp16 cells would turn into inf without the guard (convlstm.hip xguard_exp)."""
     from oracle import sweep_oracle as orc
     from aarmvs import ops
     B, N, H, W, D = 1, 4, 64, 96, 4
     sc = syn.scene(B, N, H, W, D, seed=300)
-    feats = torch.from_numpy(sc["features"]) * 40.0
+    feats = torch.from_numpy(sc["features"]) * 100.0
     proj = torch.from_numpy(sc["proj_matrices"])
     dv = torch.from_numpy(sc["depth_values"])
     P = real_P()
