@@ -46,6 +46,8 @@ const ParamLayout& param_layout() {
     pk += 4 * 2 * 64 * 8 / 2;   // halves -> floats
     l.owb_scale_off = pk;
     pk += 64;
+    l.owm_off = pk;
+    pk += 4 * 2 * 64 * 8 / 2;   // halves -> floats
     for (int k = 0; k < 2; ++k) {
       l.dct_off[k] = pk;
       pk += 16 * 9 * 16;
@@ -273,6 +275,17 @@ __global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __r
     const float x = w[(co * 32 + 8 * c + ci8) * 9 + tap] * sc;
     const _Float16 xh = (_Float16)x;
     b[i] = g < 2 ? xh : (_Float16)(x - (float)xh);
+  }
+  // omega_mfma's v_mfma_f32_32x32x16_f16 B fragments: per chunk c and kind k (0: [W_hi; W_hi]
+  // against A = [sq hi | sq lo], 1: [W_lo; 0]), lane l holds B[8 (l >> 5) + j][n = l & 31]
+  // with column n = 4 u + co (tap slot u: taps 0..3, 5..8)
+  _Float16* bm = reinterpret_cast<_Float16*>(pk + L.owm_off);
+  for (int i = threadIdx.x; i < 4 * 2 * 64 * 8; i += blockDim.x) {
+    const int j = i & 7, lane = (i >> 3) & 63, k = (i >> 9) & 1, c = i >> 10;
+    const int n = lane & 31, u = n >> 2, tap = u < 4 ? u : u + 1, co = n & 3;
+    const float x = w[(co * 32 + 8 * c + j) * 9 + tap] * sc;
+    const _Float16 xh = (_Float16)x;
+    bm[i] = k == 0 ? xh : ((lane >> 5) == 0 ? (_Float16)(x - (float)xh) : (_Float16)0.0f);
   }
 }
 
@@ -575,10 +588,12 @@ int aarmvs_cost_slice(const float* ref_fea, const float* const* src_fea, const f
   const int HW = H * W;
   if ((e = hipMemsetAsync(ws.omega_stats[0], 0, ws.omega_stats_bytes, stream)) != hipSuccess)
     return hip_fail(e, "cost_slice: stats init");
-  if ((e = launch_to_c8(ref_fea, ws.feat8[0], B, HW, stream)) != hipSuccess)
+  if ((e = hipMemsetAsync(ws.xbound, 0, sizeof(unsigned), stream)) != hipSuccess)
+    return hip_fail(e, "cost_slice: bound init");
+  if ((e = launch_to_c8(ref_fea, ws.feat8[0], B, HW, stream, ws.xbound)) != hipSuccess)
     return hip_fail(e, "cost_slice: c8 copy");
   for (int v = 0; v < nsrc; ++v)
-    if ((e = launch_to_c8(src_fea[v], ws.feat8[1 + v], B, HW, stream)) != hipSuccess)
+    if ((e = launch_to_c8(src_fea[v], ws.feat8[1 + v], B, HW, stream, ws.xbound)) != hipSuccess)
       return hip_fail(e, "cost_slice: c8 copy");
   if ((e = launch_omega_next(ca, g, ws, 0, stream)) != hipSuccess)
     return hip_fail(e, "cost_slice: omega pipeline");

@@ -12,6 +12,7 @@
 
 #include <climits>
 #include <cstdlib>
+#include <cstring>
 
 #include "device_common.h"
 
@@ -176,6 +177,7 @@ struct PipeArgs {
   float* omega_out;           // [nsrc,B,H,W] (prev plane) or null
   const float* params;
   size_t off_owb, off_owb_scale;   // omega conv MFMA B fragments, their scale
+  size_t off_owm, off_owm_scale;   // omega_mfma's 32x32x16 B fragments, their scale
   size_t off_ow0t, off_ow0, off_ob0, off_og0w, off_og0b, off_ow1, off_ob1, off_og1w, off_og1b, off_ow2,
       off_ob2, off_og2w, off_og2b, off_owo, off_obo;
   int B, H, W, nsrc;
@@ -558,7 +560,9 @@ __device__ __forceinline__ int img_half(uint32_t p, int s) { return s ^ (int)((p
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // split-fp16 sq image (MFMA A operand), 32 B per pixel: slot 0 the fp16 hi parts of the
 // 8 channels, slot 1 fp16(v - hi), the slots swapped when bit 3 of p is set (img_slot's
@@ -868,6 +872,225 @@ omega_conv_kernel(PipeArgs a,
 // the library's omega_conv variant (0: VALU conv)
 constexpr int kOmegaConvAbl = 0;
 
+// ---------------------------------------------------------------------------
+// omega_mfma: t1 of plane d_next for one (tile, view) per block with the conv3x3 32->4 on
+// the matrix cores as a GEMM followed by a shifted gather.
+//
+// The block owns a haloed 16 x 32 pixel tile (output: its 14 x 30 interior); wave w owns
+// haloed rows 2w (lanes 0-31) and 2w+1 (lanes 32-63), one pixel per lane.  Per 8-channel
+// chunk the source box arrives in LDS by LDS-DMA (as in omega_conv); each lane samples its
+// own pixel (8 channels), forms sq = (warp - ref)^2 (the reference feature straight from
+// the c8 image: one pixel per lane, no LDS), and splits sq 2^-e into fp16 hi + lo.  One
+// v_permlane32_swap per dword pair turns the 64 lanes' (hi, lo) into the A operands of
+// two v_mfma_f32_32x32x16_f16 row groups (rows = the 32 pixels of a haloed row; K =
+// [8 ch hi | 8 ch lo]), and
+//   Y[px][u, co] += A x [W_hi ; W_hi]   +   A x [W_lo ; 0]        (u: 8 off-centre taps)
+// gives hi W_hi + lo W_hi + hi W_lo (the split-fp16 product) over
+// the 32 N columns (tap slot u, output channel co).  The centre tap stays an fp32 VALU
+// chain on the lane's own sq.  After the 4 chunks Y goes to LDS (pixel stride 36 floats:
+// conflict-free float4 reads) and each interior pixel sums its 8 neighbours' Y[., u, co].
+// sq is staged x 2^-e (e from the sweep's |x| bound, ws.xbound: sq <= 4 max|feature|^2
+// <= bound) so that fp16 cannot overflow; the weights carry their own power-of-two scale.
+// ---------------------------------------------------------------------------
+constexpr int kMTileH = 16, kMTileW = 32, kMThreads = kMTileH * kMTileW;   // haloed tile
+constexpr int kMOutH = kMTileH - 2, kMOutW = kMTileW - 2;                  // output tile
+constexpr int kMYStride = 36;                                               // floats per pixel in Y
+constexpr int kMBoxPx = 1024;
+
+__global__ void __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(4)))
+omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restrict__ Rel,
+                  const unsigned* __restrict__ xbound) {
+  constexpr int NB = (2 * kMBoxPx + kMThreads - 1) / kMThreads;   // box pieces per thread
+  constexpr int YFL = kMThreads * kMYStride;                      // Y image floats
+  static_assert(YFL >= (kMBoxPx + 1) * 8, "the box fits in the Y image space");
+  __shared__ __attribute__((aligned(16))) float smem[YFL];
+  float* const box = smem;   // chunk c's source box, then (after the last chunk) Y
+  float* const yimg = smem;
+  __shared__ int red[kMThreads / 64][4];
+  __shared__ float wsum[kMThreads / 64][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.z;
+  const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
+  const int seq = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = seq / nsrc, v = seq - tile * nsrc;
+  const int tiles_x = (W + kMOutW - 1) / kMOutW;
+  const int y0 = (tile / tiles_x) * kMOutH, x0 = (tile % tiles_x) * kMOutW;
+  const int hy = 2 * wave + (lane >> 5), hx = lane & 31;   // haloed pixel of this lane
+  const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
+  const bool in_img = gy >= 0 && gy < H && gx >= 0 && gx < W;
+  const bool interior = in_img && hy >= 1 && hy <= kMOutH && hx >= 1 && hx <= kMOutW;
+  if (tid < 8) box[kMBoxPx * 8 + tid] = 0.f;   // the zero pixel
+
+  const float dep = a.dvals[b * a.D + a.d_next];
+  const float* __restrict__ m = Rel + 12 * (v * a.B + b);
+  const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);
+  const uint32_t cbytes = (uint32_t)HW * 32u;
+  const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(a.ref + (size_t)b * kC * HW, fbytes);
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
+  TapF tf{};
+  int lx = INT_MAX, ly = INT_MAX, bhx = INT_MIN, bhy = INT_MIN;
+  if (in_img) {
+    tf = tap_f(m, dep, gx, gy, H, W);
+    box_extend(tf, H, W, lx, ly, bhx, bhy);
+  }
+  const Box bx = box_reduce(lx, ly, bhx, bhy, red);
+  const bool lds = bx.nx * bx.ny <= min(kMBoxPx, a.box_cap);
+  const uint32_t zp = lds ? (uint32_t)kMBoxPx : fbytes / 32u;
+  const TapP tp = tap_p(tf, in_img, H, W, lds, bx, zp);
+  const int items = lds ? bx.nx * bx.ny * 2 : 0;
+  const uint32_t mg = box_magic(bx.nx);
+  uint32_t boff[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int i = tid + j * kMThreads, p = i >> 1, r = box_row(p, bx.nx, mg);
+    const uint32_t gp = __umul24((uint32_t)(bx.y0 + r), (uint32_t)W) + (uint32_t)bx.x0 +
+                        ((uint32_t)p - __umul24((uint32_t)r, (uint32_t)bx.nx));
+    boff[j] = gp * 32u + 16u * (uint32_t)img_half((uint32_t)p, i & 1);
+  }
+  auto stage = [&](int c) {
+    const uint32_t cb = (uint32_t)c * cbytes;
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      if (tid + j * kMThreads < items) dma16(rsrc, box + (j * kMThreads + wave * 64) * 4, boff[j] + cb);
+  };
+  // this lane's reference pixel in the c8 image (past the buffer: zeros)
+  const uint32_t rpix = in_img ? (uint32_t)(gy * W + gx) : fbytes / 32u;
+  // sq guard: sq 2^-e <= 2^15 (sq <= 4 max|f|^2 <= bound)
+  int e = 0;
+  {
+    const float bound = __uint_as_float(*xbound);
+    if (bound > 32768.0f) {
+      const int k = ilogbf(bound);
+      e = k >= 134 ? 120 : k - 14;
+    }
+  }
+  const float sqs = ldexpf(1.0f, -e);
+  const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]: centre tap = tap 4
+  const half8* __restrict__ owm = reinterpret_cast<const half8*>(P + a.off_owm);
+  floatx16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+  float o4[4] = {0.f, 0.f, 0.f, 0.f};
+
+  stage(0);
+  float4 rf0 = ld_c8(rref, rpix, 0, HW), rf1 = ld_c8(rref, rpix, 1, HW);
+  dma_wait();
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < 4; ++c) {
+    // sample the own pixel (8 channels) and form sq
+    float4 g0, g1;
+    if (lds) {
+      g0 = bil4(img_ld(box, tp.pix[0], 0), img_ld(box, tp.pix[1], 0), img_ld(box, tp.pix[2], 0),
+                img_ld(box, tp.pix[3], 0), tp);
+      g1 = bil4(img_ld(box, tp.pix[0], 1), img_ld(box, tp.pix[1], 1), img_ld(box, tp.pix[2], 1),
+                img_ld(box, tp.pix[3], 1), tp);
+    } else {
+      g0 = bil4(ld_c8(rsrc, tp.pix[0], 2 * c, HW), ld_c8(rsrc, tp.pix[1], 2 * c, HW),
+                ld_c8(rsrc, tp.pix[2], 2 * c, HW), ld_c8(rsrc, tp.pix[3], 2 * c, HW), tp);
+      g1 = bil4(ld_c8(rsrc, tp.pix[0], 2 * c + 1, HW), ld_c8(rsrc, tp.pix[1], 2 * c + 1, HW),
+                ld_c8(rsrc, tp.pix[2], 2 * c + 1, HW), ld_c8(rsrc, tp.pix[3], 2 * c + 1, HW), tp);
+    }
+    const float4 s0 = sqdiff4(g0, rf0), s1 = sqdiff4(g1, rf1);
+    const float sq[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    if (c < 3) {   // the next chunk's reference pixel, in flight during this chunk
+      rf0 = ld_c8(rref, rpix, 2 * c + 2, HW);
+      rf1 = ld_c8(rref, rpix, 2 * c + 3, HW);
+    }
+    __syncthreads();   // every lane's box reads of chunk c are done
+    if (c < 3) stage(c + 1);
+    // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel, fp32
+    {
+      const float* wt = w0t + (4 * kC + 8 * c) * 4;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int co = 0; co < 4; ++co) o4[co] = fmaf(sq[j], wt[j * 4 + co], o4[co]);
+    }
+    // split sq 2^-e into fp16 hi + lo (out-of-image pixels: the conv's zero padding)
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p0 = in_img ? sq[2 * i] * sqs : 0.f, p1 = in_img ? sq[2 * i + 1] * sqs : 0.f;
+      const _Float16 h0 = (_Float16)p0, h1 = (_Float16)p1;
+      const half2_t hv = {h0, h1};
+      const half2_t lv = {(_Float16)(p0 - (float)h0), (_Float16)(p1 - (float)h1)};
+      hw[i] = __builtin_bit_cast(uint32_t, hv);
+      lw[i] = __builtin_bit_cast(uint32_t, lv);
+    }
+    // lanes 0-31 / 32-63 hold rows 2w / 2w+1: after the swaps, (hw, lw) are the A operands
+    // of row 2w (lanes 0-31 hi, 32-63 lo of pixel lane & 31) and of row 2w+1
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane32_swap(hw[i], lw[i], false, false);
+      hw[i] = r[0];
+      lw[i] = r[1];
+    }
+    const half8 A0 = __builtin_bit_cast(half8, u32x4{hw[0], hw[1], hw[2], hw[3]});
+    const half8 A1 = __builtin_bit_cast(half8, u32x4{lw[0], lw[1], lw[2], lw[3]});
+    const half8 Bd = owm[(c * 2 + 0) * 64 + lane], Bl = owm[(c * 2 + 1) * 64 + lane];
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl, acc1, 0, 0, 0);
+    if (c < 3) {
+      dma_wait();
+      __syncthreads();   // chunk c+1's box visible
+    }
+  }
+  // Y image (over the box space: every lane passed chunk 3's box reads before the barrier
+  // above): D[row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)][col = lane & 31] of row group g
+  {
+    const int col = lane & 31, rb = 4 * (lane >> 5);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int px = (r & 3) + 8 * (r >> 2) + rb;
+      yimg[((2 * wave) * kMTileW + px) * kMYStride + col] = acc0[r];
+      yimg[((2 * wave + 1) * kMTileW + px) * kMYStride + col] = acc1[r];
+    }
+  }
+  __syncthreads();
+  float ps = 0.f, pss = 0.f;
+  if (interior) {
+    float g4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int tap = u < 4 ? u : u + 1;
+      const int q = (hy + tap / 3 - 1) * kMTileW + hx + tap % 3 - 1;
+      const float4 yv = *reinterpret_cast<const float4*>(yimg + q * kMYStride + 4 * u);
+      g4[0] += yv.x;
+      g4[1] += yv.y;
+      g4[2] += yv.z;
+      g4[3] += yv.w;
+    }
+    const float isc = P[a.off_owm_scale] * ldexpf(1.0f, e);
+    const float* __restrict__ b0 = P + a.off_ob0;
+    float4 out;
+    out.x = fmaf(g4[0], isc, o4[0]) + b0[0];
+    out.y = fmaf(g4[1], isc, o4[1]) + b0[1];
+    out.z = fmaf(g4[2], isc, o4[2]) + b0[2];
+    out.w = fmaf(g4[3], isc, o4[3]) + b0[3];
+    a.t1_next[((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
+    ps = (out.x + out.y) + (out.z + out.w);
+    pss = (out.x * out.x + out.y * out.y) + (out.z * out.z + out.w * out.w);
+  }
+  ps = wave_sum(ps);
+  pss = wave_sum(pss);
+  if (lane == 0) {
+    wsum[wave][0] = ps;
+    wsum[wave][1] = pss;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int w = 0; w < kMThreads / 64; ++w) {
+      s0 += wsum[w][0];
+      s1 += wsum[w][1];
+    }
+    stat_add(a.st_next + st_index(b, v, 0, nsrc), s0, s1);
+  }
+}
+
 // GN #STAGE (1 or 2) partial sums of the omega chain on t1 (plane d_next).
 template <int STAGE>
 __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
@@ -936,6 +1159,8 @@ static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspac
   a.off_ow0t = L.ow0t_off;
   a.off_owb = L.owb_off;
   a.off_owb_scale = L.owb_scale_off;
+  a.off_owm = L.owm_off;
+  a.off_owm_scale = L.owb_scale_off;
   a.off_ob0 = L.pk_off[P_OB0];
   a.off_og0w = L.pk_off[P_OG0W];
   a.off_og0b = L.pk_off[P_OG0B];
@@ -958,6 +1183,12 @@ static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspac
 static int pipe_box_cap() {
   const char* s = std::getenv("AARMVS_PIPE_BOX_CAP");
   return (s && *s) ? std::max(4, std::atoi(s)) : INT_MAX;
+}
+
+// omega conv variant: 2 (default) omega_mfma, 1 the VALU omega_conv (AARMVS_OMEGA=valu)
+static int omega_variant() {
+  const char* s = std::getenv("AARMVS_OMEGA");
+  return (s && std::strcmp(s, "valu") == 0) ? 1 : 2;
 }
 
 static PipeArgs pipe_args_c8(const CostArgs& ca, const SweepGeom& g, const Workspace& ws) {
@@ -992,11 +1223,17 @@ hipError_t launch_omega_next(const CostArgs& ca, const SweepGeom& g, const Works
   a.t1_next = reinterpret_cast<float4*>(ws.t1[d & 1]);
   a.st_next = ws.omega_stats[d & 1];
   hipError_t e;
-  {
+  if (omega_variant() == 1) {
     const int ntiles = ((g.W + kTileW - 1) / kTileW) * ((g.H + kTileH - 1) / kTileH);
     ProfScope ps(s, K_OMEGA_CONV);
     hipLaunchKernelGGL(omega_conv_kernel<kOmegaConvAbl>, dim3(ntiles * g.nsrc, 1, g.B), dim3(kTileThreads), 0, s, a,
                        a.params, a.rel);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  } else {
+    const int ntiles = ((g.W + kMOutW - 1) / kMOutW) * ((g.H + kMOutH - 1) / kMOutH);
+    ProfScope ps(s, K_OMEGA_CONV);
+    hipLaunchKernelGGL(omega_mfma_kernel, dim3(ntiles * g.nsrc, 1, g.B), dim3(kMThreads), 0, s, a,
+                       a.params, a.rel, ws.xbound);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // GN #1 / #2 statistics of plane d
