@@ -119,8 +119,11 @@ def homo_warp(src_fea: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor,
 # normalisation helpers
 # ----------------------------------------------------------------------------------
 def group_norm(x: torch.Tensor, groups: int, gamma: torch.Tensor, beta: torch.Tensor,
-               eps: float = GN_EPS) -> torch.Tensor:
-    """GroupNorm with biased variance over (C/G, H, W) per sample and group."""
+               eps: float = GN_EPS, fast: bool = False) -> torch.Tensor:
+    """GroupNorm with biased variance over (C/G, H, W) per sample and group.  ``fast`` calls
+    F.group_norm, the ATen kernel nn.GroupNorm (the reference) runs."""
+    if fast:
+        return F.group_norm(x, groups, gamma, beta, eps)
     B, C, H, W = x.shape
     xg = x.reshape(B, groups, -1)
     mean = xg.mean(dim=2, keepdim=True)
@@ -132,14 +135,14 @@ def group_norm(x: torch.Tensor, groups: int, gamma: torch.Tensor, beta: torch.Te
 # ----------------------------------------------------------------------------------
 # inter-view adaptive aggregation (omega)   drmvsnet.py:27-38
 # ----------------------------------------------------------------------------------
-def omega_weight(sq: torch.Tensor, P: dict) -> torch.Tensor:
+def omega_weight(sq: torch.Tensor, P: dict, fast: bool = False) -> torch.Tensor:
     k = "omega.reweight_network."
     a = F.conv2d(sq, P[k + "0.0.weight"], P[k + "0.0.bias"], padding=1)
-    a = F.relu(group_norm(a, 1, P[k + "0.1.weight"], P[k + "0.1.bias"]))
+    a = F.relu(group_norm(a, 1, P[k + "0.1.weight"], P[k + "0.1.bias"], fast=fast))
     t = F.conv2d(a, P[k + "1.stem.0.0.weight"], P[k + "1.stem.0.0.bias"])
-    t = F.relu(group_norm(t, 1, P[k + "1.stem.0.1.weight"], P[k + "1.stem.0.1.bias"]))
+    t = F.relu(group_norm(t, 1, P[k + "1.stem.0.1.weight"], P[k + "1.stem.0.1.bias"], fast=fast))
     t = F.conv2d(t, P[k + "1.stem.1.weight"], P[k + "1.stem.1.bias"])
-    t = group_norm(t, 1, P[k + "1.stem.2.weight"], P[k + "1.stem.2.bias"])
+    t = group_norm(t, 1, P[k + "1.stem.2.weight"], P[k + "1.stem.2.bias"], fast=fast)
     r = F.relu(t + a)                                                # ResnetBlockGn :262-263
     return torch.sigmoid(F.conv2d(r, P[k + "2.weight"], P[k + "2.bias"]))
 
@@ -149,7 +152,7 @@ def cost_slice(ref_fea, src_feas, rels, depth, P, fast: bool = False) -> torch.T
     acc = None
     for src, rel in zip(src_feas, rels):
         sq = (homo_warp(src, rel, depth, fast) - ref_fea).pow(2)
-        w = omega_weight(sq, P)
+        w = omega_weight(sq, P, fast)
         term = (w + 1) * sq
         acc = term if acc is None else acc + term
     return -1 * (acc / len(src_feas))
@@ -169,11 +172,11 @@ def lstm_cell(x, h, c, w, b):
     return h2, c2
 
 
-def deconv_gn_relu(x, P, name):
+def deconv_gn_relu(x, P, name, fast=False):
     k = "cost_regularization." + name + "."
     y = F.conv_transpose2d(x, P[k + "conv.weight"], P[k + "conv.bias"], stride=2,
                            padding=1, output_padding=1)
-    return F.relu(group_norm(y, 2, P[k + "gn.weight"], P[k + "gn.bias"]))
+    return F.relu(group_norm(y, 2, P[k + "gn.weight"], P[k + "gn.bias"], fast=fast))
 
 
 def init_state(B, H, W):
@@ -181,15 +184,15 @@ def init_state(B, H, W):
     return [(torch.zeros(B, *s), torch.zeros(B, *s)) for s in shapes]
 
 
-def unet_step(x, state, P):
+def unet_step(x, state, P, fast=False):
     """One depth step of UNetConvLSTM (process_sq branch), returns cost [B,1,H,W]."""
     cw = lambda i: (P[f"cost_regularization.cell_list.{i}.conv.weight"],
                     P[f"cost_regularization.cell_list.{i}.conv.bias"])
     h0, c0 = lstm_cell(x, *state[0], *cw(0))
     h1, c1 = lstm_cell(F.max_pool2d(h0, 2, 2), *state[1], *cw(1))
     h2, c2 = lstm_cell(F.max_pool2d(h1, 2, 2), *state[2], *cw(2))
-    h3, c3 = lstm_cell(torch.cat([deconv_gn_relu(h2, P, "deconv_0"), h1], 1), *state[3], *cw(3))
-    h4, c4 = lstm_cell(torch.cat([deconv_gn_relu(h3, P, "deconv_1"), h0], 1), *state[4], *cw(4))
+    h3, c3 = lstm_cell(torch.cat([deconv_gn_relu(h2, P, "deconv_0", fast), h1], 1), *state[3], *cw(3))
+    h4, c4 = lstm_cell(torch.cat([deconv_gn_relu(h3, P, "deconv_1", fast), h0], 1), *state[4], *cw(4))
     cost = F.conv2d(h4, P["cost_regularization.conv_0.weight"],
                     P["cost_regularization.conv_0.bias"], padding=1)
     return cost, [(h0, c0), (h1, c1), (h2, c2), (h3, c3), (h4, c4)]
@@ -222,7 +225,7 @@ def sweep(ref_fea, src_feas, ref_proj, src_projs, depth_values, P, planes=None,
         t0 = time.perf_counter()
         dv = depth_values[:, d].float()
         x = cost_slice(ref_fea.float(), [s.float() for s in src_feas], rels, dv, P, fast)
-        cost, state = unet_step(x, state, P)
+        cost, state = unet_step(x, state, P, fast)
         if want_volume:
             costs.append(cost)
         prob = torch.exp(cost.squeeze(1))                       # :324 (no max-subtraction)
