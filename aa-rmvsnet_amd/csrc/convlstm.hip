@@ -878,7 +878,10 @@ __global__ void __launch_bounds__(256) layout_kernel(const float* __restrict__ i
       const float q = __shfl_xor(mx, o, 64);
       mx = (q > mx || q != q) ? q : mx;
     }
-    if ((threadIdx.x & 63) == 0) atomicMax(xmax, __float_as_uint(mx != mx ? INFINITY : mx));
+    const unsigned bits = __float_as_uint(mx != mx ? INFINITY : mx);
+    if ((threadIdx.x & 63) == 0 &&
+        bits > __hip_atomic_load(xmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(xmax, bits);
   }
 }
 

@@ -1286,7 +1286,11 @@ __global__ void __launch_bounds__(256) nchw_to_c8_kernel(const float* __restrict
     float m = 0.f;
     for (int w = 0; w < 4; ++w) m = (wmax[w] > m || wmax[w] != wmax[w]) ? wmax[w] : m;
     const float bound = 8.0f * m * m;   // non-negative: float bits order like unsigned
-    atomicMax(xbound, __float_as_uint(bound != bound ? INFINITY : bound));
+    const unsigned bits = __float_as_uint(bound != bound ? INFINITY : bound);
+    // one address for the whole grid: read first, so that only blocks that raise the bound
+    // pay a (serialised) atomic
+    if (bits > __hip_atomic_load(xbound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(xbound, bits);
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {

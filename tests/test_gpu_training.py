@@ -108,7 +108,8 @@ def test_second_backward_through_freed_graph_raises():
     g1 = imgs.grad.clone()
     imgs.grad = None
     loss.backward()
-    assert torch.equal(g1, imgs.grad)
+    # the warp's backward scatters with fp32 atomics: equal up to summation order
+    torch.testing.assert_close(imgs.grad, g1, rtol=1e-5, atol=1e-6 * float(g1.abs().max()))
     with pytest.raises(RuntimeError):
         loss.backward()
 
