@@ -22,11 +22,15 @@ def child(H, W, N, out):
     proj = torch.from_numpy(sc["proj_matrices"])
     sw = ops.DepthSweep(P, dev)
     res = []
+    ops.profile_enable(True)
+    ops.profile_reset()
     for _ in range(2):
         x, om = sw.cost_slice(f[0], list(f[1:]), proj[:, 0], list(proj[:, 1:].unbind(1)),
                               torch.from_numpy(sc["depth_values"][:, 1].copy()), want_omega=True)
         torch.cuda.synchronize()
         res.append(om.cpu().numpy())
+    prof = ops.profile_read()
+    print("TIMING", {k: round(ms / n * 1e3, 1) for k, (n, ms) in prof.items()}, flush=True)
     np.save(out, np.stack(res))
 
 
@@ -36,15 +40,18 @@ if __name__ == "__main__":
         sys.exit(0)
     H, W, N = (int(v) for v in sys.argv[1:4])
     outs = {}
-    for var in ("valu", "mfma"):
-        env = dict(os.environ, AARMVS_OMEGA=var)
+    for var, extra in (("valu", {}), ("mfma", {}), ("mfma_global", {"AARMVS_PIPE_BOX_CAP": "4"})):
+        env = dict(os.environ, AARMVS_OMEGA=var.split("_")[0], **extra)
         p = f"/tmp/dbg_{var}.npy"
-        subprocess.run([sys.executable, __file__, "--child", str(H), str(W), str(N), p], env=env,
-                       check=True, timeout=300)
+        r = subprocess.run([sys.executable, __file__, "--child", str(H), str(W), str(N), p], env=env,
+                           check=True, timeout=300, capture_output=True, text=True)
+        print(var, [ln for ln in r.stdout.splitlines() if ln.startswith("TIMING")])
         outs[var] = np.load(p)
     for var, a in outs.items():
         print(var, "repeatable:", bool(np.array_equal(a[0], a[1])),
               "max run-to-run diff", float(np.abs(a[0] - a[1]).max()))
+    dg = np.abs(outs["valu"][0] - outs["mfma_global"][0])
+    print("max |valu - mfma_global|", float(dg.max()), "count > 1e-4:", int((dg > 1e-4).sum()))
     d = np.abs(outs["valu"][0] - outs["mfma"][0])   # [nsrc,1,H,W]
     print("max |valu - mfma|", float(d.max()), "mean", float(d.mean()))
     bad = np.argwhere(d > 1e-4)
