@@ -29,7 +29,7 @@ def child(planes, N, H, W, B):
     feats = torch.from_numpy(sc["features"]).to(dev)
     proj = torch.from_numpy(sc["proj_matrices"])
     dv = torch.from_numpy(sc["depth_values"])
-    sw = ops.DepthSweep(P, dev)
+    sw = ops.DepthSweep(P, dev, overlap=os.environ.get("AB_OVERLAP", "1") == "1")
     args = (feats[0], list(feats[1:]), proj[:, 0], list(proj[:, 1:].unbind(1)), dv)
     out = sw(*args, want_cost=True)
     torch.cuda.synchronize()
