@@ -13,7 +13,6 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
-#include <type_traits>
 
 #include "device_common.h"
 
@@ -893,25 +892,6 @@ constexpr int kOmegaConvAbl = 0;
 // sq is staged x 2^-e (e from the sweep's |x| bound, ws.xbound: sq <= 4 max|feature|^2
 // <= bound) so that fp16 cannot overflow; the weights carry their own power-of-two scale.
 // ---------------------------------------------------------------------------
-// Inline-asm LDS reads for omega_mfma's DMA pipeline: hipcc waits vmcnt(0) before any
-// compiler-visible LDS read while an LDS-DMA is in flight (it cannot tell the buffers
-// apart), which would drain the prefetched chunks.  These reads are invisible to that
-// analysis; lds_wait() retires them (lgkmcnt(0)) and ties the values so that their uses
-// stay below it.
-typedef float f4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint32_t lds_off(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ f4v lds_read16(uint32_t addr) {
-  f4v v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-__device__ __forceinline__ void lds_wait4(f4v& a, f4v& b, f4v& c, f4v& d) {
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
-}
-__device__ __forceinline__ float4 to_f4(f4v v) { return make_float4(v.x, v.y, v.z, v.w); }
-
 constexpr int kMTileH = 16, kMTileW = 32, kMThreads = kMTileH * kMTileW;   // haloed tile
 constexpr int kMOutH = kMTileH - 2, kMOutW = kMTileW - 2;                  // output tile
 constexpr int kMYStride = 36;                                               // floats per pixel in Y
@@ -921,14 +901,11 @@ __global__ void __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(
 omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restrict__ Rel,
                   const unsigned* __restrict__ xbound) {
   constexpr int NB = (2 * kMBoxPx + kMThreads - 1) / kMThreads;   // box pieces per thread
-  constexpr int BOXFL = (kMBoxPx + 1) * 8;                        // one box buffer (+ zero pixel)
   constexpr int YFL = kMThreads * kMYStride;                      // Y image floats
-  constexpr int BFL = 4 * 2 * 64 * 4;                             // B fragments (8 KB)
-  constexpr int SMF = YFL > 2 * BOXFL + BFL ? YFL : 2 * BOXFL + BFL;
-  static_assert(NB * kMThreads == 2 * kMBoxPx, "every lane issues NB pieces per chunk");
-  __shared__ __attribute__((aligned(16))) float smem[SMF];
-  float* const yimg = smem;   // Y image, over the box buffers and B once the chunks are done
-  half8* const bl = reinterpret_cast<half8*>(smem + 2 * BOXFL);   // [chunk][kind][lane]
+  static_assert(YFL >= (kMBoxPx + 1) * 8, "the box fits in the Y image space");
+  __shared__ __attribute__((aligned(16))) float smem[YFL];
+  float* const box = smem;   // chunk c's source box, then (after the last chunk) Y
+  float* const yimg = smem;
   __shared__ int red[kMThreads / 64][4];
   __shared__ float wsum[kMThreads / 64][2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -942,16 +919,13 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
   const bool in_img = gy >= 0 && gy < H && gx >= 0 && gx < W;
   const bool interior = in_img && hy >= 1 && hy <= kMOutH && hx >= 1 && hx <= kMOutW;
-  if (tid < 16) smem[(tid >> 3) * BOXFL + kMBoxPx * 8 + (tid & 7)] = 0.f;   // zero pixels
-  {   // the omega conv's B fragments (packed by pack_omega_conv_kernel) into LDS
-    const half8* __restrict__ owm = reinterpret_cast<const half8*>(P + a.off_owm);
-    bl[tid] = owm[tid];
-  }
+  if (tid < 8) box[kMBoxPx * 8 + tid] = 0.f;   // the zero pixel
 
   const float dep = a.dvals[b * a.D + a.d_next];
   const float* __restrict__ m = Rel + 12 * (v * a.B + b);
   const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);
   const uint32_t cbytes = (uint32_t)HW * 32u;
+  const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(a.ref + (size_t)b * kC * HW, fbytes);
   const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
   TapF tf{};
   int lx = INT_MAX, ly = INT_MAX, bhx = INT_MIN, bhy = INT_MIN;
@@ -965,24 +939,22 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   const TapP tp = tap_p(tf, in_img, H, W, lds, bx, zp);
   const int items = lds ? bx.nx * bx.ny * 2 : 0;
   const uint32_t mg = box_magic(bx.nx);
-  // chunk-0 byte offsets of this lane's DMA pieces; pieces past the box read past the
-  // buffer (zeros into unused box slots), so that every wave issues exactly NB DMA
-  // instructions per chunk and the pipeline's vmcnt waits are static
   uint32_t boff[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int i = tid + j * kMThreads, p = i >> 1, r = box_row(p, bx.nx, mg);
     const uint32_t gp = __umul24((uint32_t)(bx.y0 + r), (uint32_t)W) + (uint32_t)bx.x0 +
                         ((uint32_t)p - __umul24((uint32_t)r, (uint32_t)bx.nx));
-    boff[j] = i < items ? gp * 32u + 16u * (uint32_t)img_half((uint32_t)p, i & 1) : 0xFFFFFFF0u;
+    boff[j] = gp * 32u + 16u * (uint32_t)img_half((uint32_t)p, i & 1);
   }
-  auto stage = [&](int c) {   // chunk c's box into buffer c & 1 (NB DMA instructions)
+  auto stage = [&](int c) {
     const uint32_t cb = (uint32_t)c * cbytes;
-    float* const dst = smem + (c & 1) * BOXFL;
 #pragma unroll
     for (int j = 0; j < NB; ++j)
-      dma16(rsrc, dst + (j * kMThreads + wave * 64) * 4, boff[j] == 0xFFFFFFF0u ? fbytes : boff[j] + cb);
+      if (tid + j * kMThreads < items) dma16(rsrc, box + (j * kMThreads + wave * 64) * 4, boff[j] + cb);
   };
+  // this lane's reference pixel in the c8 image (past the buffer: zeros)
+  const uint32_t rpix = in_img ? (uint32_t)(gy * W + gx) : fbytes / 32u;
   // sq guard: sq 2^-e <= 2^15 (sq <= 4 max|f|^2 <= bound)
   int e = 0;
   {
@@ -994,128 +966,80 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   }
   const float sqs = ldexpf(1.0f, -e);
   const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]: centre tap = tap 4
-  // this lane's reference pixel (the c8 image; lanes outside the image read pixel 0: their
-  // sq is masked) through inline-asm loads: the compiler would otherwise drain the box
-  // DMAs (vmcnt(0)) at their first use; the pipeline's counted waits cover them
-  const float* const rbase = a.ref + (size_t)b * kC * HW +
-                             (size_t)(in_img ? gy * W + gx : 0) * 8;
-  auto ref_load = [&](int c, float4& r0, float4& r1) {
-    const float* p = rbase + (size_t)c * HW * 8;
-    asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:16"
-                 : "=&v"(r0), "=&v"(r1) : "v"(p) : "memory");
-  };
+  const half8* __restrict__ owm = reinterpret_cast<const half8*>(P + a.off_owm);
   floatx16 acc0, acc1;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
   float o4[4] = {0.f, 0.f, 0.f, 0.f};
 
-  // pipeline (LDS path): DMA(c + 2) is issued once every lane has sampled chunk c, so two
-  // chunks are in flight while one is sampled.  VMEM order per iteration c: B(c) [2],
-  // ref(c + 1) [2], DMA(c + 2) [NB]; at the top of iteration c everything but DMA(c + 1)
-  // must have landed: vmcnt(NB) while a DMA(c + 1) exists, else vmcnt(0).
-  __syncthreads();   // B fragments and zero pixels in LDS (no DMA in flight yet)
-  // one loop per path (LDS box or global gathers), so that the global path's loads do not
-  // enter the LDS loop's wait bookkeeping
-  auto chunks = [&](auto LDSc) {
-    constexpr bool LDS = decltype(LDSc)::value;
-    float4 rf0, rf1;
-    if (LDS) stage(0);
-    ref_load(0, rf0, rf1);
-    if (LDS) stage(1);
+  stage(0);
+  float4 rf0 = ld_c8(rref, rpix, 0, HW), rf1 = ld_c8(rref, rpix, 1, HW);
+  dma_wait();
+  __syncthreads();
 #pragma unroll 1
-    for (int c = 0; c < 4; ++c) {
-      // vmcnt(NB): everything but DMA(c + 1) has landed (DMA(c), ref(c)); the asm names the
-      // reference registers so that their uses stay below the wait
-      if (LDS && c < 3)
-        asm volatile("s_waitcnt vmcnt(%8)"
-                     : "+v"(rf0.x), "+v"(rf0.y), "+v"(rf0.z), "+v"(rf0.w), "+v"(rf1.x), "+v"(rf1.y),
-                       "+v"(rf1.z), "+v"(rf1.w)
-                     : "n"(NB) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)"
-                     : "+v"(rf0.x), "+v"(rf0.y), "+v"(rf0.z), "+v"(rf0.w), "+v"(rf1.x), "+v"(rf1.y),
-                       "+v"(rf1.z), "+v"(rf1.w)
-                     : : "memory");
-      if (LDS) asm volatile("s_barrier" ::: "memory");   // chunk c's box visible to every lane
-      const uint32_t boxa = lds_off(smem + (c & 1) * BOXFL);
-      f4v bd, bo;   // B fragments of chunk c: [W_hi; W_hi] and [W_lo; 0]
-      // sample the own pixel (8 channels) and form sq
-      float4 g0, g1;
-      if constexpr (LDS) {
-        f4v t0 = lds_read16(boxa + 4u * img_slot(tp.pix[0], 0));
-        f4v t1 = lds_read16(boxa + 4u * img_slot(tp.pix[1], 0));
-        f4v t2 = lds_read16(boxa + 4u * img_slot(tp.pix[2], 0));
-        f4v t3 = lds_read16(boxa + 4u * img_slot(tp.pix[3], 0));
-        lds_wait4(t0, t1, t2, t3);
-        g0 = bil4(to_f4(t0), to_f4(t1), to_f4(t2), to_f4(t3), tp);
-        t0 = lds_read16(boxa + 4u * img_slot(tp.pix[0], 1));
-        t1 = lds_read16(boxa + 4u * img_slot(tp.pix[1], 1));
-        t2 = lds_read16(boxa + 4u * img_slot(tp.pix[2], 1));
-        t3 = lds_read16(boxa + 4u * img_slot(tp.pix[3], 1));
-        bd = lds_read16(lds_off(bl + (c * 2 + 0) * 64 + lane));
-        bo = lds_read16(lds_off(bl + (c * 2 + 1) * 64 + lane));
-        lds_wait4(t0, t1, t2, t3);
-        lds_wait4(bd, bo, bd, bo);
-        g1 = bil4(to_f4(t0), to_f4(t1), to_f4(t2), to_f4(t3), tp);
-      } else {
-        bd = lds_read16(lds_off(bl + (c * 2 + 0) * 64 + lane));
-        bo = lds_read16(lds_off(bl + (c * 2 + 1) * 64 + lane));
-        lds_wait4(bd, bo, bd, bo);
-        g0 = bil4(ld_c8(rsrc, tp.pix[0], 2 * c, HW), ld_c8(rsrc, tp.pix[1], 2 * c, HW),
-                  ld_c8(rsrc, tp.pix[2], 2 * c, HW), ld_c8(rsrc, tp.pix[3], 2 * c, HW), tp);
-        g1 = bil4(ld_c8(rsrc, tp.pix[0], 2 * c + 1, HW), ld_c8(rsrc, tp.pix[1], 2 * c + 1, HW),
-                  ld_c8(rsrc, tp.pix[2], 2 * c + 1, HW), ld_c8(rsrc, tp.pix[3], 2 * c + 1, HW), tp);
-      }
-      const float4 s0 = sqdiff4(g0, rf0), s1 = sqdiff4(g1, rf1);
-      const float sq[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-      if (c < 3) ref_load(c + 1, rf0, rf1);   // the next chunk's reference pixel
-      if (LDS && c < 2) {
-        // every lane's reads of buffer c & 1 are done (retired by lds_wait4): refill it
-        asm volatile("s_barrier" ::: "memory");
-        stage(c + 2);
-      }
-      // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel, fp32
-      {
-        const float* wt = w0t + (4 * kC + 8 * c) * 4;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int co = 0; co < 4; ++co) o4[co] = fmaf(sq[j], wt[j * 4 + co], o4[co]);
-      }
-      // split sq 2^-e into fp16 hi + lo (out-of-image pixels: the conv's zero padding)
-      uint32_t hw[4], lw[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p0 = in_img ? sq[2 * i] * sqs : 0.f, p1 = in_img ? sq[2 * i + 1] * sqs : 0.f;
-        const _Float16 h0 = (_Float16)p0, h1 = (_Float16)p1;
-        const half2_t hv = {h0, h1};
-        const half2_t lv = {(_Float16)(p0 - (float)h0), (_Float16)(p1 - (float)h1)};
-        hw[i] = __builtin_bit_cast(uint32_t, hv);
-        lw[i] = __builtin_bit_cast(uint32_t, lv);
-      }
-      // lanes 0-31 / 32-63 hold rows 2w / 2w+1: after the swaps, (hw, lw) are the A operands
-      // of row 2w (lanes 0-31 hi, 32-63 lo of pixel lane & 31) and of row 2w+1
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const auto r = __builtin_amdgcn_permlane32_swap(hw[i], lw[i], false, false);
-        hw[i] = r[0];
-        lw[i] = r[1];
-      }
-      const half8 A0 = __builtin_bit_cast(half8, u32x4{hw[0], hw[1], hw[2], hw[3]});
-      const half8 A1 = __builtin_bit_cast(half8, u32x4{lw[0], lw[1], lw[2], lw[3]});
-      const half8 Bd = __builtin_bit_cast(half8, bd), Bl = __builtin_bit_cast(half8, bo);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl, acc1, 0, 0, 0);
+  for (int c = 0; c < 4; ++c) {
+    // sample the own pixel (8 channels) and form sq
+    float4 g0, g1;
+    if (lds) {
+      g0 = bil4(img_ld(box, tp.pix[0], 0), img_ld(box, tp.pix[1], 0), img_ld(box, tp.pix[2], 0),
+                img_ld(box, tp.pix[3], 0), tp);
+      g1 = bil4(img_ld(box, tp.pix[0], 1), img_ld(box, tp.pix[1], 1), img_ld(box, tp.pix[2], 1),
+                img_ld(box, tp.pix[3], 1), tp);
+    } else {
+      g0 = bil4(ld_c8(rsrc, tp.pix[0], 2 * c, HW), ld_c8(rsrc, tp.pix[1], 2 * c, HW),
+                ld_c8(rsrc, tp.pix[2], 2 * c, HW), ld_c8(rsrc, tp.pix[3], 2 * c, HW), tp);
+      g1 = bil4(ld_c8(rsrc, tp.pix[0], 2 * c + 1, HW), ld_c8(rsrc, tp.pix[1], 2 * c + 1, HW),
+                ld_c8(rsrc, tp.pix[2], 2 * c + 1, HW), ld_c8(rsrc, tp.pix[3], 2 * c + 1, HW), tp);
     }
-  };
-  if (lds)
-    chunks(std::integral_constant<bool, true>{});
-  else
-    chunks(std::integral_constant<bool, false>{});
-  __syncthreads();   // chunk 3's box reads are done: Y goes over the box buffers
-  // Y image: D[row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)][col = lane & 31] of row group g
+    const float4 s0 = sqdiff4(g0, rf0), s1 = sqdiff4(g1, rf1);
+    const float sq[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    if (c < 3) {   // the next chunk's reference pixel, in flight during this chunk
+      rf0 = ld_c8(rref, rpix, 2 * c + 2, HW);
+      rf1 = ld_c8(rref, rpix, 2 * c + 3, HW);
+    }
+    __syncthreads();   // every lane's box reads of chunk c are done
+    if (c < 3) stage(c + 1);
+    // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel, fp32
+    {
+      const float* wt = w0t + (4 * kC + 8 * c) * 4;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int co = 0; co < 4; ++co) o4[co] = fmaf(sq[j], wt[j * 4 + co], o4[co]);
+    }
+    // split sq 2^-e into fp16 hi + lo (out-of-image pixels: the conv's zero padding)
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p0 = in_img ? sq[2 * i] * sqs : 0.f, p1 = in_img ? sq[2 * i + 1] * sqs : 0.f;
+      const _Float16 h0 = (_Float16)p0, h1 = (_Float16)p1;
+      const half2_t hv = {h0, h1};
+      const half2_t lv = {(_Float16)(p0 - (float)h0), (_Float16)(p1 - (float)h1)};
+      hw[i] = __builtin_bit_cast(uint32_t, hv);
+      lw[i] = __builtin_bit_cast(uint32_t, lv);
+    }
+    // lanes 0-31 / 32-63 hold rows 2w / 2w+1: after the swaps, (hw, lw) are the A operands
+    // of row 2w (lanes 0-31 hi, 32-63 lo of pixel lane & 31) and of row 2w+1
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane32_swap(hw[i], lw[i], false, false);
+      hw[i] = r[0];
+      lw[i] = r[1];
+    }
+    const half8 A0 = __builtin_bit_cast(half8, u32x4{hw[0], hw[1], hw[2], hw[3]});
+    const half8 A1 = __builtin_bit_cast(half8, u32x4{lw[0], lw[1], lw[2], lw[3]});
+    const half8 Bd = owm[(c * 2 + 0) * 64 + lane], Bl = owm[(c * 2 + 1) * 64 + lane];
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl, acc1, 0, 0, 0);
+    if (c < 3) {
+      dma_wait();
+      __syncthreads();   // chunk c+1's box visible
+    }
+  }
+  // Y image (over the box space: every lane passed chunk 3's box reads before the barrier
+  // above): D[row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)][col = lane & 31] of row group g
   {
     const int col = lane & 31, rb = 4 * (lane >> 5);
 #pragma unroll
@@ -1261,10 +1185,12 @@ static int pipe_box_cap() {
   return (s && *s) ? std::max(4, std::atoi(s)) : INT_MAX;
 }
 
-// omega conv variant: 2 (default) omega_mfma, 1 the VALU omega_conv (AARMVS_OMEGA=valu)
+// omega conv variant: 1 (default) the VALU omega_conv, 2 omega_mfma (AARMVS_OMEGA=mfma):
+// parity-green and deterministic, 713 vs 748 us per plane at the headline (one A/B on one
+// box), but the round-2 pipelined form of it did not pay off; kept opt-in
 static int omega_variant() {
   const char* s = std::getenv("AARMVS_OMEGA");
-  return (s && std::strcmp(s, "valu") == 0) ? 1 : 2;
+  return (s && std::strcmp(s, "mfma") == 0) ? 2 : 1;
 }
 
 static PipeArgs pipe_args_c8(const CostArgs& ca, const SweepGeom& g, const Workspace& ws) {
