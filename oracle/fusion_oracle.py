@@ -171,3 +171,57 @@ def synthetic_views(H, W, nsrc, seed=0):
         depths.append(d)
     conf = rng.random((H, W)).astype(np.float32)
     return depths, cams, conf
+
+
+def filter_depth_scan(pair_data, images, cam_texts, depth_ests, confidences, photo_threshold):
+    """fusion.py:135-273 on in-memory inputs: pair_data [(ref, [src...])], images {view: float32
+    [H,W,3] in [0,1]}, cam_texts {view: cam.txt text}, depth_ests / confidences {view: float32
+    [h,w]} (views without a depth map are skipped).  Returns (masks {ref: (photo, geo, final)},
+    xyz float32 [n,3], rgb uint8 [n,3]).  The image rescale is the identity here (the tests
+    use scale 1: cv2 is absent, its INTER_LINEAR resize is parity unpinned)."""
+    def cam(text, scale, index, flag):                       # fusion.py:27-42
+        lines = [ln.rstrip() for ln in text.splitlines()]
+        E = np.array(" ".join(lines[1:5]).split(), dtype=np.float32).reshape((4, 4))
+        K = np.array(" ".join(lines[7:10]).split(), dtype=np.float32).reshape((3, 3))
+        K[:2, :] *= scale
+        if flag == 0:
+            K[0, 2] -= index
+        else:
+            K[1, 2] -= index
+        return K, E
+
+    masks, verts, cols = {}, [], []
+    for ref_view, src_views in pair_data:
+        if ref_view not in depth_ests:
+            continue
+        ref_img = images[ref_view]
+        ref_depth = depth_ests[ref_view]
+        conf = confidences[ref_view]
+        scale = float(conf.shape[0]) / ref_img.shape[0]       # fusion.py:157-171
+        index = int((int(ref_img.shape[1] * scale) - conf.shape[1]) / 2)
+        index_p = (int(ref_img.shape[1] * scale) - conf.shape[1]) - index
+        flag = 0
+        if conf.shape[1] / ref_img.shape[1] > scale:
+            scale = float(conf.shape[1]) / ref_img.shape[1]
+            index = int((int(ref_img.shape[0] * scale) - conf.shape[0]) / 2)
+            index_p = (int(ref_img.shape[0] * scale) - conf.shape[0]) - index
+            flag = 1
+        assert (int(ref_img.shape[1] * scale), int(ref_img.shape[0] * scale)) == ref_img.shape[1::-1]
+        if flag == 0:
+            ref_img = ref_img[:, index:ref_img.shape[1] - index_p, :]
+        else:
+            ref_img = ref_img[index:ref_img.shape[0] - index_p, :, :]
+        ref_cam = cam(cam_texts[ref_view], scale, index, flag)
+        src_d = [depth_ests[s] for s in src_views]
+        src_c = [cam(cam_texts[s], scale, index, flag) for s in src_views]
+        photo, geo, final, avg = filter_depth_core(ref_depth, conf, ref_cam, src_d, src_c, photo_threshold)
+        masks[ref_view] = (photo, geo, final)
+        h, w = avg.shape                                       # fusion.py:246-257
+        x, y = np.meshgrid(np.arange(0, w), np.arange(0, h))
+        x, y, depth = x[final], y[final], avg[final]
+        color = ref_img[final]
+        xyz_ref = np.matmul(np.linalg.inv(ref_cam[0]), np.vstack((x, y, np.ones_like(x))) * depth)
+        xyz_world = np.matmul(np.linalg.inv(ref_cam[1]), np.vstack((xyz_ref, np.ones_like(x))))[:3]
+        verts.append(xyz_world.transpose((1, 0)))
+        cols.append((color * 255).astype(np.uint8))
+    return masks, np.concatenate(verts).astype(np.float32), np.concatenate(cols)

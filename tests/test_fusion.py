@@ -132,3 +132,76 @@ def test_gpu_filter_rejects_bad_input():
     with pytest.raises(AarmvsError):
         fusion.filter_depth_core(torch.from_numpy(depths[0]), torch.from_numpy(conf), cams[0],
                                  [torch.from_numpy(d) for d in depths[1:]], cams[1:], 0.35)
+
+
+def test_crop_params_and_resize_identity():
+    # DTU eval: 1200x1600 images, 1184x1600 depth maps -> scale 1, crop 8 rows top and bottom
+    assert fusion.crop_params((1200, 1600), (1184, 1600)) == (1.0, 8, 8, 1)
+    # a 2x downscale that crops columns
+    s, i, ip, f = fusion.crop_params((600, 820), (300, 400))
+    assert (s, i, ip, f) == (0.5, 5, 5, 0)
+    img = np.random.default_rng(0).random((6, 8, 3)).astype(np.float32)
+    np.testing.assert_array_equal(fusion.resize_linear(img, 8, 6), img)
+    half = fusion.resize_linear(img, 4, 3)                  # INTER_AREA path: 2x2 means
+    np.testing.assert_allclose(half[1, 2], img[2:4, 4:6].mean((0, 1)), rtol=1e-6)
+    up = fusion.resize_linear(img[:, :, 0], 16, 12)          # bilinear, clamped borders
+    assert up.shape == (12, 16) and up[0, 0] == img[0, 0, 0] and up[-1, -1] == img[-1, -1, 0]
+
+
+def _write_scan(root, H, W, nsrc, pad):
+    """A scan folder in the DTU layout: pair.txt, cams/, images/ (pad extra rows top and
+    bottom: the driver's crop), depth_est_0/ and confidence_0/ PFMs."""
+    from PIL import Image
+    depths, cams, conf = fo.synthetic_views(H, W, nsrc, seed=11)
+    n = nsrc + 1
+    scan, out = root / "scan1", root / "out"
+    for d in ("cams", "images"):
+        (scan / d).mkdir(parents=True, exist_ok=True)
+    for d in ("depth_est_0", "confidence_0"):
+        (out / d).mkdir(parents=True, exist_ok=True)
+    rng = np.random.default_rng(3)
+    pair, images, cam_texts, dmaps, confs = [], {}, {}, {}, {}
+    for v in range(n):
+        K, E = cams[v]
+        K = K.copy()
+        K[1, 2] += pad                      # the image has pad more rows above the crop
+        txt = ("extrinsic\n" + "\n".join(" ".join(repr(float(q)) for q in row) for row in E)
+               + "\n\nintrinsic\n" + "\n".join(" ".join(repr(float(q)) for q in row) for row in K)
+               + "\n\n425 2.5\n")
+        (scan / "cams" / "{:0>8}_cam.txt".format(v)).write_text(txt)
+        cam_texts[v] = txt
+        img = (rng.random((H + 2 * pad, W, 3)) * 255).astype(np.uint8)
+        Image.fromarray(img).save(str(scan / "images" / "{:0>8}.jpg".format(v)), format="PNG")
+        images[v] = np.array(Image.open(str(scan / "images" / "{:0>8}.jpg".format(v))), np.float32) / 255.0
+        cv = np.roll(conf, 7 * v, axis=1) if v else conf
+        fusion.save_pfm(str(out / "depth_est_0" / "{:0>8}.pfm".format(v)), depths[v])
+        fusion.save_pfm(str(out / "confidence_0" / "{:0>8}.pfm".format(v)), cv)
+        dmaps[v], confs[v] = depths[v], cv
+        pair.append((v, [s for s in range(n) if s != v]))
+    with open(scan / "pair.txt", "w") as f:
+        f.write(f"{n}\n")
+        for v, srcs in pair:
+            f.write(f"{v}\n{len(srcs)} " + " ".join(f"{s} {9.0 - s:.1f}" for s in srcs) + "\n")
+    return scan, out, (pair, images, cam_texts, dmaps, confs)
+
+
+@pytest.mark.gpu
+def test_gpu_filter_depth_scan_matches_oracle(tmp_path):
+    """The per-scan driver (fusion.py:135-273): image crop and camera re-centring, the masks
+    of every reference view (PNG files) and the scan's PLY, bit-exact vs the oracle."""
+    from PIL import Image
+    scan, out, (pair, images, cam_texts, dmaps, confs) = _write_scan(tmp_path, 48, 64, 3, 4)
+    ply = tmp_path / "scan1.ply"
+    npts = fusion.filter_depth(str(scan), str(out), str(ply), 0.35)
+    masks, xyz, rgb = fo.filter_depth_scan(pair, images, cam_texts, dmaps, confs, 0.35)
+    assert npts == xyz.shape[0] > 0
+    for v, (photo, geo, final) in masks.items():
+        for name, m in (("photo", photo), ("geo", geo), ("final", final)):
+            png = np.array(Image.open(str(out / "mask" / "{:0>8}_{}.png".format(v, name))))
+            np.testing.assert_array_equal(png, m.astype(np.uint8) * 255)
+    head, body = ply.read_bytes().split(b"end_header\n", 1)
+    assert f"element vertex {npts}".encode() in head
+    v = np.frombuffer(body, dtype=[("x", "<f4"), ("y", "<f4"), ("z", "<f4"),
+                                   ("red", "u1"), ("green", "u1"), ("blue", "u1")])
+    np.testing.assert_array_equal(np.stack([v["x"], v["y"], v["z"]], 1), xyz)
+    np.testing.assert_array_equal(np.stack([v["red"], v["green"], v["blue"]], 1), rgb)
