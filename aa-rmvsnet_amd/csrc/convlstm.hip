@@ -15,6 +15,9 @@
 // the deconv outputs) is NHWC, [B][H][W][C] fp32.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -392,7 +395,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
   using D = typename C::D;
-  constexpr int MT = C::MT, HID = C::HID, NCHK = C::NCHK;
+  constexpr int MT = C::MT, NCHK = C::NCHK;
   extern __shared__ __attribute__((aligned(16))) char lds_h3[];
   char* wl_hi = lds_h3;
   char* wl_lo = wl_hi + C::A_HALVES * 2;
@@ -491,7 +494,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
   using D = typename C::D;
-  constexpr int MT = C::MT, HID = C::HID, NCHK = C::NCHK;
+  constexpr int MT = C::MT, NCHK = C::NCHK;
   constexpr int PB = C::NPIX * 32;   // one plane (hi or lo) of one input buffer
   static_assert(NCHK >= 2, "two or more input chunks");
   extern __shared__ __attribute__((aligned(16))) char lds_h3[];
@@ -622,106 +625,92 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
 }
 
 // ---------------------------------------------------------------------------
-// deConvGnReLU's transposed conv (module.py:281): ConvTranspose2d(16,16,3,s2,p1,op1).
-// One thread per input pixel produces its 2x2 output quad (uniform weight taps), plus
-// GroupNorm(2,16) partial sums (the GN+ReLU itself is fused into the consuming cell's
-// input staging).  A block takes a 256-pixel segment of an input row: the segment and
-// the one below (+ the right neighbour) are staged in LDS from contiguous NHWC runs
-// (channel stride 17: conflict-free per-channel reads), and each output row segment is
-// assembled in LDS and written back as one contiguous run.
+// deConvGnReLU's transposed conv (module.py:281): ConvTranspose2d(16,16,3,s2,p1,op1), plus
+// GroupNorm(2,16) partial sums (the GN+ReLU itself is fused into the consuming cell's input
+// staging).
 // ---------------------------------------------------------------------------
-constexpr int kDcTW = 256;    // input pixels per block
-constexpr int kDcOut = 20;    // LDS floats per output pixel (16 + 4 pad: 2-way writes)
-__global__ void __launch_bounds__(256) deconv_kernel(const float* __restrict__ in,
-                                                     const float* __restrict__ w,
-                                                     const float* __restrict__ bias, int Hi,
-                                                     int Wi, float* __restrict__ out,
-                                                     double* __restrict__ stats) {
-  __shared__ float tin[2][kDcTW + 1][17];
-  __shared__ __attribute__((aligned(16))) float tout[2 * kDcTW * kDcOut];
+// deconv_px: one thread per input pixel of an 8 x 32 tile (its 2 x 2 output quad, uniform
+// weight taps) and all batch elements in one launch.  The tile and its bottom / right neighbours (9 x 33 px, 19
+// KB) are staged once in LDS channel-major; each thread accumulates its 2 x 2 output quad's
+// 64 values and stores the quad straight to NHWC (each thread's two 128-B output row runs are
+// completed by its own eight 16-B stores).  The round-1 form staged 2 input rows and 2
+// output rows of a 256-pixel segment in 76 KB of LDS (2 blocks per CU, 3 barriers per
+// segment, a partial last segment per row): 84 / 47 us per plane at the headline geometry
+// against 71 / 37 us here (profiles/r02_*).
+constexpr int kDpTH = 8, kDpTW = 32;
+__global__ void __launch_bounds__(256) deconv_px_kernel(const float* __restrict__ in,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bias, int Hi,
+                                                        int Wi, float* __restrict__ out,
+                                                        double* __restrict__ stats,
+                                                        int stats_bstride) {
+  constexpr int SH = kDpTH + 1, SW = kDpTW + 1;   // the tile + its bottom / right neighbours
+  __shared__ float tin[16][SH][SW];               // [ci][y][x] (row stride 33: conflict-free)
   __shared__ float red[4 * 4];
-  const int b = blockIdx.y, tid = threadIdx.x;
+  const int b = blockIdx.z, tid = threadIdx.x;
+  const int y0 = blockIdx.y * kDpTH, x0 = blockIdx.x * kDpTW;
+  const int ty = tid / kDpTW, tx = tid % kDpTW;
+  const int iy = y0 + ty, ix = x0 + tx;
   const int Wo = 2 * Wi;
+  const bool ok = iy < Hi && ix < Wi;
   const float* ib = in + (size_t)b * 16 * Hi * Wi;
-  float* ob = out + (size_t)b * 16 * 4 * Hi * Wi;
-  const int segs = (Wi + kDcTW - 1) / kDcTW;
-  float part[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int t = blockIdx.x; t < Hi * segs; t += gridDim.x) {
-    const int iy = t / segs, x0 = (t % segs) * kDcTW, n = min(kDcTW, Wi - x0);
-    __syncthreads();   // the previous segment's LDS reads are done
-    for (int i = tid; i < 2 * (kDcTW + 1) * 4; i += 256) {
-      const int r = i / ((kDcTW + 1) * 4), rem = i % ((kDcTW + 1) * 4);
-      const int px = rem >> 2, c4 = rem & 3;
-      const int gy = iy + r, gx = x0 + px;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);   // zero padding past the image
-      if (px <= n && gy < Hi && gx < Wi)
-        v = *reinterpret_cast<const float4*>(ib + ((size_t)gy * Wi + gx) * 16 + 4 * c4);
-      float* d = &tin[r][px][4 * c4];
-      d[0] = v.x;
-      d[1] = v.y;
-      d[2] = v.z;
-      d[3] = v.w;
-    }
-    __syncthreads();
-    const int lp = tid;
-    float o[4][16];
+  // stage: 16-B pieces (4 channels of one pixel), channel group fastest (coalesced NHWC)
+  for (int i = tid; i < SH * SW * 4; i += 256) {
+    const int c4 = i & 3, px = i >> 2, yy = px / SW, xx = px - yy * SW;
+    const int gy = y0 + yy, gx = x0 + xx;
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);   // zero padding past the image
+    if (gy < Hi && gx < Wi) q = *reinterpret_cast<const float4*>(ib + ((size_t)gy * Wi + gx) * 16 + 4 * c4);
+    tin[4 * c4 + 0][yy][xx] = q.x;
+    tin[4 * c4 + 1][yy][xx] = q.y;
+    tin[4 * c4 + 2][yy][xx] = q.z;
+    tin[4 * c4 + 3][yy][xx] = q.w;
+  }
+  __syncthreads();
+  float o[4][16];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int co = 0; co < 16; ++co) o[q][co] = 0.f;
-    if (lp < n) {
-      // one input channel per iteration (its 144 weights are scalar loads)
+    for (int co = 0; co < 16; ++co) o[q][co] = 0.f;
+  // one input channel per iteration (its 144 weights are scalar loads)
 #pragma unroll 1
-      for (int ci = 0; ci < 16; ++ci) {
-        const float v00 = tin[0][lp][ci], v01 = tin[0][lp + 1][ci];
-        const float v10 = tin[1][lp][ci], v11 = tin[1][lp + 1][ci];
-        const float* wc = w + ci * 9 * 16;   // [ci][tap][co] (pack_deconv_kernel)
+  for (int ci = 0; ci < 16; ++ci) {
+    const float v00 = tin[ci][ty][tx], v01 = tin[ci][ty][tx + 1];
+    const float v10 = tin[ci][ty + 1][tx], v11 = tin[ci][ty + 1][tx + 1];
+    const float* wc = w + ci * 9 * 16;   // [ci][tap][co] (pack_deconv_kernel)
 #pragma unroll
-        for (int co = 0; co < 16; ++co) {
-          auto k = [&](int tap) { return wc[tap * 16 + co]; };
-          // out(2iy,2ix): (ky,kx)=(1,1) from (iy,ix)
-          o[0][co] = fmaf(v00, k(4), o[0][co]);
-          // out(2iy,2ix+1): kx=2 from ix, kx=0 from ix+1 (ky=1)
-          o[1][co] = fmaf(v00, k(5), fmaf(v01, k(3), o[1][co]));
-          // out(2iy+1,2ix): ky=2 from iy, ky=0 from iy+1 (kx=1)
-          o[2][co] = fmaf(v00, k(7), fmaf(v10, k(1), o[2][co]));
-          // out(2iy+1,2ix+1)
-          o[3][co] = fmaf(v00, k(8), fmaf(v01, k(6), fmaf(v10, k(2), fmaf(v11, k(0), o[3][co]))));
-        }
-      }
+    for (int co = 0; co < 16; ++co) {
+      auto k = [&](int tap) { return wc[tap * 16 + co]; };
+      o[0][co] = fmaf(v00, k(4), o[0][co]);
+      o[1][co] = fmaf(v00, k(5), fmaf(v01, k(3), o[1][co]));
+      o[2][co] = fmaf(v00, k(7), fmaf(v10, k(1), o[2][co]));
+      o[3][co] = fmaf(v00, k(8), fmaf(v01, k(6), fmaf(v10, k(2), fmaf(v11, k(0), o[3][co]))));
     }
+  }
+  float part[4] = {0.f, 0.f, 0.f, 0.f};
+  if (ok) {
+    float* ob = out + (size_t)b * 16 * 4 * Hi * Wi;
 #pragma unroll
-    for (int ry = 0; ry < 2; ++ry) {
-      if (lp < n) {
+    for (int q = 0; q < 4; ++q) {
+      float4* d = reinterpret_cast<float4*>(ob + ((size_t)(2 * iy + (q >> 1)) * Wo + 2 * ix + (q & 1)) * 16);
 #pragma unroll
-        for (int dxo = 0; dxo < 2; ++dxo) {
-          float4* d = reinterpret_cast<float4*>(&tout[(2 * lp + dxo) * kDcOut]);
+      for (int c4 = 0; c4 < 4; ++c4) {
+        float r[4];
 #pragma unroll
-          for (int c4 = 0; c4 < 4; ++c4) {
-            float r[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int co = 4 * c4 + u;
-              r[u] = o[2 * ry + dxo][co] + bias[co];
-              part[(co >> 3) * 2] += r[u];
-              part[(co >> 3) * 2 + 1] += r[u] * r[u];
-            }
-            d[c4] = make_float4(r[0], r[1], r[2], r[3]);
-          }
+        for (int u = 0; u < 4; ++u) {
+          const int co = 4 * c4 + u;
+          r[u] = o[q][co] + bias[co];
+          part[(co >> 3) * 2] += r[u];
+          part[(co >> 3) * 2 + 1] += r[u] * r[u];
         }
+        d[c4] = make_float4(r[0], r[1], r[2], r[3]);
       }
-      __syncthreads();
-      // output row 2 iy + ry, pixels 2 x0 .. 2 (x0 + n) - 1: one contiguous run
-      float4* orow = reinterpret_cast<float4*>(ob + ((size_t)(2 * iy + ry) * Wo + 2 * x0) * 16);
-      for (int j = tid; j < 2 * n * 4; j += 256)
-        orow[j] = *reinterpret_cast<const float4*>(&tout[(j >> 2) * kDcOut + 4 * (j & 3)]);
-      __syncthreads();
     }
   }
   block_sum<4>(part, red);
-  if (threadIdx.x == 0) {
-    stat_add(stats, part[0], part[1]);
-    stat_add(stats + kSlots * 2, part[2], part[3]);
+  if (tid == 0) {
+    double* st = stats + (size_t)b * stats_bstride;
+    stat_add(st, part[0], part[1]);
+    stat_add(st + kSlots * 2, part[2], part[3]);
   }
 }
 
@@ -934,16 +923,12 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
   {
     const int Hi = H / 4, Wi = W / 4;
-    const int blocks = std::max(1, std::min(Hi * ((Wi + kDcTW - 1) / kDcTW), 4 * cu));
-    for (int b = 0; b < B; ++b) {
-      double* st = ws.reg_stats + reg_stat_index(b, 0, 0);
-      ProfScope ps(s, K_DECONV0);
-      hipLaunchKernelGGL(deconv_kernel, dim3(blocks, 1), dim3(256), 0, s,
-                         ws.h[2][nxt] + (size_t)b * 16 * Hi * Wi, params + L.dct_off[0],
-                         params + L.pk_off[P_D0B], Hi, Wi, ws.u0 + (size_t)b * 16 * 4 * Hi * Wi,
-                         st);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
+    ProfScope ps(s, K_DECONV0);
+    hipLaunchKernelGGL(deconv_px_kernel, dim3((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B),
+                       dim3(256), 0, s, ws.h[2][nxt], params + L.dct_off[0], params + L.pk_off[P_D0B],
+                       Hi, Wi, ws.u0, ws.reg_stats + reg_stat_index(0, 0, 0),
+                       (int)(reg_stat_index(1, 0, 0) - reg_stat_index(0, 0, 0)));
+    if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // cell 3: [gnrelu(u0), h1', h3] @ H/2
   for (int b = 0; b < B; ++b) {
@@ -962,16 +947,12 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // deconv_1: h3' (H/2) -> u1 (H) + GN stats
   {
     const int Hi = H / 2, Wi = W / 2;
-    const int blocks = std::max(1, std::min(Hi * ((Wi + kDcTW - 1) / kDcTW), 4 * cu));
-    for (int b = 0; b < B; ++b) {
-      double* st = ws.reg_stats + reg_stat_index(b, 1, 0);
-      ProfScope ps(s, K_DECONV1);
-      hipLaunchKernelGGL(deconv_kernel, dim3(blocks, 1), dim3(256), 0, s,
-                         ws.h[3][nxt] + (size_t)b * 16 * Hi * Wi, params + L.dct_off[1],
-                         params + L.pk_off[P_D1B], Hi, Wi, ws.u1 + (size_t)b * 16 * 4 * Hi * Wi,
-                         st);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
+    ProfScope ps(s, K_DECONV1);
+    hipLaunchKernelGGL(deconv_px_kernel, dim3((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B),
+                       dim3(256), 0, s, ws.h[3][nxt], params + L.dct_off[1], params + L.pk_off[P_D1B],
+                       Hi, Wi, ws.u1, ws.reg_stats + reg_stat_index(0, 1, 0),
+                       (int)(reg_stat_index(1, 1, 0) - reg_stat_index(0, 1, 0)));
+    if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // cell 4: [gnrelu(u1), h0', h4] @ H
   for (int b = 0; b < B; ++b) {

