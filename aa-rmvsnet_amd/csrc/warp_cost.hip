@@ -1185,12 +1185,12 @@ static int pipe_box_cap() {
   return (s && *s) ? std::max(4, std::atoi(s)) : INT_MAX;
 }
 
-// omega conv variant: 1 (default) the VALU omega_conv, 2 omega_mfma (AARMVS_OMEGA=mfma):
-// parity-green and deterministic, 713 vs 748 us per plane at the headline (one A/B on one
-// box), but the round-2 pipelined form of it did not pay off; kept opt-in
+// omega conv variant: 2 (default) omega_mfma, the conv3x3 on the matrix cores (split-fp16,
+// parity-green in every GPU test; 703-715 vs 718-753 us per plane at the headline in two
+// A/B runs on two boxes, profiles/r02_*); 1 the VALU omega_conv (AARMVS_OMEGA=valu)
 static int omega_variant() {
   const char* s = std::getenv("AARMVS_OMEGA");
-  return (s && std::strcmp(s, "mfma") == 0) ? 2 : 1;
+  return (s && std::strcmp(s, "valu") == 0) ? 1 : 2;
 }
 
 static PipeArgs pipe_args_c8(const CostArgs& ca, const SweepGeom& g, const Workspace& ws) {

@@ -169,7 +169,7 @@ def test_training_backward_matches_cpu_autograd():
             continue
         gr = P_cpu[k].grad.numpy()
         if k == "cost_regularization.conv_0.bias":
-            assert abs(float(p.grad)) < 1e-4 * gmax and abs(float(gr)) < 1e-4 * gmax
+            assert abs(float(p.grad)) < 1e-4 * gmax and abs(float(gr.item())) < 1e-4 * gmax
             continue
         tol = 1e-4 * max(np.abs(gr).max(), 1e-3 * gmax)
         np.testing.assert_allclose(p.grad.cpu().numpy(), gr, atol=tol, err_msg=k)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 measurement session: all GPU tests + smoke, bench lines (headline, configs 2 and 5,
+# Measurement session: all GPU tests + smoke, bench lines (headline, configs 2 and 5,
 # batched headline), rocprofv3 kernel stats of the headline command, PMC bytes passes.
 source tools/gpu_round.sh
 export TMPDIR=/tmp
