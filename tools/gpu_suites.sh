@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU suite on the default path, then the parity files with the VALU omega_conv selected
 # (the A/B of the two omega variants)
+set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
   > gpurun_out/r02_tests3.log 2>&1; rc=$?
