@@ -258,6 +258,54 @@ def e2e_bench(N: int, H: int, W: int, D: int, B: int, dev, reps: int = 2):
                 images=f"[{B},{N},3,{H},{W}] ~N(0,1)", depth_finite=ok)
 
 
+def train_bench(dev, planes=(4, 8), reps: int = 2):
+    """Training-step time at config 4's geometry (BASELINE configs[3]: 640x512, N=3, one
+    sample per GPU): the drop-in EMVSNet train forward (FeatNet + the HIP sweep with state
+    snapshots), softmax, mvsnet_cls_loss, and the backward (reverse-plane recompute, DESIGN
+    §6).  Timed at two truncated depth counts; D=192 is projected linearly from them (the
+    sweep and its recompute are uniform per plane)."""
+    from models.drmvsnet import EMVSNet, mvsnet_cls_loss
+    B, N, H, W, D_full = 1, 3, 512, 640, 192
+    g = torch.Generator(device="cpu").manual_seed(0)
+    imgs = torch.randn(B, N, 3, H, W, generator=g).to(dev)
+    sc = syn.scene(B, N, H, W, D_full, seed=0)
+    proj = torch.from_numpy(sc["proj_matrices"]).to(dev)
+    times = {}
+    for D in planes:
+        torch.manual_seed(0)
+        model = EMVSNet(D, image_scale=1.0, max_h=H, max_w=W, evidential=False).to(dev).train()
+        dv = torch.from_numpy(sc["depth_values"][:, :D].copy()).to(dev)
+        depth_gt = dv[:, D // 2].reshape(B, 1, 1).expand(B, H, W).contiguous()
+        mask = torch.ones(B, H, W, device=dev)
+
+        def step():
+            model.zero_grad(set_to_none=True)
+            prob, _, _ = model(imgs, proj, dv)
+            loss = mvsnet_cls_loss(prob, depth_gt, mask, dv)[0]
+            loss.backward()
+            return loss
+
+        step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            loss = step()
+        torch.cuda.synchronize()
+        times[D] = (time.perf_counter() - t0) / reps
+        ok = bool(torch.isfinite(loss))
+        del model
+    (d0, t0_), (d1, t1_) = sorted(times.items())
+    per_plane = (t1_ - t0_) / (d1 - d0)
+    fixed = t0_ - d0 * per_plane
+    return dict(metric="training step (forward + mvsnet_cls_loss + backward), 1 sample / GPU",
+                config="dtu_train_640x512_n3_d192", s_per_step_measured={str(k): round(v, 3) for k, v in times.items()},
+                s_per_plane=round(per_plane, 4), s_fixed=round(fixed, 3),
+                projected_s_per_step_d192=round(fixed + D_full * per_plane, 2),
+                note="D truncated to the measured counts; D=192 projected linearly",
+                backward="reverse-plane recompute in PyTorch on the GPU + HIP warp scatter",
+                loss_finite=ok)
+
+
 def spawn_ranks(n: int) -> int:
     """``--gpus N`` without a launcher: start N rank processes (one per GPU, the torchrun
     environment set by hand) from this parent, which never initialises the GPU
@@ -313,6 +361,8 @@ def main():
                     help="run the sweep's main stream at high priority (aux stream normal)")
     ap.add_argument("--no-fusion", action="store_true",
                     help="skip the depth-map fusion measurement (the next §8 row)")
+    ap.add_argument("--train", action="store_true",
+                    help="also time a config-4 training step (train_bench)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end EMVSNet.forward figure (FeatNet + sweep)")
     ap.add_argument("--planes", type=int, default=0,
@@ -430,6 +480,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = e2e_bench(N, H, W, D, B, dev)
 
+    train = None
+    if rank == 0 and world == 1 and args.train:
+        train = train_bench(dev)
+
     if rank == 0:
         line = {
             "metric": "depth-hypotheses/sec (ref-views x H x W x D / s)",
@@ -452,6 +506,7 @@ def main():
             "parity": parity,
             "fusion": fusion_res,
             "e2e": e2e,
+            "train": train,
             "kernels": {k: {kk: vv for kk, vv in v.items() if kk != "per_launch"}
                         for k, v in kernels.items()},
         }

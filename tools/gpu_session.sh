@@ -5,7 +5,7 @@ source tools/gpu_round.sh
 export TMPDIR=/tmp
 run tests 1000 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread
 run smoke 180 python -c "import __graft_entry__ as g; g.smoke()"
-run bench_headline 900 python bench.py
+run bench_headline 900 python bench.py --train
 run bench_cfg2 900 python bench.py --config dtu_eval_800x600_n5_d256 --no-e2e
 run bench_cfg5 900 python bench.py --config tnt_1920x1056_n11_d898 --no-e2e --steps 2
 run bench_headline_b2 900 python bench.py --batch 2 --no-cpu --no-fusion --no-e2e --steps 2
