@@ -28,10 +28,24 @@ def shard_range(n_items: int, rank: int, world: int) -> range:
     return range(start, start + base + (1 if rank < extra else 0))
 
 
+def shared_gpu() -> bool:
+    """AARMVS_SHARED_GPU=1: a rehearsal of the multi-rank path with every rank on the one
+    visible GPU (gloo, since RCCL refuses two ranks on one device); never set in production."""
+    return os.environ.get("AARMVS_SHARED_GPU", "0") == "1"
+
+
+def local_device_index(local_rank: int) -> int:
+    """The GPU a rank drives: its local rank (one process per GPU), or the one visible GPU
+    in a shared-GPU rehearsal."""
+    return local_rank % max(1, torch.cuda.device_count()) if shared_gpu() else local_rank
+
+
 def max_over_ranks(value: float, device=None) -> float:
     """Max of a host float over all ranks (identity without a process group)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
+    if dist.get_backend() == "gloo":
+        device = None
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -42,7 +56,7 @@ def init_process_group(device: torch.device | None = None) -> None:
     _, _, world = env()
     if world == 1 or dist.is_initialized():
         return
-    if device is not None and device.type == "cuda":
+    if device is not None and device.type == "cuda" and not shared_gpu():
         dist.init_process_group("nccl", device_id=device)
     else:
         dist.init_process_group("gloo")

@@ -41,7 +41,7 @@ for _p in (ROOT, os.path.join(ROOT, "aa-rmvsnet_amd")):
         sys.path.insert(0, _p)
 
 from aarmvs import ops, synthetic as syn  # noqa: E402
-from aarmvs.dist import env, init_process_group, max_over_ranks  # noqa: E402
+from aarmvs.dist import env, init_process_group, local_device_index, max_over_ranks  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= vector) dense peak
@@ -314,7 +314,7 @@ def spawn_ranks(n: int) -> int:
     import socket
     import subprocess
     visible = torch.cuda.device_count()
-    if n > visible:
+    if n > visible and not os.environ.get("AARMVS_SHARED_GPU") == "1":
         print(f"bench.py: --gpus {n} but only {visible} GPU(s) are visible", file=sys.stderr)
         return 2
     with socket.socket() as s:
@@ -377,8 +377,8 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched",
               file=sys.stderr)
         sys.exit(2)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local_device_index(local))
+    torch.cuda.set_device(dev)
     init_process_group(dev)
 
     cfg = dict(CONFIGS[args.config])
