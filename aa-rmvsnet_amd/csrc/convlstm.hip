@@ -824,7 +824,11 @@ __global__ void finalize_kernel(const float* __restrict__ max_prob, const float*
   }
 }
 
-// softmax over D (dim=1 of [B,D,H,W]); one thread per (b, pixel), coalesced over pixels.
+// softmax over D (dim=1 of [B,D,H,W], drmvsnet.py:291/:342); one thread per (b, pixel),
+// coalesced over pixels.  Two passes over D instead of three: the running max and the
+// rescaled running sum in one (online softmax, one exp per element: e = exp(-|v - m|)
+// serves both the rescale of the sum when v raises the max and the new term otherwise),
+// then exp(v - m) / sum.  Four planes' loads in flight per iteration.
 __global__ void __launch_bounds__(256) softmax_depth_kernel(const float* __restrict__ cost,
                                                             float* __restrict__ prob, int D,
                                                             int HW) {
@@ -832,12 +836,35 @@ __global__ void __launch_bounds__(256) softmax_depth_kernel(const float* __restr
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
     const float* c = cost + (size_t)b * D * HW + p;
     float* o = prob + (size_t)b * D * HW + p;
-    float m = -INFINITY;
-    for (int d = 0; d < D; ++d) m = fmaxf(m, c[(size_t)d * HW]);
-    float s = 0.f;
-    for (int d = 0; d < D; ++d) s += expf(c[(size_t)d * HW] - m);
+    float m = -INFINITY, s = 0.f;
+    auto add = [&](float v) {
+      const float dv = v - m;
+      const float e = expf(-fabsf(dv));
+      if (dv > 0.f) {
+        s = s * e + 1.0f;
+        m = v;
+      } else {
+        s += e;
+      }
+    };
+    int d = 0;
+    for (; d + 4 <= D; d += 4) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = c[(size_t)(d + u) * HW];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(v[u]);
+    }
+    for (; d < D; ++d) add(c[(size_t)d * HW]);
     const float inv = 1.0f / s;
-    for (int d = 0; d < D; ++d) o[(size_t)d * HW] = expf(c[(size_t)d * HW] - m) * inv;
+    for (d = 0; d + 4 <= D; d += 4) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = c[(size_t)(d + u) * HW];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[(size_t)(d + u) * HW] = expf(v[u] - m) * inv;
+    }
+    for (; d < D; ++d) o[(size_t)d * HW] = expf(c[(size_t)d * HW] - m) * inv;
   }
 }
 

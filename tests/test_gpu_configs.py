@@ -147,3 +147,17 @@ def test_standalone_wta_update_matches_sweep_and_reference_rule():
     ops.wta_update(c, torch.tensor([5.0]), mp, dm, es)
     ops.wta_update(c, torch.tensor([7.0]), mp, dm, es)
     assert torch.equal(dm, torch.full_like(dm, 5.0)) and torch.equal(es, torch.full_like(es, 2.0))
+
+
+def test_softmax_depth_matches_torch():
+    """aarmvs_softmax_depth (online two-pass softmax over D) vs torch.softmax(dim=1), D not
+    a multiple of the kernel's 4-plane unroll, costs spanning +-80 (exp over/underflow
+    handled by the max subtraction)."""
+    import torch
+    from aarmvs import ops
+    g = torch.Generator().manual_seed(9)
+    for B, D, H, W in [(2, 37, 24, 40), (1, 192, 16, 20), (1, 1, 8, 8)]:
+        cost = (torch.rand(B, D, H, W, generator=g) * 160.0 - 80.0)
+        ref = torch.softmax(cost.double(), dim=1).float()
+        got = ops.softmax_depth(cost.cuda()).cpu()
+        np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-5, atol=1e-7)

@@ -1,5 +1,8 @@
+#!/bin/bash
+# a quick subset of the GPU tests (args: pytest selectors; default: the configs + eval files)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_eval.py tests/test_fusion.py -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/r02_eval_tests.log 2>&1; rc=$?
-tail -15 gpurun_out/r02_eval_tests.log
+sel=${@:-tests/test_gpu_configs.py tests/test_gpu_eval.py}
+timeout -k 10 400 python -u -m pytest $sel -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/quick_tests.log 2>&1; rc=$?
+tail -8 gpurun_out/quick_tests.log
 exit $rc
