@@ -172,3 +172,64 @@ def test_ddp_world2_gradients_equal_hand_averaged():
         assert p.returncode == 0, out[-3000:]
     for out in outs:
         assert "DDP_OK" in out, out[-3000:]
+
+
+def _train_args(tmp_path, numdepth, extra=()):
+    from aarmvs import train_ddp
+    mini = os.path.join(ROOT, "tests", "golden", "dtu_mini")
+    return train_ddp.parse_args([
+        "--trainpath", mini, "--trainlist", os.path.join(mini, "scans.txt"), "--numdepth", str(numdepth),
+        "--max_h", "64", "--max_w", "80", "--image_scale", "0.25", "--epochs", "2", "--max_steps", "2",
+        "--logdir", str(tmp_path / "ckpt"), "--summary_freq", "1", "--train_light_idx", "3", *extra])
+
+
+@pytest.mark.parametrize("numdepth", [8, 32])
+def test_train_driver_steps_and_checkpoints(tmp_path, numdepth):
+    """aarmvs.train_ddp (train.py's loop) on the tiny DTU tree: finite losses, one checkpoint
+    per epoch in train.py's format, reloadable into a fresh model, and --resume continues
+    from the last epoch (D=32: the evidential head and loss_der run, as in train.py)."""
+    from aarmvs import train_ddp
+    from models import EMVSNet
+    out = train_ddp.train(_train_args(tmp_path, numdepth), 0, 1, DEV, log=lambda *a: None)
+    assert len(out["losses"]) == 4 and all(np.isfinite(out["losses"]))
+    assert [os.path.basename(p) for p in out["checkpoints"]] == ["model_000000.ckpt", "model_000001.ckpt"]
+    st = torch.load(out["checkpoints"][-1], map_location="cpu", weights_only=True)
+    assert set(st) == {"epoch", "model", "optimizer"} and st["epoch"] == 1
+    EMVSNet(disparity_level=numdepth, image_scale=0.25, max_h=64, max_w=80).load_state_dict(st["model"], strict=True)
+    args = _train_args(tmp_path, numdepth, ["--resume"])
+    args.epochs = 3
+    out2 = train_ddp.train(args, 0, 1, DEV, log=lambda *a: None)
+    assert [os.path.basename(p) for p in out2["checkpoints"]] == ["model_000002.ckpt"]
+
+
+def test_train_driver_two_ranks_share_the_samples(tmp_path):
+    """Two ranks of aarmvs.train_ddp (shared-GPU rehearsal: both on cuda:0, gloo): DDP over
+    the HIP training path, each rank on its half of the samples, rank 0 checkpoints."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mini = os.path.join(ROOT, "tests", "golden", "dtu_mini")
+    cmd = [sys.executable, "-m", "aarmvs.train_ddp", "--trainpath", mini, "--trainlist",
+           os.path.join(mini, "scans.txt"), "--numdepth", "8", "--max_h", "64", "--max_w", "80",
+           "--epochs", "1", "--max_steps", "2", "--logdir", str(tmp_path / "ck"), "--train_light_idx", "3"]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), AARMVS_SHARED_GPU="1",
+                   PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "aa-rmvsnet_amd"), ROOT,
+                                               os.environ.get("PYTHONPATH", "")]))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=150)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+        assert p.returncode == 0, out[-3000:]
+    assert "rank 0/2: 2 steps" in outs[0] and "rank 1/2: 2 steps" in outs[1], outs
+    assert os.path.exists(tmp_path / "ck" / "model_000000.ckpt")
