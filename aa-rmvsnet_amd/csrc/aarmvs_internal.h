@@ -13,6 +13,10 @@ namespace aarmvs {
 constexpr int kC = 32;          // feature channels (FeatNet output)
 constexpr int kSlots = 32;      // fp64 atomic slots per GroupNorm statistic
 constexpr float kGnEps = 1e-5f; // nn.GroupNorm default eps
+// The sweep computes cost slices in groups of up to kPlaneGroup planes: one launch of each
+// cost-slice kernel covers the group, so the neighbouring planes' bilinear footprints (and
+// the reference tile) are fetched from HBM once and re-read from L2.
+constexpr int kPlaneGroup = 8;
 
 // ---------------------------------------------------------------------------
 // Parameter tensors, in raw-blob order (aarmvs.h).
@@ -66,27 +70,30 @@ const ParamLayout& param_layout();
 // Workspace layout.
 // ---------------------------------------------------------------------------
 struct Workspace {
-  double* omega_stats[2]; // per plane parity: [B][nsrc][3][kSlots][2] omega GN statistics
+  double* omega_stats;    // [kPlaneGroup][B][nsrc][3][kSlots][2] omega GN statistics per group plane
   double* reg_stats;      // [B][2 deconvs][2 groups][kSlots][2] U-Net GN statistics
   unsigned* xbound;       // float bits of an upper bound on |x| (cost slice) for this sweep:
                           // 8 max|feature|^2 (to_c8) or max|x| (unet_step); cell 0's fp16 range
   float* max_prob;        // [B,HW]
   float* exp_sum;         // [B,HW]
   float* depth;           // [B,HW]
-  float* x;               // [B,32,H,W] cost slice
+  float* xg[2];           // per group parity: [kPlaneGroup][B][H][W][32] cost slices (NHWC)
+  float* x;               // = xg[0]: the single-slice buffer of aarmvs_unet_step / cost_slice
   float* feat8[AARMVS_MAX_SRC + 1]; // [B][4][H][W][8] "c8" copies of ref (0) and source views
-  float* t1[2];           // per plane parity: [B][nsrc][HW][4] omega conv3x3 output
+  float* t1;              // [kPlaneGroup][B][nsrc][HW][4] omega conv3x3 output per group plane
   float* u0;              // [B,16,H/2,W/2] deconv_0 output (pre-GN)
   float* u1;              // [B,16,H,W]     deconv_1 output (pre-GN)
   float* h[5][2];         // ping-pong hidden states
   float* c[5];            // cell states (updated in place)
   size_t bytes;
-  size_t omega_stats_bytes;  // one parity
+  size_t omega_stats_bytes;  // one plane
   size_t reg_stats_bytes;
-  size_t stats_bytes;        // both omega parities + reg (contiguous, for the initial clear)
+  size_t stats_bytes;        // omega + reg statistics and xbound (contiguous, for the initial clear)
   size_t state_bytes;        // h[*][*], c[*] region (contiguous) for zero-init
   void* state_begin;
   size_t wta_bytes;          // max_prob/exp_sum/depth region
+  size_t x_plane;            // floats per plane in xg
+  size_t t1_plane;           // float4s per plane in t1
 };
 Workspace carve_workspace(void* base, int B, int H, int W, int nsrc);
 // U-Net statistic (deconv j, group g) of batch element b within reg_stats
@@ -115,10 +122,11 @@ struct CostArgs {
   const float* depth_values;  // [B,D]
   const float* params;    // packed
 };
-// The cost-slice pipeline (warp_cost.hip): cost_x writes plane d's cost slice from t1_d
-// and plane d's statistics; omega_next produces t1 and the three GroupNorm statistics of
-// plane d (omega_conv + omega_stats<1> + <2>).  The statistics of a plane must be zero
-// before its omega_next and are cleared by the caller once its cost_x has run.
+// The cost-slice stage (warp_cost.hip) for the planes d0 .. d0 + n - 1 (n <= kPlaneGroup):
+// omega_group clears the group's statistics, then writes t1 and the three GroupNorm
+// statistics of every plane (omega conv + omega_stats<1> + <2>); cost_x_group then writes
+// each plane's cost slice to x0 + k ws.x_plane (and, for plane omega_k, the omega weights
+// to omega_out).  Both use the t1 / statistics slots of the workspace: one group at a time.
 // NCHW <-> NHWC copy of a [B][C][HW] / [B][HW][C] fp32 tensor (API edges only)
 // depth-map fusion core (fusion.hip)
 hipError_t launch_fusion_filter(const aarmvs_fusion_args* a, hipStream_t s);
@@ -129,10 +137,10 @@ hipError_t launch_layout(const float* in, float* out, int B, int C, int HW, bool
 // slice's |x| (|warp - ref| <= 2 max|feature|, (1 + w) <= 2)
 hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s,
                         unsigned* xbound = nullptr);
-hipError_t launch_cost_x(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d,
-                         float* omega_out, hipStream_t s);
-hipError_t launch_omega_next(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d,
-                             hipStream_t s);
+hipError_t launch_omega_group(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d0,
+                              int n, hipStream_t s);
+hipError_t launch_cost_x_group(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d0,
+                               int n, float* x0, float* omega_out, int omega_k, hipStream_t s);
 
 hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
                             const Workspace& ws, int parity, hipStream_t s);

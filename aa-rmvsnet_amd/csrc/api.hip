@@ -141,8 +141,7 @@ Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
   ws.omega_stats_bytes = (size_t)B * nsrc * 3 * kSlots * 2 * sizeof(double);
   ws.reg_stats_bytes = (size_t)B * 4 * kSlots * 2 * sizeof(double);
   const size_t stats_begin = off;
-  ws.omega_stats[0] = reinterpret_cast<double*>(take(ws.omega_stats_bytes));
-  ws.omega_stats[1] = reinterpret_cast<double*>(take(ws.omega_stats_bytes));
+  ws.omega_stats = reinterpret_cast<double*>(take(kPlaneGroup * ws.omega_stats_bytes));
   ws.reg_stats = reinterpret_cast<double*>(take(ws.reg_stats_bytes));
   ws.xbound = reinterpret_cast<unsigned*>(take(sizeof(unsigned)));
   ws.stats_bytes = off - stats_begin;
@@ -151,10 +150,13 @@ Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
   ws.exp_sum = reinterpret_cast<float*>(take(B * HW * 4));
   ws.depth = reinterpret_cast<float*>(take(B * HW * 4));
   ws.wta_bytes = off - wta_begin;
-  ws.x = reinterpret_cast<float*>(take(B * kC * HW * 4));
+  ws.x_plane = (size_t)B * kC * HW;
+  ws.t1_plane = (size_t)B * nsrc * HW;
+  ws.xg[0] = reinterpret_cast<float*>(take(kPlaneGroup * ws.x_plane * 4));
+  ws.xg[1] = reinterpret_cast<float*>(take(kPlaneGroup * ws.x_plane * 4));
+  ws.x = ws.xg[0];
   for (int v = 0; v <= nsrc; ++v) ws.feat8[v] = reinterpret_cast<float*>(take(B * kC * HW * 4));
-  ws.t1[0] = reinterpret_cast<float*>(take((size_t)B * nsrc * HW * 16));
-  ws.t1[1] = reinterpret_cast<float*>(take((size_t)B * nsrc * HW * 16));
+  ws.t1 = reinterpret_cast<float*>(take(kPlaneGroup * ws.t1_plane * 16));
   ws.u0 = reinterpret_cast<float*>(take(B * 16 * HW2 * 4));
   ws.u1 = reinterpret_cast<float*>(take(B * 16 * HW * 4));
   const size_t state_begin = off;
@@ -412,6 +414,17 @@ float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int plan
   return which == 0 ? ws.h[cell][plane_parity & 1] : ws.c[cell];
 }
 
+}  // extern "C"
+
+// planes per cost-stage group: kPlaneGroup, or AARMVS_NPL=n (1 <= n <= kPlaneGroup; A/B runs)
+static int plane_group() {
+  const char* s = std::getenv("AARMVS_NPL");
+  const int n = (s && *s) ? std::atoi(s) : kPlaneGroup;
+  return std::max(1, std::min(kPlaneGroup, n));
+}
+
+extern "C" {
+
 int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   if (!a) return fail(AARMVS_ERR_INVALID, "sweep: null args");
   int rc = check_geom(a->B, a->H, a->W, a->nsrc);
@@ -434,26 +447,21 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   ca.rel = a->rel_proj;
   ca.depth_values = a->depth_values;
   ca.params = params;
-  // Two-stream schedule (a->aux_stream): the omega pipeline of plane d+1 (omega_conv +
-  // statistics) runs on the aux stream while the main stream runs plane d's cost slice
-  // and regulariser step.  Per plane two events: ev_aux[p] "t1/statistics of plane p
-  // ready" (aux -> main, before cost_x(p)) and ev_main[p] "cost_x(p) done and plane p's
-  // statistics cleared" (main -> aux, before omega of plane p + 2, which reuses the
-  // buffers of parity p).
+  // Planes are processed in groups of up to kPlaneGroup (AARMVS_NPL=n for A/B runs).  The
+  // cost slices do not depend on the recurrence, so a group's whole cost-slice stage
+  // (omega conv, statistics, cost_x: one launch each over the group's planes) runs ahead of
+  // its regulariser steps.  Two-stream schedule (a->aux_stream): the cost stage runs on the
+  // aux stream, group i's beside group i-1's regulariser steps on the main stream; per
+  // group parity two events: ev_cost[p] "group's slices ready" (aux -> main) and
+  // ev_used[p] "group's slices consumed" (main -> aux, before group i+2 reuses the slots).
   hipStream_t aux = (a->aux_stream && a->aux_stream != stream) ? a->aux_stream : nullptr;
-  // Overlap mode: by default omega(d+1) starts as soon as cost_x(d-1) released its buffers
-  // (beside plane d-1's regulariser step and plane d's cost slice).  AARMVS_OVERLAP=costx
-  // runs it beside cost_x(d) only (the regulariser step waits for it, so the whole-CU
-  // ConvLSTM blocks never queue behind omega blocks): measured 888 vs 904 M hyp/s (single
-  // stream 885), so not the default.
-  const char* ov_env = std::getenv("AARMVS_OVERLAP");
-  const bool ov_all = !(ov_env && std::strcmp(ov_env, "costx") == 0);
-  // main[2], aux[2], fork/join, start[2]: a per-thread, per-device set reused across calls
-  // (a training forward makes one call per plane).  Events are only recorded/waited on the
+  const int G = plane_group();
+  // ev_cost[2], ev_used[2], fork/join: a per-thread, per-device set reused across calls (a
+  // training forward makes one call per plane).  Events are only recorded/waited on the
   // caller's streams, and a record overwrites the previous one, so reuse is safe.
   struct EventSet {
     int dev = -1;
-    hipEvent_t ev[7] = {};
+    hipEvent_t ev[5] = {};
   };
   static thread_local EventSet evs;
   hipEvent_t* ev = evs.ev;
@@ -471,10 +479,9 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
       evs.dev = dev;
     }
   }
-  hipEvent_t* ev_main = ev;
-  hipEvent_t* ev_aux = ev + 2;
-  hipEvent_t* ev_start = ev + 5;
-  hipStream_t os = aux ? aux : stream;   // the omega pipeline's stream
+  hipEvent_t* ev_cost = ev;
+  hipEvent_t* ev_used = ev + 2;
+  hipStream_t cs = aux ? aux : stream;   // the cost stage's stream
 
   if (a->d_begin == 0) {
     // UNetConvLSTM._init_hidden (drmvsnet.py:133-134, 202-206) and the WTA images
@@ -483,9 +490,9 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
       return sweep_fail(e, "sweep: state init");
     if ((e = hipMemsetAsync(ws.max_prob, 0, ws.wta_bytes, stream)) != hipSuccess)
       return sweep_fail(e, "sweep: wta init");
-    if ((e = hipMemsetAsync(ws.omega_stats[0], 0, ws.stats_bytes, stream)) != hipSuccess)
+    if ((e = hipMemsetAsync(ws.omega_stats, 0, ws.stats_bytes, stream)) != hipSuccess)
       return sweep_fail(e, "sweep: stats init");
-    // c8 copies of the features for the pipeline
+    // c8 copies of the features for the cost stage
     const int HW = a->H * a->W;
     // (each copy also folds 8 max|feature|^2 into ws.xbound: cell 0's fp16 range guard)
     if ((e = launch_to_c8(a->ref_fea, ws.feat8[0], a->B, HW, stream, ws.xbound)) != hipSuccess)
@@ -500,57 +507,43 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         (e = hipStreamWaitEvent(aux, ev[4], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: fork");
   }
-  if (a->d_begin == 0) {   // prime the pipeline with plane 0's omega conv and statistics
-    if ((e = launch_omega_next(ca, g, ws, 0, os)) != hipSuccess)
-      return sweep_fail(e, "sweep: omega pipeline prologue");
-    if (aux && (e = hipEventRecord(ev_aux[0], aux)) != hipSuccess)
-      return sweep_fail(e, "sweep: event record");
-  }
   // the WTA images are maintained on every plane, whether or not this call returns depth:
   // a sweep split into d_range calls gives the same depth/confidence however its earlier
   // pieces were requested (24 B/px per plane, <0.5% of a plane's time)
   const bool wta = true;
-  const size_t stats_parity_bytes = ws.omega_stats_bytes;
-  for (int d = a->d_begin; d < a->d_end; ++d) {
-    const bool last = d == a->d_end - 1;
-    // omega pipeline of plane d + 1; its buffers were last read by cost_x(d - 1)
-    if (aux && !ov_all && (e = hipEventRecord(ev_start[d & 1], stream)) != hipSuccess)
-      return sweep_fail(e, "sweep: event record");
-    if (d + 1 < a->D) {
-      if (aux && ov_all && d - 1 >= a->d_begin &&
-          (e = hipStreamWaitEvent(aux, ev_main[(d - 1) & 1], 0)) != hipSuccess)
-        return sweep_fail(e, "sweep: event wait");
-      if (aux && !ov_all && (e = hipStreamWaitEvent(aux, ev_start[d & 1], 0)) != hipSuccess)
-        return sweep_fail(e, "sweep: event wait");
-      if ((e = launch_omega_next(ca, g, ws, d + 1, os)) != hipSuccess)
-        return sweep_fail(e, "sweep: omega pipeline");
-      if (aux && (e = hipEventRecord(ev_aux[(d + 1) & 1], aux)) != hipSuccess)
-        return sweep_fail(e, "sweep: event record");
-    }
-    // cost slice of plane d (its omega pipeline ran in the previous iteration, or in the
-    // previous call for the first plane of a continued range)
-    if (aux && (d > a->d_begin || a->d_begin == 0) &&
-        (e = hipStreamWaitEvent(stream, ev_aux[d & 1], 0)) != hipSuccess)
+  const int d_last = a->d_end - 1;
+  int gi = 0;
+  for (int g0 = a->d_begin; g0 < a->d_end; g0 += G, ++gi) {
+    const int n = std::min(G, a->d_end - g0);
+    float* const xs = ws.xg[gi & 1];
+    // cost stage: its slots were last read by group gi - 2's regulariser steps
+    if (aux && gi >= 2 && (e = hipStreamWaitEvent(aux, ev_used[gi & 1], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: event wait");
-    if ((e = launch_cost_x(ca, g, ws, d, last ? a->omega_out : nullptr, stream)) != hipSuccess)
-      return sweep_fail(e, "sweep: cost slice");
-    // plane d's statistics are consumed: clear them for plane d + 2
-    if ((e = hipMemsetAsync(ws.omega_stats[d & 1], 0, stats_parity_bytes, stream)) != hipSuccess)
-      return sweep_fail(e, "sweep: stats clear");
-    if (aux && (e = hipEventRecord(ev_main[d & 1], stream)) != hipSuccess)
-      return sweep_fail(e, "sweep: event record");
-    if (aux && !ov_all && d + 1 < a->D &&
-        (e = hipStreamWaitEvent(stream, ev_aux[(d + 1) & 1], 0)) != hipSuccess)
-      return sweep_fail(e, "sweep: event wait");
-    if (last && a->slice_out) {
-      e = launch_layout(ws.x, a->slice_out, a->B, kC, a->H * a->W, false, stream);
-      if (e != hipSuccess) return sweep_fail(e, "sweep: slice copy");
-    }
-    if ((e = launch_unet_step(ws.x, params, g, ws, d & 1, stream)) != hipSuccess)
-      return sweep_fail(e, "sweep: regulariser step");
-    if ((e = launch_head_wta(params, g, ws, d & 1, a->depth_values, d, a->cost_out, wta, stream)) !=
+    if ((e = launch_omega_group(ca, g, ws, g0, n, cs)) != hipSuccess)
+      return sweep_fail(e, "sweep: omega stage");
+    const int ok = d_last < g0 + n ? d_last - g0 : -1;
+    if ((e = launch_cost_x_group(ca, g, ws, g0, n, xs, ok >= 0 ? a->omega_out : nullptr, ok, cs)) !=
         hipSuccess)
-      return sweep_fail(e, "sweep: head/wta");
+      return sweep_fail(e, "sweep: cost slices");
+    if (aux && ((e = hipEventRecord(ev_cost[gi & 1], aux)) != hipSuccess ||
+                (e = hipStreamWaitEvent(stream, ev_cost[gi & 1], 0)) != hipSuccess))
+      return sweep_fail(e, "sweep: event");
+    // regulariser steps and WTA of the group's planes
+    for (int k = 0; k < n; ++k) {
+      const int d = g0 + k;
+      const float* xd = xs + (size_t)k * ws.x_plane;
+      if (d == d_last && a->slice_out) {
+        e = launch_layout(xd, a->slice_out, a->B, kC, a->H * a->W, false, stream);
+        if (e != hipSuccess) return sweep_fail(e, "sweep: slice copy");
+      }
+      if ((e = launch_unet_step(xd, params, g, ws, d & 1, stream)) != hipSuccess)
+        return sweep_fail(e, "sweep: regulariser step");
+      if ((e = launch_head_wta(params, g, ws, d & 1, a->depth_values, d, a->cost_out, wta,
+                               stream)) != hipSuccess)
+        return sweep_fail(e, "sweep: head/wta");
+    }
+    if (aux && (e = hipEventRecord(ev_used[gi & 1], stream)) != hipSuccess)
+      return sweep_fail(e, "sweep: event record");
   }
   if (aux) {   // join: everything the call enqueued is ordered on `stream` at return
     if ((e = hipEventRecord(ev[4], aux)) != hipSuccess ||
@@ -586,8 +579,6 @@ int aarmvs_cost_slice(const float* ref_fea, const float* const* src_fea, const f
   ca.params = static_cast<const float*>(packed_params);
   hipError_t e;
   const int HW = H * W;
-  if ((e = hipMemsetAsync(ws.omega_stats[0], 0, ws.omega_stats_bytes, stream)) != hipSuccess)
-    return hip_fail(e, "cost_slice: stats init");
   if ((e = hipMemsetAsync(ws.xbound, 0, sizeof(unsigned), stream)) != hipSuccess)
     return hip_fail(e, "cost_slice: bound init");
   if ((e = launch_to_c8(ref_fea, ws.feat8[0], B, HW, stream, ws.xbound)) != hipSuccess)
@@ -595,9 +586,9 @@ int aarmvs_cost_slice(const float* ref_fea, const float* const* src_fea, const f
   for (int v = 0; v < nsrc; ++v)
     if ((e = launch_to_c8(src_fea[v], ws.feat8[1 + v], B, HW, stream, ws.xbound)) != hipSuccess)
       return hip_fail(e, "cost_slice: c8 copy");
-  if ((e = launch_omega_next(ca, g, ws, 0, stream)) != hipSuccess)
-    return hip_fail(e, "cost_slice: omega pipeline");
-  if ((e = launch_cost_x(ca, g, ws, 0, omega_out, stream)) != hipSuccess)
+  if ((e = launch_omega_group(ca, g, ws, 0, 1, stream)) != hipSuccess)
+    return hip_fail(e, "cost_slice: omega stage");
+  if ((e = launch_cost_x_group(ca, g, ws, 0, 1, ws.x, omega_out, 0, stream)) != hipSuccess)
     return hip_fail(e, "cost_slice: cost slice");
   if ((e = launch_layout(ws.x, slice_out, B, kC, HW, false, stream)) != hipSuccess)
     return hip_fail(e, "cost_slice: slice copy");

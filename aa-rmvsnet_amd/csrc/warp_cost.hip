@@ -182,6 +182,13 @@ struct PipeArgs {
       off_ob2, off_og2w, off_og2b, off_owo, off_obo;
   int B, H, W, nsrc;
   int box_cap;                // LDS source-box capacity in pixels (diagnostic override, <= the kernel's)
+  // plane batching: one launch covers planes d .. d + npl - 1 (d = d_prev or d_next), plane
+  // k's t1 / statistics / x at k times these strides from the plane-0 pointers
+  int npl;
+  size_t t1_kstride;          // float4s
+  size_t st_kstride;          // doubles
+  size_t x_kstride;           // floats
+  int omega_k;                // cost_x: the plane (0 .. npl-1) whose omega weights go to omega_out
 };
 
 // omega pointwise chain helpers (ResnetBlockGn, module.py:252-264)
@@ -443,21 +450,25 @@ __attribute__((amdgpu_waves_per_eu((XV & 8) ? 6 : (XV & 4) ? 5 : 4))) cost_x_ker
   __shared__ GnStat gs[AARMVS_MAX_SRC][3];
   const int tid = threadIdx.x, b = blockIdx.y;
   const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  // the npl planes of a tile are consecutive blocks of one XCD: their taps share its L2
+  const int seq = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = seq / a.npl, kp = seq - tile * a.npl;
   const int tiles_x = (W + kTileW - 1) / kTileW;
   const int h = tid & 1, q = tid >> 1;
   const int gy = (tile / tiles_x) * kXRows + q / kTileW, gx = (tile % tiles_x) * kTileW + q % kTileW;
   if (tid < 3 * nsrc) {
     const int v = tid / 3, k = tid % 3;
-    gs[v][k] = stat_read(a.st_prev + st_index(b, v, k, nsrc), 4.0 * HW);
+    gs[v][k] = stat_read(a.st_prev + kp * a.st_kstride + st_index(b, v, k, nsrc), 4.0 * HW);
   }
   __syncthreads();
   if (gy >= H || gx >= W) return;
+  const float4* __restrict__ t1p = a.t1_prev + kp * a.t1_kstride;
+  float* const omega_out = kp == a.omega_k ? a.omega_out : nullptr;
   // parameters come through a __restrict__ argument so that their uniform loads are
   // scalar (s_load) despite the kernel's vector stores
   OmegaP o;
   load_omega(a, P, o);
-  const float dep = a.dvals[b * a.D + a.d_prev];
+  const float dep = a.dvals[b * a.D + a.d_prev + kp];
   const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's c8 image
   const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(a.ref + (size_t)b * kC * HW, fbytes);
   const size_t p = (size_t)gy * W + gx;
@@ -479,9 +490,9 @@ __attribute__((amdgpu_waves_per_eu((XV & 8) ? 6 : (XV & 4) ? 5 : 4))) cost_x_ker
       // base (scalar) plus this lane's view step
       const uint32_t p32 = (uint32_t)p, hw = (uint32_t)HW;
       const float w = omega_weight(
-          a.t1_prev[(uint32_t)(b * nsrc + vp) * hw + (uint32_t)(vm - vp) * hw + p32], gs[vm], o);
-      if (a.omega_out && vp + h < nsrc)
-        a.omega_out[(uint32_t)(vp * a.B + b) * hw + (uint32_t)(h * a.B) * hw + p32] = w;
+          t1p[(uint32_t)(b * nsrc + vp) * hw + (uint32_t)(vm - vp) * hw + p32], gs[vm], o);
+      if (omega_out && vp + h < nsrc)
+        omega_out[(uint32_t)(vp * a.B + b) * hw + (uint32_t)(h * a.B) * hw + p32] = w;
       const float ws = swap_pair(w);
       wv[vp] = h ? ws : w;
       if (vp + 1 < AARMVS_MAX_SRC) wv[vp + 1] = h ? w : ws;
@@ -496,8 +507,8 @@ __attribute__((amdgpu_waves_per_eu((XV & 8) ? 6 : (XV & 4) ? 5 : 4))) cost_x_ker
 #pragma unroll
       for (int k = 1; k < AARMVS_MAX_SRC; ++k) w = v == k ? wv[k] : w;
     } else {
-      w = omega_weight(a.t1_prev[((size_t)b * nsrc + v) * HW + p], gs[v], o);
-      if (a.omega_out && h == 0) a.omega_out[((size_t)v * a.B + b) * HW + p] = w;
+      w = omega_weight(t1p[((size_t)b * nsrc + v) * HW + p], gs[v], o);
+      if (omega_out && h == 0) omega_out[((size_t)v * a.B + b) * HW + p] = w;
     }
     const float wp1 = __fadd_rn(w, 1.0f);
     const Box none{0, 0, 0, 0};
@@ -532,7 +543,7 @@ __attribute__((amdgpu_waves_per_eu((XV & 8) ? 6 : (XV & 4) ? 5 : 4))) cost_x_ker
     }
   }
   // NHWC: this lane's channels 8c + 4h .. +3 of pixel p, one 16-B store per chunk
-  float* xo = a.x + ((size_t)b * HW + p) * kC + 4 * h;
+  float* xo = a.x + kp * a.x_kstride + ((size_t)b * HW + p) * kC + 4 * h;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     float r[4];
@@ -633,7 +644,8 @@ omega_conv_kernel(PipeArgs a,
   // the views of one tile are consecutive blocks on one XCD: the reference tile is
   // fetched from HBM once and re-read from that XCD's L2
   const int seq = xcd_tile(blockIdx.x, gridDim.x);
-  const int tile = seq / nsrc, v = seq - tile * nsrc;
+  const int tile = seq / (nsrc * a.npl), vk = seq - tile * (nsrc * a.npl);
+  const int v = vk / a.npl, kp = vk - v * a.npl;
   const int tiles_x = (W + kTileW - 1) / kTileW;
   const int y0 = (tile / tiles_x) * kTileH, x0 = (tile % tiles_x) * kTileW;
   const int ty = tid / kTileW, tx = tid % kTileW;
@@ -661,7 +673,7 @@ omega_conv_kernel(PipeArgs a,
   const uint32_t ring_hp = (uint32_t)(hy * kCHW + hx);
   if (tid < 8) box[kCBoxPx * 8 + tid] = 0.f;   // the zero pixel
 
-  const float dep = a.dvals[b * a.D + a.d_next];
+  const float dep = a.dvals[b * a.D + a.d_next + kp];
   const float* __restrict__ m = Rel + 12 * (v * a.B + b);
   const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's c8 image
   const uint32_t cbytes = (uint32_t)HW * 32u;                // one chunk image
@@ -848,7 +860,7 @@ omega_conv_kernel(PipeArgs a,
     out.y = o4[1] + b0[1];
     out.z = o4[2] + b0[2];
     out.w = o4[3] + b0[3];
-    a.t1_next[((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
+    a.t1_next[kp * a.t1_kstride + ((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
     ps = (out.x + out.y) + (out.z + out.w);
     pss = (out.x * out.x + out.y * out.y) + (out.z * out.z + out.w * out.w);
   }
@@ -865,7 +877,7 @@ omega_conv_kernel(PipeArgs a,
       s0 += wsum[w][0];
       s1 += wsum[w][1];
     }
-    stat_add(a.st_next + st_index(b, v, 0, nsrc), s0, s1);
+    stat_add(a.st_next + kp * a.st_kstride + st_index(b, v, 0, nsrc), s0, s1);
   }
 }
 
@@ -911,8 +923,11 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.z;
   const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
+  // a tile's (view, plane) blocks are consecutive on one XCD: the reference tile, and a
+  // view's source box across the npl neighbouring planes, come from its L2
   const int seq = xcd_tile(blockIdx.x, gridDim.x);
-  const int tile = seq / nsrc, v = seq - tile * nsrc;
+  const int tile = seq / (nsrc * a.npl), vk = seq - tile * (nsrc * a.npl);
+  const int v = vk / a.npl, kp = vk - v * a.npl;
   const int tiles_x = (W + kMOutW - 1) / kMOutW;
   const int y0 = (tile / tiles_x) * kMOutH, x0 = (tile % tiles_x) * kMOutW;
   const int hy = 2 * wave + (lane >> 5), hx = lane & 31;   // haloed pixel of this lane
@@ -921,7 +936,7 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   const bool interior = in_img && hy >= 1 && hy <= kMOutH && hx >= 1 && hx <= kMOutW;
   if (tid < 8) box[kMBoxPx * 8 + tid] = 0.f;   // the zero pixel
 
-  const float dep = a.dvals[b * a.D + a.d_next];
+  const float dep = a.dvals[b * a.D + a.d_next + kp];
   const float* __restrict__ m = Rel + 12 * (v * a.B + b);
   const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);
   const uint32_t cbytes = (uint32_t)HW * 32u;
@@ -1070,7 +1085,7 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     out.y = fmaf(g4[1], isc, o4[1]) + b0[1];
     out.z = fmaf(g4[2], isc, o4[2]) + b0[2];
     out.w = fmaf(g4[3], isc, o4[3]) + b0[3];
-    a.t1_next[((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
+    a.t1_next[kp * a.t1_kstride + ((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
     ps = (out.x + out.y) + (out.z + out.w);
     pss = (out.x * out.x + out.y * out.y) + (out.z * out.z + out.w * out.w);
   }
@@ -1087,7 +1102,7 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
       s0 += wsum[w][0];
       s1 += wsum[w][1];
     }
-    stat_add(a.st_next + st_index(b, v, 0, nsrc), s0, s1);
+    stat_add(a.st_next + kp * a.st_kstride + st_index(b, v, 0, nsrc), s0, s1);
   }
 }
 
@@ -1097,14 +1112,15 @@ __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
                                                           const float* __restrict__ P) {
   __shared__ float red[2 * 4];
   __shared__ GnStat gs[2];
-  const int v = blockIdx.y, b = blockIdx.z;
+  const int v = blockIdx.y, b = blockIdx.z / a.npl, kp = blockIdx.z - b * a.npl;
   const int HW = a.H * a.W;
+  double* const st = a.st_next + kp * a.st_kstride;
   if (threadIdx.x < STAGE)
-    gs[threadIdx.x] = stat_read(a.st_next + st_index(b, v, threadIdx.x, a.nsrc), 4.0 * HW);
+    gs[threadIdx.x] = stat_read(st + st_index(b, v, threadIdx.x, a.nsrc), 4.0 * HW);
   __syncthreads();
   OmegaP o;
   load_omega(a, P, o);
-  const float4* t1 = a.t1_next + ((size_t)b * a.nsrc + v) * HW;
+  const float4* t1 = a.t1_next + kp * a.t1_kstride + ((size_t)b * a.nsrc + v) * HW;
   float part[2] = {0.f, 0.f};
   // four independent 16-B loads in flight per thread per iteration
   const int gstride = gridDim.x * blockDim.x;
@@ -1137,7 +1153,7 @@ __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
     }
   }
   block_sum<2>(part, red);
-  if (threadIdx.x == 0) stat_add(a.st_next + st_index(b, v, STAGE, a.nsrc), part[0], part[1]);
+  if (threadIdx.x == 0) stat_add(st + st_index(b, v, STAGE, a.nsrc), part[0], part[1]);
 }
 
 static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspace& ws) {
@@ -1155,6 +1171,8 @@ static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspac
   a.W = g.W;
   a.nsrc = g.nsrc;
   a.box_cap = INT_MAX;
+  a.npl = 1;
+  a.omega_k = 0;
   a.off_ow0 = L.pk_off[P_OW0];
   a.off_ow0t = L.ow0t_off;
   a.off_owb = L.owb_off;
@@ -1202,54 +1220,72 @@ static PipeArgs pipe_args_c8(const CostArgs& ca, const SweepGeom& g, const Works
   return a;
 }
 
-hipError_t launch_cost_x(const CostArgs& ca, const SweepGeom& g, const Workspace& ws, int d,
-                         float* omega_out, hipStream_t s) {
+static void group_strides(PipeArgs& a, const Workspace& ws, int n) {
+  a.npl = n;
+  a.t1_kstride = ws.t1_plane;
+  a.st_kstride = ws.omega_stats_bytes / sizeof(double);
+  a.x_kstride = ws.x_plane;
+}
+
+hipError_t launch_cost_x_group(const CostArgs& ca, const SweepGeom& g, const Workspace& ws, int d0,
+                               int n, float* x0, float* omega_out, int omega_k, hipStream_t s) {
   PipeArgs a = pipe_args_c8(ca, g, ws);
-  a.d_prev = d;
+  group_strides(a, ws, n);
+  a.d_prev = d0;
   a.d_next = -1;
-  a.t1_prev = reinterpret_cast<const float4*>(ws.t1[d & 1]);
-  a.st_prev = ws.omega_stats[d & 1];
+  a.x = x0;
+  a.t1_prev = reinterpret_cast<const float4*>(ws.t1);
+  a.st_prev = ws.omega_stats;
   a.omega_out = omega_out;
+  a.omega_k = omega_out ? omega_k : -1;
   const int ntiles = ((g.W + kTileW - 1) / kTileW) * ((g.H + kXRows - 1) / kXRows);
   ProfScope ps(s, K_COST_X);
-  hipLaunchKernelGGL(cost_x_kernel<2>, dim3(ntiles, g.B), dim3(2 * kXRows * kTileW), 0, s, a, a.params,
-                     a.rel);
+  hipLaunchKernelGGL(cost_x_kernel<2>, dim3(ntiles * n, g.B), dim3(2 * kXRows * kTileW), 0, s, a,
+                     a.params, a.rel);
   return hipGetLastError();
 }
 
-hipError_t launch_omega_next(const CostArgs& ca, const SweepGeom& g, const Workspace& ws, int d,
-                             hipStream_t s) {
+hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Workspace& ws, int d0,
+                              int n, hipStream_t s) {
   PipeArgs a = pipe_args_c8(ca, g, ws);
+  group_strides(a, ws, n);
   a.d_prev = -1;
-  a.d_next = d;
-  a.t1_next = reinterpret_cast<float4*>(ws.t1[d & 1]);
-  a.st_next = ws.omega_stats[d & 1];
+  a.d_next = d0;
+  a.t1_next = reinterpret_cast<float4*>(ws.t1);
+  a.st_next = ws.omega_stats;
   hipError_t e;
+  // the group's statistics accumulate from zero
+  if ((e = hipMemsetAsync(ws.omega_stats, 0, (size_t)n * ws.omega_stats_bytes, s)) != hipSuccess)
+    return e;
   if (omega_variant() == 1) {
     const int ntiles = ((g.W + kTileW - 1) / kTileW) * ((g.H + kTileH - 1) / kTileH);
     ProfScope ps(s, K_OMEGA_CONV);
-    hipLaunchKernelGGL(omega_conv_kernel<kOmegaConvAbl>, dim3(ntiles * g.nsrc, 1, g.B), dim3(kTileThreads), 0, s, a,
-                       a.params, a.rel);
+    hipLaunchKernelGGL(omega_conv_kernel<kOmegaConvAbl>, dim3(ntiles * g.nsrc * n, 1, g.B),
+                       dim3(kTileThreads), 0, s, a, a.params, a.rel);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   } else {
     const int ntiles = ((g.W + kMOutW - 1) / kMOutW) * ((g.H + kMOutH - 1) / kMOutH);
     ProfScope ps(s, K_OMEGA_CONV);
-    hipLaunchKernelGGL(omega_mfma_kernel, dim3(ntiles * g.nsrc, 1, g.B), dim3(kMThreads), 0, s, a,
-                       a.params, a.rel, ws.xbound);
+    hipLaunchKernelGGL(omega_mfma_kernel, dim3(ntiles * g.nsrc * n, 1, g.B), dim3(kMThreads), 0, s,
+                       a, a.params, a.rel, ws.xbound);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  // GN #1 / #2 statistics of plane d
+  // GN #1 / #2 statistics of every plane of the group.  The blocks per (plane, view) must
+  // not depend on n: the fp32 per-thread partial sums follow the grid stride, and a plane's
+  // statistics are bit-identical however the sweep is grouped or split into d_range calls.
   const int HW = g.H * g.W;
   const int pblk =
       std::max(1, std::min((HW + 1023) / 1024, 8 * g.cu_count / std::max(1, g.B * g.nsrc) + 1));
   {
     ProfScope ps(s, K_OMEGA1);
-    hipLaunchKernelGGL(omega_stats_kernel<1>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a, a.params);
+    hipLaunchKernelGGL(omega_stats_kernel<1>, dim3(pblk, g.nsrc, g.B * n), dim3(256), 0, s, a,
+                       a.params);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   {
     ProfScope ps(s, K_OMEGA2);
-    hipLaunchKernelGGL(omega_stats_kernel<2>, dim3(pblk, g.nsrc, g.B), dim3(256), 0, s, a, a.params);
+    hipLaunchKernelGGL(omega_stats_kernel<2>, dim3(pblk, g.nsrc, g.B * n), dim3(256), 0, s, a,
+                       a.params);
   }
   return hipGetLastError();
 }

@@ -102,7 +102,9 @@ def kernel_table(prof: dict, planes: int, B: int, N: int, H: int, W: int):
     rows = {}
     total = sum(ms for _, ms in prof.values()) or 1.0
     for name, (n, ms) in prof.items():
-        per_plane = max(1, round(n / planes))
+        # launches per plane: 1/G for the cost-slice kernels (one launch covers a group of G
+        # planes), 1 for the regulariser's
+        per_plane = n / planes
         kind, amount = algorithmic_work(name, B, N, H, W, per_plane)
         avg_s = ms / n / 1e3
         if kind == "bytes":

@@ -5,13 +5,14 @@
 #include "../../aa-rmvsnet_amd/csrc/warp_cost.hip"
 
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 using namespace aarmvs;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
 int main(int argc, char** argv) {
-  const int B = 1, H = 1184, W = 1600, nsrc = 6, D = 4;
+  const int B = 1, H = 1184, W = 1600, nsrc = 6, D = 16;
   const size_t HW = (size_t)H * W, fn = (size_t)kC * HW;
   std::vector<float> h(fn);
   uint32_t st = 1;
@@ -43,7 +44,8 @@ int main(int argc, char** argv) {
   }
   float *drel, *ddv, *dpar;
   CK(hipMalloc(&drel, rel.size() * 4)); CK(hipMemcpy(drel, rel.data(), rel.size() * 4, hipMemcpyHostToDevice));
-  float dvh[D] = {600.f, 601.f, 602.f, 603.f};
+  float dvh[D];
+  for (int d = 0; d < D; ++d) dvh[d] = 600.f + d;
   CK(hipMalloc(&ddv, sizeof(dvh))); CK(hipMemcpy(ddv, dvh, sizeof(dvh), hipMemcpyHostToDevice));
   size_t pb = aarmvs_packed_param_bytes();
   std::vector<float> ph(pb / 4);
@@ -59,14 +61,14 @@ int main(int argc, char** argv) {
   ca.rel = drel; ca.depth_values = ddv; ca.params = dpar;
   CK(launch_to_c8(feats[0], ws.feat8[0], B, (int)HW, 0));
   for (int v = 0; v < nsrc; ++v) CK(launch_to_c8(feats[v + 1], ws.feat8[v + 1], B, (int)HW, 0));
-  CK(launch_omega_next(ca, g, ws, 0, 0));
+  CK(launch_omega_group(ca, g, ws, 0, 1, 0));
   CK(hipDeviceSynchronize());
   PipeArgs a0 = pipe_args(ca, g, ws);
   a0.d_prev = 0; a0.d_next = 1;
   a0.ref = ws.feat8[0];
   for (int v = 0; v < nsrc; ++v) a0.src[v] = ws.feat8[v + 1];
-  a0.t1_prev = reinterpret_cast<const float4*>(ws.t1[0]); a0.st_prev = ws.omega_stats[0];
-  a0.t1_next = reinterpret_cast<float4*>(ws.t1[1]); a0.st_next = ws.omega_stats[1];
+  a0.t1_prev = reinterpret_cast<const float4*>(ws.t1); a0.st_prev = ws.omega_stats;
+  a0.t1_next = nullptr; a0.st_next = nullptr;
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int tiles_x = (W + kTileW - 1) / kTileW;
   auto run = [&](const char* name, auto kern, dim3 grid, int threads, double bytes) {
@@ -79,26 +81,47 @@ int main(int argc, char** argv) {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     printf("%-36s %8.3f ms  %7.0f GB/s algorithmic\n", name, ms / R, bytes / (ms / R) / 1e6);
   };
-  const dim3 gx(tiles_x * ((H + kXRows - 1) / kXRows), B);
-  const double bx = 128.0 * (nsrc + 2) * HW;
-  run("cost_x", cost_x_kernel<0>, gx, 2 * kXRows * kTileW, bx);
-  run("cost_x pair sample_pos (1)", cost_x_kernel<1>, gx, 2 * kXRows * kTileW, bx);
-  run("cost_x pair omega (2)", cost_x_kernel<2>, gx, 2 * kXRows * kTileW, bx);
-  run("cost_x pair both (3)", cost_x_kernel<3>, gx, 2 * kXRows * kTileW, bx);
-  run("cost_x pair omega, 5 waves/SIMD (6)", cost_x_kernel<6>, gx, 2 * kXRows * kTileW, bx);
-  run("cost_x pair omega, 6 waves/SIMD (10)", cost_x_kernel<10>, gx, 2 * kXRows * kTileW, bx);
-  const dim3 gc(tiles_x * ((H + kTileH - 1) / kTileH) * nsrc, 1, B);
+  // plane batching: one launch over npl planes (per-plane time = launch / npl)
+  const size_t t1k = (size_t)B * nsrc * HW, stk = ws.omega_stats_bytes / 8, xk = (size_t)B * kC * HW;
+  float4* t1b; double* stb; float* xb;
+  CK(hipMalloc(&t1b, 8 * t1k * 16)); CK(hipMalloc(&stb, 8 * stk * 8)); CK(hipMalloc(&xb, 8 * xk * 4));
+  CK(hipMemset(stb, 0, 8 * stk * 8));
+  const int ntm = ((W + kMOutW - 1) / kMOutW) * ((H + kMOutH - 1) / kMOutH);
   const double bc = (128.0 * (nsrc + 1) + 16.0 * nsrc) * HW;
-  run("omega_conv", omega_conv_kernel<0>, gc, kTileThreads, bc);
-  run("omega_conv no conv (1)", omega_conv_kernel<1>, gc, kTileThreads, bc);
-  run("omega_conv no sq (2)", omega_conv_kernel<2>, gc, kTileThreads, bc);
-  run("omega_conv no box loads (4)", omega_conv_kernel<4>, gc, kTileThreads, bc);
-  run("omega_conv no sq/box (6)", omega_conv_kernel<6>, gc, kTileThreads, bc);
-  run("omega_conv skeleton (7)", omega_conv_kernel<7>, gc, kTileThreads, bc);
-  run("omega_conv MFMA off-centre taps (16)", omega_conv_kernel<16>, gc, kTileThreads, bc);
-  run("omega_conv conv rolled (8)", omega_conv_kernel<8>, gc, kTileThreads, bc);
-  a0.box_cap = 64;
-  run("omega_conv (box cap 64: global gathers)", omega_conv_kernel<0>, gc, kTileThreads, bc);
+  const double bx = 128.0 * (nsrc + 2) * HW;
+  for (int npl : {1, 2, 4, 8}) {
+    PipeArgs a = a0;
+    a.npl = npl; a.t1_kstride = t1k; a.st_kstride = stk; a.x_kstride = xk;
+    a.d_next = 1; a.t1_next = t1b; a.st_next = stb;
+    auto om = [&] { hipLaunchKernelGGL(omega_mfma_kernel, dim3(ntm * nsrc * npl, 1, B), dim3(kMThreads), 0, 0, a, dpar, drel, ws.xbound); };
+    for (int i = 0; i < 2; ++i) om();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 10; ++i) om();
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("omega_mfma npl=%d  %8.3f ms/plane  %7.0f GB/s algorithmic\n", npl, ms / 10 / npl, bc * npl / (ms / 10) / 1e6);
+    // plane npl-1 must equal a single-plane launch at d_next = npl
+    if (npl > 1) {
+      std::vector<float4> hb(t1k), hs(t1k);
+      CK(hipMemcpy(hb.data(), t1b + (npl - 1) * t1k, t1k * 16, hipMemcpyDeviceToHost));
+      PipeArgs a1 = a; a1.npl = 1; a1.d_next = npl;
+      hipLaunchKernelGGL(omega_mfma_kernel, dim3(ntm * nsrc, 1, B), dim3(kMThreads), 0, 0, a1, dpar, drel, ws.xbound);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(hs.data(), t1b, t1k * 16, hipMemcpyDeviceToHost));
+      printf("  plane %d vs single launch: %s\n", npl - 1, memcmp(hb.data(), hs.data(), t1k * 16) ? "DIFFERENT" : "identical");
+    }
+    PipeArgs c = a0;
+    c.npl = npl; c.t1_kstride = 0; c.st_kstride = 0; c.x_kstride = xk; c.x = xb; c.omega_k = -1;
+    auto cx = [&] { hipLaunchKernelGGL(cost_x_kernel<2>, dim3(tiles_x * ((H + kXRows - 1) / kXRows) * npl, B), dim3(2 * kXRows * kTileW), 0, 0, c, dpar, drel); };
+    for (int i = 0; i < 2; ++i) cx();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 10; ++i) cx();
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("cost_x npl=%d      %8.3f ms/plane  %7.0f GB/s algorithmic\n", npl, ms / 10 / npl, bx * npl / (ms / 10) / 1e6);
+  }
   {
     CK(hipEventRecord(e0));
     for (int i = 0; i < 10; ++i) CK(launch_to_c8(feats[0], ws.feat8[0], B, (int)HW, 0));
