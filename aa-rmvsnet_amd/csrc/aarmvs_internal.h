@@ -16,7 +16,7 @@ constexpr float kGnEps = 1e-5f; // nn.GroupNorm default eps
 // The sweep computes cost slices in groups of up to kPlaneGroup planes: one launch of each
 // cost-slice kernel covers the group, so the neighbouring planes' bilinear footprints (and
 // the reference tile) are fetched from HBM once and re-read from L2.
-constexpr int kPlaneGroup = 8;
+constexpr int kPlaneGroup = 16;
 
 // ---------------------------------------------------------------------------
 // Parameter tensors, in raw-blob order (aarmvs.h).
@@ -71,7 +71,10 @@ const ParamLayout& param_layout();
 // ---------------------------------------------------------------------------
 struct Workspace {
   double* omega_stats;    // [kPlaneGroup][B][nsrc][3][kSlots][2] omega GN statistics per group plane
+  double* omega_part;     // [kPlaneGroup][B][nsrc][omega_part_n][2] per-block GN partial sums
+  int omega_part_n;       // partials per (plane, b, view): >= omega tiles, >= statistics blocks
   double* reg_stats;      // [B][2 deconvs][2 groups][kSlots][2] U-Net GN statistics
+  double* reg_part;       // [B][deconv blocks][4] a deconv's per-block GN partials (one deconv at a time)
   unsigned* xbound;       // float bits of an upper bound on |x| (cost slice) for this sweep:
                           // 8 max|feature|^2 (to_c8) or max|x| (unet_step); cell 0's fp16 range
   float* max_prob;        // [B,HW]

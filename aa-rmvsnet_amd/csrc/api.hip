@@ -157,6 +157,14 @@ Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
   ws.x = ws.xg[0];
   for (int v = 0; v <= nsrc; ++v) ws.feat8[v] = reinterpret_cast<float*>(take(B * kC * HW * 4));
   ws.t1 = reinterpret_cast<float*>(take(kPlaneGroup * ws.t1_plane * 16));
+  // one partial per omega block (haloed 16 x 32 tiles: 14 x 30 outputs; the VALU variant's
+  // 16 x 32 output tiles are fewer) or statistics block (<= one per 1024 pixels)
+  ws.omega_part_n = (int)std::max(((size_t)(W + 29) / 30) * ((size_t)(H + 13) / 14), (HW + 1023) / 1024);
+  ws.omega_part = reinterpret_cast<double*>(
+      take((size_t)kPlaneGroup * B * nsrc * ws.omega_part_n * 2 * sizeof(double)));
+  // deconv_1's blocks (8 x 32 tiles of its H/2 x W/2 input) outnumber deconv_0's
+  ws.reg_part = reinterpret_cast<double*>(
+      take((size_t)B * ((W / 2 + 31) / 32) * ((H / 2 + 7) / 8) * 4 * sizeof(double)));
   ws.u0 = reinterpret_cast<float*>(take(B * 16 * HW2 * 4));
   ws.u1 = reinterpret_cast<float*>(take(B * 16 * HW * 4));
   const size_t state_begin = off;

@@ -642,8 +642,7 @@ __global__ void __launch_bounds__(256) deconv_px_kernel(const float* __restrict_
                                                         const float* __restrict__ w,
                                                         const float* __restrict__ bias, int Hi,
                                                         int Wi, float* __restrict__ out,
-                                                        double* __restrict__ stats,
-                                                        int stats_bstride) {
+                                                        double* __restrict__ gn_part) {
   constexpr int SH = kDpTH + 1, SW = kDpTW + 1;   // the tile + its bottom / right neighbours
   __shared__ float tin[16][SH][SW];               // [ci][y][x] (row stride 33: conflict-free)
   __shared__ float red[4 * 4];
@@ -707,10 +706,43 @@ __global__ void __launch_bounds__(256) deconv_px_kernel(const float* __restrict_
     }
   }
   block_sum<4>(part, red);
+  // this block's GroupNorm partials (groups of 8 channels: sum, sumsq), reduced in a fixed
+  // order by gn_reduce_kernel: statistics independent of block timing
   if (tid == 0) {
+    double* pp = gn_part + 4 * (((size_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pp[j] = part[j];
+  }
+}
+
+// GroupNorm statistics of one deconv output per batch element (blockIdx.x) from its
+// deconv_px blocks' partials: strided sequential sums, then a fixed tree; the result goes
+// to slot 0 of each group's statistic (the other slots are zero).
+__global__ void __launch_bounds__(256) gn_reduce_kernel(const double* __restrict__ part, int nblk,
+                                                        double* __restrict__ stats,
+                                                        int stats_bstride) {
+  __shared__ double red[4][256];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const double* pp = part + 4 * (size_t)b * nblk;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int i = t; i < nblk; i += 256)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += pp[4 * i + j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[j][t] = acc[j];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[j][t] += red[j][t + o];
+    __syncthreads();
+  }
+  if (t == 0) {
     double* st = stats + (size_t)b * stats_bstride;
-    stat_add(st, part[0], part[1]);
-    stat_add(st + kSlots * 2, part[2], part[3]);
+    st[0] = red[0][0];
+    st[1] = red[1][0];
+    st[kSlots * 2] = red[2][0];
+    st[kSlots * 2 + 1] = red[3][0];
   }
 }
 
@@ -951,9 +983,12 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   {
     const int Hi = H / 4, Wi = W / 4;
     ProfScope ps(s, K_DECONV0);
-    hipLaunchKernelGGL(deconv_px_kernel, dim3((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B),
-                       dim3(256), 0, s, ws.h[2][nxt], params + L.dct_off[0], params + L.pk_off[P_D0B],
-                       Hi, Wi, ws.u0, ws.reg_stats + reg_stat_index(0, 0, 0),
+    const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
+    hipLaunchKernelGGL(deconv_px_kernel, grid, dim3(256), 0, s, ws.h[2][nxt], params + L.dct_off[0],
+                       params + L.pk_off[P_D0B], Hi, Wi, ws.u0, ws.reg_part);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(gn_reduce_kernel, dim3(B), dim3(256), 0, s, ws.reg_part, (int)(grid.x * grid.y),
+                       ws.reg_stats + reg_stat_index(0, 0, 0),
                        (int)(reg_stat_index(1, 0, 0) - reg_stat_index(0, 0, 0)));
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
@@ -975,9 +1010,12 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   {
     const int Hi = H / 2, Wi = W / 2;
     ProfScope ps(s, K_DECONV1);
-    hipLaunchKernelGGL(deconv_px_kernel, dim3((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B),
-                       dim3(256), 0, s, ws.h[3][nxt], params + L.dct_off[1], params + L.pk_off[P_D1B],
-                       Hi, Wi, ws.u1, ws.reg_stats + reg_stat_index(0, 1, 0),
+    const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
+    hipLaunchKernelGGL(deconv_px_kernel, grid, dim3(256), 0, s, ws.h[3][nxt], params + L.dct_off[1],
+                       params + L.pk_off[P_D1B], Hi, Wi, ws.u1, ws.reg_part);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(gn_reduce_kernel, dim3(B), dim3(256), 0, s, ws.reg_part, (int)(grid.x * grid.y),
+                       ws.reg_stats + reg_stat_index(0, 1, 0),
                        (int)(reg_stat_index(1, 1, 0) - reg_stat_index(0, 1, 0)));
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

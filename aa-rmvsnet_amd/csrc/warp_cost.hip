@@ -189,7 +189,19 @@ struct PipeArgs {
   size_t st_kstride;          // doubles
   size_t x_kstride;           // floats
   int omega_k;                // cost_x: the plane (0 .. npl-1) whose omega weights go to omega_out
+  // GroupNorm partial sums: one (sum, sumsq) per producing block, [npl][B][nsrc][part_n],
+  // reduced in a fixed order by stat_reduce_kernel (deterministic statistics, independent of
+  // the launch's grouping and of block timing)
+  double* part;
+  int part_n;
 };
+
+__device__ __forceinline__ void part_put(const PipeArgs& a, int kp, int b, int v, int i, double s,
+                                         double ss) {
+  const size_t k = (((size_t)kp * a.B + b) * a.nsrc + v) * a.part_n + i;
+  a.part[2 * k] = s;
+  a.part[2 * k + 1] = ss;
+}
 
 // omega pointwise chain helpers (ResnetBlockGn, module.py:252-264)
 struct OmegaP {
@@ -877,7 +889,7 @@ omega_conv_kernel(PipeArgs a,
       s0 += wsum[w][0];
       s1 += wsum[w][1];
     }
-    stat_add(a.st_next + kp * a.st_kstride + st_index(b, v, 0, nsrc), s0, s1);
+    part_put(a, kp, b, v, tile, s0, s1);
   }
 }
 
@@ -909,6 +921,11 @@ constexpr int kMOutH = kMTileH - 2, kMOutW = kMTileW - 2;                  // ou
 constexpr int kMYStride = 36;                                               // floats per pixel in Y
 constexpr int kMBoxPx = 1024;
 
+// ABL: ablation bits for the diagnostic harness only (tools/microbench/pipe_bench.cpp; the
+// library instantiates ABL = 0): 1 no MFMAs, 2 no box DMA, 4 no box sampling, 8 no reference
+// loads, 16 sampling positions without the homography divisions (the own pixel), 32 no Y
+// image / gather (t1 from the accumulators), 64 no statistics atomics, 128 no B-fragment loads
+template <int ABL = 0>
 __global__ void __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(4)))
 omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restrict__ Rel,
                   const unsigned* __restrict__ xbound) {
@@ -934,7 +951,13 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
   const bool in_img = gy >= 0 && gy < H && gx >= 0 && gx < W;
   const bool interior = in_img && hy >= 1 && hy <= kMOutH && hx >= 1 && hx <= kMOutW;
+  // DB (ABL bit 256): two box buffers (chunk c+1's DMA in flight while chunk c is sampled;
+  // both fit in the Y image's space)
+  constexpr bool DB = (ABL & 256) != 0;
+  constexpr int kBoxFl = (kMBoxPx + 1) * 8;
+  static_assert(!DB || 2 * kBoxFl <= YFL, "two boxes fit in the Y image space");
   if (tid < 8) box[kMBoxPx * 8 + tid] = 0.f;   // the zero pixel
+  if (DB && tid < 8) box[kBoxFl + kMBoxPx * 8 + tid] = 0.f;
 
   const float dep = a.dvals[b * a.D + a.d_next + kp];
   const float* __restrict__ m = Rel + 12 * (v * a.B + b);
@@ -945,7 +968,14 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   TapF tf{};
   int lx = INT_MAX, ly = INT_MAX, bhx = INT_MIN, bhy = INT_MIN;
   if (in_img) {
-    tf = tap_f(m, dep, gx, gy, H, W);
+    if constexpr ((ABL & 16) != 0) {
+      tf.xf = (float)gx + 0.25f * dep * 1e-3f;
+      tf.yf = (float)gy;
+      tf.wt[0] = tf.wt[1] = tf.wt[2] = tf.wt[3] = 0.25f;
+      tf.xf = floorf(tf.xf);
+    } else {
+      tf = tap_f(m, dep, gx, gy, H, W);
+    }
     box_extend(tf, H, W, lx, ly, bhx, bhy);
   }
   const Box bx = box_reduce(lx, ly, bhx, bhy, red);
@@ -966,7 +996,8 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     const uint32_t cb = (uint32_t)c * cbytes;
 #pragma unroll
     for (int j = 0; j < NB; ++j)
-      if (tid + j * kMThreads < items) dma16(rsrc, box + (j * kMThreads + wave * 64) * 4, boff[j] + cb);
+      if (!(ABL & 2) && tid + j * kMThreads < items)
+        dma16(rsrc, box + (DB && (c & 1) ? kBoxFl : 0) + (j * kMThreads + wave * 64) * 4, boff[j] + cb);
   };
   // this lane's reference pixel in the c8 image (past the buffer: zeros)
   const uint32_t rpix = in_img ? (uint32_t)(gy * W + gx) : fbytes / 32u;
@@ -993,13 +1024,17 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   __syncthreads();
 #pragma unroll 1
   for (int c = 0; c < 4; ++c) {
+    if (DB && c < 3) stage(c + 1);   // the other buffer: last read in chunk c - 1
+    const float* const bx_c = box + (DB && (c & 1) ? kBoxFl : 0);
     // sample the own pixel (8 channels) and form sq
     float4 g0, g1;
-    if (lds) {
-      g0 = bil4(img_ld(box, tp.pix[0], 0), img_ld(box, tp.pix[1], 0), img_ld(box, tp.pix[2], 0),
-                img_ld(box, tp.pix[3], 0), tp);
-      g1 = bil4(img_ld(box, tp.pix[0], 1), img_ld(box, tp.pix[1], 1), img_ld(box, tp.pix[2], 1),
-                img_ld(box, tp.pix[3], 1), tp);
+    if (ABL & 4) {
+      g0 = g1 = make_float4(tp.wt[0], tp.wt[1], tp.wt[2], tp.wt[3]);
+    } else if (lds) {
+      g0 = bil4(img_ld(bx_c, tp.pix[0], 0), img_ld(bx_c, tp.pix[1], 0), img_ld(bx_c, tp.pix[2], 0),
+                img_ld(bx_c, tp.pix[3], 0), tp);
+      g1 = bil4(img_ld(bx_c, tp.pix[0], 1), img_ld(bx_c, tp.pix[1], 1), img_ld(bx_c, tp.pix[2], 1),
+                img_ld(bx_c, tp.pix[3], 1), tp);
     } else {
       g0 = bil4(ld_c8(rsrc, tp.pix[0], 2 * c, HW), ld_c8(rsrc, tp.pix[1], 2 * c, HW),
                 ld_c8(rsrc, tp.pix[2], 2 * c, HW), ld_c8(rsrc, tp.pix[3], 2 * c, HW), tp);
@@ -1008,12 +1043,14 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     }
     const float4 s0 = sqdiff4(g0, rf0), s1 = sqdiff4(g1, rf1);
     const float sq[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    if (c < 3) {   // the next chunk's reference pixel, in flight during this chunk
+    if (c < 3 && !(ABL & 8)) {   // the next chunk's reference pixel, in flight during this chunk
       rf0 = ld_c8(rref, rpix, 2 * c + 2, HW);
       rf1 = ld_c8(rref, rpix, 2 * c + 3, HW);
     }
-    __syncthreads();   // every lane's box reads of chunk c are done
-    if (c < 3) stage(c + 1);
+    if (!DB) {
+      __syncthreads();   // every lane's box reads of chunk c are done
+      if (c < 3) stage(c + 1);
+    }
     // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel, fp32
     {
       const float* wt = w0t + (4 * kC + 8 * c) * 4;
@@ -1043,19 +1080,32 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     }
     const half8 A0 = __builtin_bit_cast(half8, u32x4{hw[0], hw[1], hw[2], hw[3]});
     const half8 A1 = __builtin_bit_cast(half8, u32x4{lw[0], lw[1], lw[2], lw[3]});
-    const half8 Bd = owm[(c * 2 + 0) * 64 + lane], Bl = owm[(c * 2 + 1) * 64 + lane];
-    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl, acc1, 0, 0, 0);
+    half8 Bd, Bl;
+    if constexpr ((ABL & 128) != 0) {
+      Bd = A1;
+      Bl = A0;
+    } else {
+      Bd = owm[(c * 2 + 0) * 64 + lane];
+      Bl = owm[(c * 2 + 1) * 64 + lane];
+    }
+    if (!(ABL & 1)) {
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl, acc1, 0, 0, 0);
+    } else {
+      acc0[0] += (float)A0[0] + (float)Bd[1];
+      acc1[0] += (float)A1[0] + (float)Bl[1];
+    }
     if (c < 3) {
       dma_wait();
-      __syncthreads();   // chunk c+1's box visible
+      __syncthreads();   // chunk c+1's box visible (DB: and chunk c's buffer free)
     }
   }
+  if (DB) __syncthreads();   // chunk 3's box reads done before Y overwrites the boxes
   // Y image (over the box space: every lane passed chunk 3's box reads before the barrier
   // above): D[row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)][col = lane & 31] of row group g
-  {
+  if constexpr ((ABL & 32) == 0) {
     const int col = lane & 31, rb = 4 * (lane >> 5);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -1068,6 +1118,12 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   float ps = 0.f, pss = 0.f;
   if (interior) {
     float g4[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr ((ABL & 32) != 0) {
+      g4[0] = acc0[0] + acc1[1];
+      g4[1] = acc0[2] + acc1[3];
+      g4[2] = acc0[4] + acc1[5];
+      g4[3] = acc0[6] + acc1[7];
+    } else {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int tap = u < 4 ? u : u + 1;
@@ -1077,6 +1133,7 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
       g4[1] += yv.y;
       g4[2] += yv.z;
       g4[3] += yv.w;
+    }
     }
     const float isc = P[a.off_owm_scale] * ldexpf(1.0f, e);
     const float* __restrict__ b0 = P + a.off_ob0;
@@ -1102,7 +1159,7 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
       s0 += wsum[w][0];
       s1 += wsum[w][1];
     }
-    stat_add(a.st_next + kp * a.st_kstride + st_index(b, v, 0, nsrc), s0, s1);
+    if (!(ABL & 64)) part_put(a, kp, b, v, tile, s0, s1);
   }
 }
 
@@ -1153,7 +1210,36 @@ __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
     }
   }
   block_sum<2>(part, red);
-  if (threadIdx.x == 0) stat_add(st + st_index(b, v, STAGE, a.nsrc), part[0], part[1]);
+  if (threadIdx.x == 0) part_put(a, kp, b, v, blockIdx.x, part[0], part[1]);
+}
+
+// Statistic STAGE of every (plane, batch element, view) of a group from the per-block
+// partials: one block per (plane, b, v), each thread a strided sequential sum, then a fixed
+// tree; the result goes to slot 0 of the statistic (the other slots stay zero).
+__global__ void __launch_bounds__(256) stat_reduce_kernel(PipeArgs a, int stage) {
+  __shared__ double red[2][256];
+  const int g = blockIdx.x, v = g % a.nsrc, b = (g / a.nsrc) % a.B, kp = g / (a.nsrc * a.B);
+  const double* pp = a.part + 2 * (size_t)g * a.part_n;
+  double s = 0.0, ss = 0.0;
+  for (int i = threadIdx.x; i < a.part_n; i += 256) {
+    s += pp[2 * i];
+    ss += pp[2 * i + 1];
+  }
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = ss;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double* st = a.st_next + kp * a.st_kstride + st_index(b, v, stage, a.nsrc);
+    st[0] = red[0][0];
+    st[1] = red[1][0];
+  }
 }
 
 static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspace& ws) {
@@ -1253,40 +1339,51 @@ hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Work
   a.d_next = d0;
   a.t1_next = reinterpret_cast<float4*>(ws.t1);
   a.st_next = ws.omega_stats;
+  a.part = ws.omega_part;
   hipError_t e;
+  const int nred = n * g.B * g.nsrc;   // reduce blocks
   // the group's statistics accumulate from zero
   if ((e = hipMemsetAsync(ws.omega_stats, 0, (size_t)n * ws.omega_stats_bytes, s)) != hipSuccess)
     return e;
   if (omega_variant() == 1) {
     const int ntiles = ((g.W + kTileW - 1) / kTileW) * ((g.H + kTileH - 1) / kTileH);
     ProfScope ps(s, K_OMEGA_CONV);
+    a.part_n = ntiles;
     hipLaunchKernelGGL(omega_conv_kernel<kOmegaConvAbl>, dim3(ntiles * g.nsrc * n, 1, g.B),
                        dim3(kTileThreads), 0, s, a, a.params, a.rel);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   } else {
     const int ntiles = ((g.W + kMOutW - 1) / kMOutW) * ((g.H + kMOutH - 1) / kMOutH);
     ProfScope ps(s, K_OMEGA_CONV);
-    hipLaunchKernelGGL(omega_mfma_kernel, dim3(ntiles * g.nsrc * n, 1, g.B), dim3(kMThreads), 0, s,
+    a.part_n = ntiles;
+    hipLaunchKernelGGL(omega_mfma_kernel<0>, dim3(ntiles * g.nsrc * n, 1, g.B), dim3(kMThreads), 0, s,
                        a, a.params, a.rel, ws.xbound);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
+  hipLaunchKernelGGL(stat_reduce_kernel, dim3(nred), dim3(256), 0, s, a, 0);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   // GN #1 / #2 statistics of every plane of the group.  The blocks per (plane, view) must
   // not depend on n: the fp32 per-thread partial sums follow the grid stride, and a plane's
   // statistics are bit-identical however the sweep is grouped or split into d_range calls.
   const int HW = g.H * g.W;
   const int pblk =
       std::max(1, std::min((HW + 1023) / 1024, 8 * g.cu_count / std::max(1, g.B * g.nsrc) + 1));
+  a.part_n = pblk;
   {
     ProfScope ps(s, K_OMEGA1);
     hipLaunchKernelGGL(omega_stats_kernel<1>, dim3(pblk, g.nsrc, g.B * n), dim3(256), 0, s, a,
                        a.params);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(stat_reduce_kernel, dim3(nred), dim3(256), 0, s, a, 1);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   {
     ProfScope ps(s, K_OMEGA2);
     hipLaunchKernelGGL(omega_stats_kernel<2>, dim3(pblk, g.nsrc, g.B * n), dim3(256), 0, s, a,
                        a.params);
   }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(stat_reduce_kernel, dim3(nred), dim3(256), 0, s, a, 2);
   return hipGetLastError();
 }
 

@@ -64,6 +64,7 @@ int main(int argc, char** argv) {
   CK(launch_omega_group(ca, g, ws, 0, 1, 0));
   CK(hipDeviceSynchronize());
   PipeArgs a0 = pipe_args(ca, g, ws);
+  a0.part = ws.omega_part; a0.part_n = ws.omega_part_n;   // GN partials (npl <= kPlaneGroup)
   a0.d_prev = 0; a0.d_next = 1;
   a0.ref = ws.feat8[0];
   for (int v = 0; v < nsrc; ++v) a0.src[v] = ws.feat8[v + 1];
@@ -81,6 +82,20 @@ int main(int argc, char** argv) {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     printf("%-36s %8.3f ms  %7.0f GB/s algorithmic\n", name, ms / R, bytes / (ms / R) / 1e6);
   };
+  // omega_mfma ablations at npl = 8 (tools: what bounds the kernel)
+  auto ablate = [&](const char* name, auto kern, float4* t1o, double* sto) {
+    PipeArgs a = a0;
+    a.npl = 8; a.t1_kstride = (size_t)B * nsrc * HW; a.st_kstride = ws.omega_stats_bytes / 8;
+    a.d_next = 1; a.t1_next = t1o; a.st_next = sto;
+    const int ntm = ((W + kMOutW - 1) / kMOutW) * ((H + kMOutH - 1) / kMOutH);
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, dim3(ntm * nsrc * 8, 1, B), dim3(kMThreads), 0, 0, a, dpar, drel, ws.xbound);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(kern, dim3(ntm * nsrc * 8, 1, B), dim3(kMThreads), 0, 0, a, dpar, drel, ws.xbound);
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("omega_mfma npl=8 %-34s %8.3f ms/plane\n", name, ms / 5 / 8);
+  };
   // plane batching: one launch over npl planes (per-plane time = launch / npl)
   const size_t t1k = (size_t)B * nsrc * HW, stk = ws.omega_stats_bytes / 8, xk = (size_t)B * kC * HW;
   float4* t1b; double* stb; float* xb;
@@ -93,7 +108,7 @@ int main(int argc, char** argv) {
     PipeArgs a = a0;
     a.npl = npl; a.t1_kstride = t1k; a.st_kstride = stk; a.x_kstride = xk;
     a.d_next = 1; a.t1_next = t1b; a.st_next = stb;
-    auto om = [&] { hipLaunchKernelGGL(omega_mfma_kernel, dim3(ntm * nsrc * npl, 1, B), dim3(kMThreads), 0, 0, a, dpar, drel, ws.xbound); };
+    auto om = [&] { hipLaunchKernelGGL(omega_mfma_kernel<0>, dim3(ntm * nsrc * npl, 1, B), dim3(kMThreads), 0, 0, a, dpar, drel, ws.xbound); };
     for (int i = 0; i < 2; ++i) om();
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
@@ -101,12 +116,37 @@ int main(int argc, char** argv) {
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     printf("omega_mfma npl=%d  %8.3f ms/plane  %7.0f GB/s algorithmic\n", npl, ms / 10 / npl, bc * npl / (ms / 10) / 1e6);
+    if (npl == 8) {
+      {
+        std::vector<float4> h0(8 * t1k), h1(8 * t1k);
+        CK(hipMemcpy(h0.data(), t1b, 8 * t1k * 16, hipMemcpyDeviceToHost));
+        ablate("double-buffered box (256)", omega_mfma_kernel<256>, t1b, stb);
+        CK(hipMemcpy(h1.data(), t1b, 8 * t1k * 16, hipMemcpyDeviceToHost));
+        printf("  DB t1 vs default: %s\n", memcmp(h0.data(), h1.data(), 8 * t1k * 16) ? "DIFFERENT" : "identical");
+      }
+      ablate("no MFMA (1)", omega_mfma_kernel<1>, t1b, stb);
+      ablate("no box DMA (2)", omega_mfma_kernel<2>, t1b, stb);
+      ablate("no sampling (4)", omega_mfma_kernel<4>, t1b, stb);
+      ablate("no ref loads (8)", omega_mfma_kernel<8>, t1b, stb);
+      ablate("no divisions (16)", omega_mfma_kernel<16>, t1b, stb);
+      ablate("double-buffered box (256)", omega_mfma_kernel<256>, t1b, stb);
+      ablate("double-buffered box, no Y image (288)", omega_mfma_kernel<288>, t1b, stb);
+      ablate("no DMA, no sampling (6)", omega_mfma_kernel<6>, t1b, stb);
+      ablate("no DMA/sampling/MFMA/ref (15)", omega_mfma_kernel<15>, t1b, stb);
+      ablate("skeleton (31)", omega_mfma_kernel<31>, t1b, stb);
+      ablate("skeleton, no Y image (63)", omega_mfma_kernel<63>, t1b, stb);
+      ablate("skeleton, no stats atomics (95)", omega_mfma_kernel<95>, t1b, stb);
+      ablate("skeleton, no B loads (159)", omega_mfma_kernel<159>, t1b, stb);
+      ablate("skeleton - Y/atomics/B (255)", omega_mfma_kernel<255>, t1b, stb);
+      ablate("no Y image (32)", omega_mfma_kernel<32>, t1b, stb);
+      ablate("no B loads (128)", omega_mfma_kernel<128>, t1b, stb);
+    }
     // plane npl-1 must equal a single-plane launch at d_next = npl
     if (npl > 1) {
       std::vector<float4> hb(t1k), hs(t1k);
       CK(hipMemcpy(hb.data(), t1b + (npl - 1) * t1k, t1k * 16, hipMemcpyDeviceToHost));
       PipeArgs a1 = a; a1.npl = 1; a1.d_next = npl;
-      hipLaunchKernelGGL(omega_mfma_kernel, dim3(ntm * nsrc, 1, B), dim3(kMThreads), 0, 0, a1, dpar, drel, ws.xbound);
+      hipLaunchKernelGGL(omega_mfma_kernel<0>, dim3(ntm * nsrc, 1, B), dim3(kMThreads), 0, 0, a1, dpar, drel, ws.xbound);
       CK(hipDeviceSynchronize());
       CK(hipMemcpy(hs.data(), t1b, t1k * 16, hipMemcpyDeviceToHost));
       printf("  plane %d vs single launch: %s\n", npl - 1, memcmp(hb.data(), hs.data(), t1k * 16) ? "DIFFERENT" : "identical");
