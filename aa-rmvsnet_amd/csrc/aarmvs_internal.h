@@ -166,8 +166,8 @@ int cu_count();
 enum KernelId : int {
   K_COST_X, K_OMEGA_CONV, K_FUSION, K_OMEGA1, K_OMEGA2,
   K_CELL0, K_CELL1, K_CELL2, K_CELL3, K_CELL4,
-  K_DECONV0, K_DECONV1, K_HEAD_WTA, K_FINALIZE, K_SOFTMAX, K_WARP, K_TO_C8,
-  K_COUNT
+  K_DECONV0, K_DECONV1, K_HEAD_WTA, K_FINALIZE, K_SOFTMAX, K_WARP, K_TO_C8, K_STAT_REDUCE,
+  K_GN_REDUCE, K_COUNT
 };
 extern bool g_prof_on;
 void prof_mark(hipStream_t s, int id, bool begin);

@@ -79,7 +79,8 @@ static long long g_prof_n[K_COUNT];
 static const char* kKernelNames[K_COUNT] = {
     "cost_x", "omega_conv", "fusion", "omega_stats1", "omega_stats2",
     "lstm_cell0", "lstm_cell1", "lstm_cell2", "lstm_cell3", "lstm_cell4",
-    "deconv0", "deconv1", "head_wta", "finalize", "softmax_depth", "homo_warp", "to_c8"};
+    "deconv0", "deconv1", "head_wta", "finalize", "softmax_depth", "homo_warp", "to_c8",
+    "omega_stat_reduce", "gn_reduce"};
 
 static hipEvent_t prof_event() {
   if (g_prof_used == g_prof_pool.size()) {

@@ -982,11 +982,14 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
   {
     const int Hi = H / 4, Wi = W / 4;
-    ProfScope ps(s, K_DECONV0);
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
-    hipLaunchKernelGGL(deconv_px_kernel, grid, dim3(256), 0, s, ws.h[2][nxt], params + L.dct_off[0],
-                       params + L.pk_off[P_D0B], Hi, Wi, ws.u0, ws.reg_part);
+    {
+      ProfScope ps(s, K_DECONV0);
+      hipLaunchKernelGGL(deconv_px_kernel, grid, dim3(256), 0, s, ws.h[2][nxt], params + L.dct_off[0],
+                         params + L.pk_off[P_D0B], Hi, Wi, ws.u0, ws.reg_part);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    ProfScope pr(s, K_GN_REDUCE);
     hipLaunchKernelGGL(gn_reduce_kernel, dim3(B), dim3(256), 0, s, ws.reg_part, (int)(grid.x * grid.y),
                        ws.reg_stats + reg_stat_index(0, 0, 0),
                        (int)(reg_stat_index(1, 0, 0) - reg_stat_index(0, 0, 0)));
@@ -1009,11 +1012,14 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // deconv_1: h3' (H/2) -> u1 (H) + GN stats
   {
     const int Hi = H / 2, Wi = W / 2;
-    ProfScope ps(s, K_DECONV1);
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
-    hipLaunchKernelGGL(deconv_px_kernel, grid, dim3(256), 0, s, ws.h[3][nxt], params + L.dct_off[1],
-                       params + L.pk_off[P_D1B], Hi, Wi, ws.u1, ws.reg_part);
+    {
+      ProfScope ps(s, K_DECONV1);
+      hipLaunchKernelGGL(deconv_px_kernel, grid, dim3(256), 0, s, ws.h[3][nxt], params + L.dct_off[1],
+                         params + L.pk_off[P_D1B], Hi, Wi, ws.u1, ws.reg_part);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    ProfScope pr(s, K_GN_REDUCE);
     hipLaunchKernelGGL(gn_reduce_kernel, dim3(B), dim3(256), 0, s, ws.reg_part, (int)(grid.x * grid.y),
                        ws.reg_stats + reg_stat_index(0, 1, 0),
                        (int)(reg_stat_index(1, 1, 0) - reg_stat_index(0, 1, 0)));

@@ -1360,7 +1360,10 @@ hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Work
                        a, a.params, a.rel, ws.xbound);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(stat_reduce_kernel, dim3(nred), dim3(256), 0, s, a, 0);
+  {
+    ProfScope ps(s, K_STAT_REDUCE);
+    hipLaunchKernelGGL(stat_reduce_kernel, dim3(nred), dim3(256), 0, s, a, 0);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // GN #1 / #2 statistics of every plane of the group.  The blocks per (plane, view) must
   // not depend on n: the fp32 per-thread partial sums follow the grid stride, and a plane's
@@ -1375,7 +1378,10 @@ hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Work
                        a.params);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(stat_reduce_kernel, dim3(nred), dim3(256), 0, s, a, 1);
+  {
+    ProfScope ps(s, K_STAT_REDUCE);
+    hipLaunchKernelGGL(stat_reduce_kernel, dim3(nred), dim3(256), 0, s, a, 1);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   {
     ProfScope ps(s, K_OMEGA2);
@@ -1383,7 +1389,10 @@ hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Work
                        a.params);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(stat_reduce_kernel, dim3(nred), dim3(256), 0, s, a, 2);
+  {
+    ProfScope ps(s, K_STAT_REDUCE);
+    hipLaunchKernelGGL(stat_reduce_kernel, dim3(nred), dim3(256), 0, s, a, 2);
+  }
   return hipGetLastError();
 }
 

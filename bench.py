@@ -451,7 +451,8 @@ def main():
                         timing=f"separate pass, {prof_steps} step(s), one stream, hipEvents per launch")
         # the warp + aggregation path as a whole (every launch that produces the cost
         # slice): 128*(N+1) algorithmic B/hyp over the summed device time of its kernels
-        group = [k for k in ("cost_x", "omega_conv", "omega_stats1", "omega_stats2") if k in prof]
+        group = [k for k in ("cost_x", "omega_conv", "omega_stats1", "omega_stats2", "omega_stat_reduce")
+                 if k in prof]
         if group:
             ms = sum(prof[k][1] for k in group)
             planes = D * prof_steps
