@@ -638,6 +638,9 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
 // segment, a partial last segment per row): 84 / 47 us per plane at the headline geometry
 // against 71 / 37 us here (profiles/r02_*).
 constexpr int kDpTH = 8, kDpTW = 32;
+// ABL: ablation bits for tools/microbench/cell_bench only (the library instantiates 0):
+// 1 no output stores, 2 no channel loop, 4 no input staging loads
+template <int ABL = 0>
 __global__ void __launch_bounds__(256) deconv_px_kernel(const float* __restrict__ in,
                                                         const float* __restrict__ w,
                                                         const float* __restrict__ bias, int Hi,
@@ -645,6 +648,7 @@ __global__ void __launch_bounds__(256) deconv_px_kernel(const float* __restrict_
                                                         double* __restrict__ gn_part) {
   constexpr int SH = kDpTH + 1, SW = kDpTW + 1;   // the tile + its bottom / right neighbours
   __shared__ float tin[16][SH][SW];               // [ci][y][x] (row stride 33: conflict-free)
+  __shared__ float4 wsh[16 * 9 * 4];              // weights [ci][tap][co / 4] (broadcast reads)
   __shared__ float red[4 * 4];
   const int b = blockIdx.z, tid = threadIdx.x;
   const int y0 = blockIdx.y * kDpTH, x0 = blockIdx.x * kDpTW;
@@ -658,31 +662,44 @@ __global__ void __launch_bounds__(256) deconv_px_kernel(const float* __restrict_
     const int c4 = i & 3, px = i >> 2, yy = px / SW, xx = px - yy * SW;
     const int gy = y0 + yy, gx = x0 + xx;
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);   // zero padding past the image
-    if (gy < Hi && gx < Wi) q = *reinterpret_cast<const float4*>(ib + ((size_t)gy * Wi + gx) * 16 + 4 * c4);
+    if (!(ABL & 4) && gy < Hi && gx < Wi)
+      q = *reinterpret_cast<const float4*>(ib + ((size_t)gy * Wi + gx) * 16 + 4 * c4);
     tin[4 * c4 + 0][yy][xx] = q.x;
     tin[4 * c4 + 1][yy][xx] = q.y;
     tin[4 * c4 + 2][yy][xx] = q.z;
     tin[4 * c4 + 3][yy][xx] = q.w;
   }
+  for (int i = tid; i < 16 * 9 * 4; i += 256) wsh[i] = reinterpret_cast<const float4*>(w)[i];
   __syncthreads();
   float o[4][16];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int co = 0; co < 16; ++co) o[q][co] = 0.f;
-  // one input channel per iteration (its 144 weights are scalar loads)
+  // one input channel per iteration; its 144 weights are LDS broadcast reads (as scalar
+  // loads they cost three full scalar-cache round trips per channel: 76 vs 38 us at H/2)
 #pragma unroll 1
-  for (int ci = 0; ci < 16; ++ci) {
+  for (int ci = 0; ci < ((ABL & 2) ? 1 : 16); ++ci) {
     const float v00 = tin[ci][ty][tx], v01 = tin[ci][ty][tx + 1];
     const float v10 = tin[ci][ty + 1][tx], v11 = tin[ci][ty + 1][tx + 1];
-    const float* wc = w + ci * 9 * 16;   // [ci][tap][co] (pack_deconv_kernel)
+    const float4* wc = wsh + ci * 9 * 4;   // [tap][co / 4] (pack_deconv_kernel's [ci][tap][co])
 #pragma unroll
-    for (int co = 0; co < 16; ++co) {
-      auto k = [&](int tap) { return wc[tap * 16 + co]; };
-      o[0][co] = fmaf(v00, k(4), o[0][co]);
-      o[1][co] = fmaf(v00, k(5), fmaf(v01, k(3), o[1][co]));
-      o[2][co] = fmaf(v00, k(7), fmaf(v10, k(1), o[2][co]));
-      o[3][co] = fmaf(v00, k(8), fmaf(v01, k(6), fmaf(v10, k(2), fmaf(v11, k(0), o[3][co]))));
+    for (int c4 = 0; c4 < 4; ++c4) {
+      float4 kt[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) kt[t] = wc[t * 4 + c4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int co = 4 * c4 + u;
+        auto k = [&](int tap) {
+          const float4 q = kt[tap];
+          return u == 0 ? q.x : u == 1 ? q.y : u == 2 ? q.z : q.w;
+        };
+        o[0][co] = fmaf(v00, k(4), o[0][co]);
+        o[1][co] = fmaf(v00, k(5), fmaf(v01, k(3), o[1][co]));
+        o[2][co] = fmaf(v00, k(7), fmaf(v10, k(1), o[2][co]));
+        o[3][co] = fmaf(v00, k(8), fmaf(v01, k(6), fmaf(v10, k(2), fmaf(v11, k(0), o[3][co]))));
+      }
     }
   }
   float part[4] = {0.f, 0.f, 0.f, 0.f};
@@ -701,7 +718,7 @@ __global__ void __launch_bounds__(256) deconv_px_kernel(const float* __restrict_
           part[(co >> 3) * 2] += r[u];
           part[(co >> 3) * 2 + 1] += r[u] * r[u];
         }
-        d[c4] = make_float4(r[0], r[1], r[2], r[3]);
+        if (!(ABL & 1) || r[0] == 1234.5f) d[c4] = make_float4(r[0], r[1], r[2], r[3]);
       }
     }
   }
@@ -985,7 +1002,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
     {
       ProfScope ps(s, K_DECONV0);
-      hipLaunchKernelGGL(deconv_px_kernel, grid, dim3(256), 0, s, ws.h[2][nxt], params + L.dct_off[0],
+      hipLaunchKernelGGL(deconv_px_kernel<0>, grid, dim3(256), 0, s, ws.h[2][nxt], params + L.dct_off[0],
                          params + L.pk_off[P_D0B], Hi, Wi, ws.u0, ws.reg_part);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1015,7 +1032,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
     {
       ProfScope ps(s, K_DECONV1);
-      hipLaunchKernelGGL(deconv_px_kernel, grid, dim3(256), 0, s, ws.h[3][nxt], params + L.dct_off[1],
+      hipLaunchKernelGGL(deconv_px_kernel<0>, grid, dim3(256), 0, s, ws.h[3][nxt], params + L.dct_off[1],
                          params + L.pk_off[P_D1B], Hi, Wi, ws.u1, ws.reg_part);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -71,6 +71,19 @@ int main() {
   const double fl0 = 2.0 * 9 * 48 * 64 * HW, fl1 = 2.0 * 9 * 32 * 64 * HW / 4, fl3 = 2.0 * 9 * 48 * 64 * HW / 4,
                fl4 = 2.0 * 9 * 40 * 32 * HW;
   auto h3 = [&](CellArgs a) { a.wpk = reinterpret_cast<const float*>(wh); return a; };
+  {
+    const int Hi = H / 2, Wi = W / 2;
+    const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
+    double* gp; CK(hipMalloc(&gp, (size_t)grid.x * grid.y * 4 * 8));
+    const double fld = 2.0 * 16 * 16 * 9 * Hi * Wi;
+    auto dc = [&](auto kern) { return [=] { hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, f16a, wts, bias, Hi, Wi, hout, gp); return hipGetLastError(); }; };
+    run("deconv1 (H/2 -> H)", dc(deconv_px_kernel<0>), fld);
+    run("deconv1 no stores (1)", dc(deconv_px_kernel<1>), fld);
+    run("deconv1 no channel loop (2)", dc(deconv_px_kernel<2>), fld);
+    run("deconv1 no staging loads (4)", dc(deconv_px_kernel<4>), fld);
+    run("deconv1 no stores/loop (3)", dc(deconv_px_kernel<3>), fld);
+    run("deconv1 skeleton (7)", dc(deconv_px_kernel<7>), fld);
+  }
   run("cell0 h3 DB0 PIPE0", [&] { return run_cell_h3<0, 1, 8, 0, 0, 0>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 DB0 PIPE1", [&] { return run_cell_h3<0, 1, 8, 0, 0, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 DB1 PIPE0", [&] { return run_cell_h3<0, 1, 8, 0, 1, 0>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
