@@ -5,9 +5,10 @@
 //            models/drmvsnet.py:27-38 (InterViewAAModule), :307-319 (accumulation).
 //
 // Per plane and batch element the cost slice needs three grid-wide GroupNorm
-// reductions per source view.  They are met by a one-plane-ahead pipeline
-// (see cost_pipe_kernel below): per plane one streaming launch over the source
-// features plus two small statistics launches over the 16-B/px/view omega conv output.
+// reductions per source view.  The slices do not depend on the recurrence, so
+// they are computed a plane group at a time (kPlaneGroup): one omega conv launch over the
+// group's planes, two statistics launches over its 16-B/px/view omega conv output (each
+// statistic reduced in a fixed order), then one cost_x launch writing the group's slices.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -148,16 +149,13 @@ hipError_t launch_homo_warp_bwd(const float* gout, const float* rel, const float
 }
 
 // ---------------------------------------------------------------------------
-// Cost-slice pipeline.
-//
-// The cost slice of plane d does not depend on the recurrence, so the sweep runs it
-// one plane ahead of the regulariser.  Per plane d it launches
-//   cost_x(d)          x_d = -(sum_v (1 + w_v) (warp_v(d) - ref)^2) / nsrc, with w_v from
-//                      the omega conv output t1_d and plane d's three GroupNorm statistics
-//                      (drmvsnet.py:307-319);
-//   omega_conv(d + 1)  sq_v(d+1) = (warp_v(d+1) - ref)^2 on a haloed tile in LDS, the
-//                      omega conv3x3 32->4 -> t1_{d+1} (16 B/px/view), GN #0 partial sums;
-//   omega_stats<1>/<2>(d + 1)  GN #1/#2 statistics from t1_{d+1} alone.
+// Cost-slice stage, per plane group d0 .. d0 + n - 1 (launch_omega_group, launch_cost_x_group):
+//   omega_conv         sq_v(d) = (warp_v(d) - ref)^2 on a haloed tile in LDS, the omega
+//                      conv3x3 32->4 -> t1_d (16 B/px/view), GN #0 partial sums;
+//   omega_stats<1>/<2> GN #1/#2 partial sums from t1_d alone (each followed by a fixed-order
+//                      stat_reduce);
+//   cost_x             x_d = -(sum_v (1 + w_v) (warp_v(d) - ref)^2) / nsrc, with w_v from
+//                      t1_d and plane d's three GroupNorm statistics (drmvsnet.py:307-319).
 // Both gather their bilinear taps straight from the "c8" feature copies
 // ([B][4][H][W][8], to_c8_kernel): one tap of one 8-channel chunk is a 32-B segment,
 // and neighbouring output pixels share taps in L1/L2.
