@@ -124,6 +124,10 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(h1.data(), t1b, 8 * t1k * 16, hipMemcpyDeviceToHost));
         printf("  DB t1 vs default: %s\n", memcmp(h0.data(), h1.data(), 8 * t1k * 16) ? "DIFFERENT" : "identical");
       }
+      {
+        std::vector<float4> h0(8 * t1k), h1(8 * t1k);
+        ablate("default (0)", omega_mfma_kernel<0>, t1b, stb);
+      }
       ablate("no MFMA (1)", omega_mfma_kernel<1>, t1b, stb);
       ablate("no box DMA (2)", omega_mfma_kernel<2>, t1b, stb);
       ablate("no sampling (4)", omega_mfma_kernel<4>, t1b, stb);
