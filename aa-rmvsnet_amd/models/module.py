@@ -85,13 +85,45 @@ def _groups(channels: int, group_channel: int) -> int:
     return int(max(1, channels / group_channel))
 
 
+class GroupNorm(nn.GroupNorm):
+    """nn.GroupNorm (same parameters and state_dict keys) whose GPU forward takes the
+    per-group statistics with ATen's multi-block reductions.
+
+    ATen's ROCm group_norm reduces each (sample, group) row in ONE thread block
+    (RowwiseMomentsCUDAKernel): at B=1 with one or two groups over a full-resolution plane
+    that is one or two busy CUs -- 0.9 ms per call at 640x512, over half of a training
+    step's GPU time in the BPTT recompute (rocprofv3).  Here mean and
+    variance come from torch.mean / torch.var (grid-wide reductions) and the output is
+    ATen's own form y = x * (rstd * gamma) + (beta - mean * rstd * gamma), differentiated
+    by autograd.  On the CPU the reference's F.group_norm runs unchanged."""
+
+    def forward(self, x):
+        if not x.is_cuda:
+            return super().forward(x)
+        B, C = x.shape[:2]
+        G = self.num_groups
+        xg = x.reshape(B, G, -1)
+        var, mean = torch.var_mean(xg, dim=-1, unbiased=False, keepdim=True)
+        rstd = torch.rsqrt(var + self.eps)                      # [B, G, 1]
+        cg = C // G
+        if self.affine:
+            w = self.weight.view(1, G, cg)
+            a = rstd * w                                        # [B, G, cg]
+            b = self.bias.view(1, G, cg) - mean * a
+        else:
+            a = rstd.expand(B, G, cg)
+            b = -mean * a
+        y = x.reshape(B, G, cg, -1) * a.unsqueeze(-1) + b.unsqueeze(-1)
+        return y.reshape_as(x)
+
+
 def convgnrelu(in_channels, out_channels, kernel_size=3, stride=1, dilation=1, bias=True,
                group_channel=8):
     """models/module.py:98-103."""
     return nn.Sequential(
         nn.Conv2d(in_channels, out_channels, kernel_size=kernel_size, stride=stride,
                   dilation=dilation, padding=((kernel_size - 1) // 2) * dilation, bias=bias),
-        nn.GroupNorm(_groups(out_channels, group_channel), out_channels),
+        GroupNorm(_groups(out_channels, group_channel), out_channels),
         nn.ReLU(inplace=True),
     )
 
@@ -170,7 +202,7 @@ def deformconvgnrelu(in_channels, out_channels, kernel_size=3, stride=1, dilatio
     """models/module.py:238-243."""
     return nn.Sequential(
         DeformConv2d(in_channels, out_channels, kernel_size=kernel_size, stride=stride, bias=bias),
-        nn.GroupNorm(_groups(out_channels, group_channel), out_channels),
+        GroupNorm(_groups(out_channels, group_channel), out_channels),
         nn.ReLU(inplace=True),
     )
 
@@ -186,7 +218,7 @@ class ResnetBlockGn(nn.Module):
             nn.Conv2d(in_channels, in_channels, kernel_size=kernel_size, stride=1,
                       dilation=dilation[1], padding=((kernel_size - 1) // 2) * dilation[1],
                       bias=bias),
-            nn.GroupNorm(_groups(in_channels, group_channel), in_channels),
+            GroupNorm(_groups(in_channels, group_channel), in_channels),
         )
         self.relu = nn.ReLU(inplace=True)
 
@@ -210,7 +242,7 @@ class deConvGnReLU(nn.Module):  # noqa: N801  (reference name)
                                        padding=padding, output_padding=output_padding,
                                        stride=stride, bias=bias)
         self.group_channel = group_channel
-        self.gn = nn.GroupNorm(_groups(out_channels, group_channel), out_channels)
+        self.gn = GroupNorm(_groups(out_channels, group_channel), out_channels)
 
     def forward(self, x):
         return F.relu(self.gn(self.conv(x)), inplace=True)
