@@ -61,6 +61,9 @@ struct ParamLayout {
   size_t owm_off;           // omega conv3x3 off-centre taps as split-fp16 v_mfma_f32_32x32x16_f16
                             // B fragments [chunk][2][64 lanes][8] (omega_mfma; same scale)
   size_t dct_off[2];        // deconv_0/1 weights as [ci][tap][co] (2,304 floats each)
+  size_t dcm_off[2];        // deconv_0/1 as split-fp16 v_mfma_f32_32x32x16_f16 A fragments
+                            // [6 tap pairs][hi, lo][64 lanes][8 halves], then 1 float: 2^-e
+                            // (the fragments carry the power-of-two weight scale 2^e)
   size_t raw_total;
   size_t pk_total;
 };

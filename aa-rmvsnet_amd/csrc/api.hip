@@ -52,6 +52,10 @@ const ParamLayout& param_layout() {
       l.dct_off[k] = pk;
       pk += 16 * 9 * 16;
     }
+    for (int k = 0; k < 2; ++k) {
+      l.dcm_off[k] = pk;
+      pk += 6 * 2 * 64 * 8 / 2 + 64;   // halves -> floats, then the scale (64-float aligned)
+    }
     l.raw_total = raw;
     l.pk_total = pk;
     return l;
@@ -158,9 +162,9 @@ Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
   ws.x = ws.xg[0];
   for (int v = 0; v <= nsrc; ++v) ws.feat8[v] = reinterpret_cast<float*>(take(B * kC * HW * 4));
   ws.t1 = reinterpret_cast<float*>(take(kPlaneGroup * ws.t1_plane * 16));
-  // one partial per omega block (haloed 16 x 32 tiles: 14 x 30 outputs; the VALU variant's
-  // 16 x 32 output tiles are fewer) or statistics block (<= one per 1024 pixels)
-  ws.omega_part_n = (int)std::max(((size_t)(W + 29) / 30) * ((size_t)(H + 13) / 14), (HW + 1023) / 1024);
+  // one partial per omega block (haloed 16 x TW tiles, 14 x (TW - 2) outputs, TW >= 16; the
+  // VALU variant's 16 x 32 output tiles are fewer) or statistics block (<= one per 1024 px)
+  ws.omega_part_n = (int)std::max(((size_t)(W + 13) / 14) * ((size_t)(H + 13) / 14), (HW + 1023) / 1024);
   ws.omega_part = reinterpret_cast<double*>(
       take((size_t)kPlaneGroup * B * nsrc * ws.omega_part_n * 2 * sizeof(double)));
   // deconv_1's blocks (8 x 32 tiles of its H/2 x W/2 input) outnumber deconv_0's
@@ -314,6 +318,39 @@ __global__ void pack_deconv_kernel(const float* __restrict__ raw, float* __restr
   }
 }
 
+// deconv_0/1 as split-fp16 MFMA A fragments (deconv_mfma_kernel): six tap pairs, rows
+// m = slot * 16 + co (slot 0 / 1: the two output pixels of a pair), k = ci; lane l holds row
+// l & 31, input channels 8 (l >> 5) .. +7.  Pairs (tap of slot 0 | slot 1, input pixel):
+// (4 | 5, v00), (- | 3, v01), (7 | 8, v00), (- | 6, v01), (1 | 2, v10), (- | 0, v11) -- the
+// ConvTranspose2d(k3, s2, p1, op1) taps feeding output (2y + a, 2x + b) from input (y, x)
+// and its right / lower neighbours.  Values are scaled by 2^e (max |w| 2^e < 2^15).
+__global__ void pack_deconv_mfma_kernel(const float* __restrict__ raw, float* __restrict__ pk,
+                                        ParamLayout L) {
+  __shared__ float red[4];
+  const int k = blockIdx.x;
+  const float* w = raw + L.raw_off[k ? P_D1W : P_D0W];   // [ci][co][3][3]
+  float mx = 0.f;
+  for (int i = threadIdx.x; i < 16 * 16 * 9; i += blockDim.x) mx = fmaxf(mx, fabsf(w[i]));
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const int e = mx > 0.f ? 14 - ilogbf(mx) : 0;
+  const float sc = ldexpf(1.0f, e);
+  constexpr int kTap[6][2] = {{4, 5}, {-1, 3}, {7, 8}, {-1, 6}, {1, 2}, {-1, 0}};
+  _Float16* f = reinterpret_cast<_Float16*>(pk + L.dcm_off[k]);
+  for (int i = threadIdx.x; i < 6 * 64 * 8; i += blockDim.x) {
+    const int j = i & 7, lane = (i >> 3) & 63, pair = i >> 9;
+    const int m = lane & 31, slot = m >> 4, co = m & 15, ci = 8 * (lane >> 5) + j;
+    const int tap = kTap[pair][slot];
+    const float v = tap < 0 ? 0.f : w[(ci * 16 + co) * 9 + tap] * sc;
+    const _Float16 hi = (_Float16)v;
+    f[((pair * 2 + 0) * 64 + lane) * 8 + j] = hi;
+    f[((pair * 2 + 1) * 64 + lane) * 8 + j] = (_Float16)(v - (float)hi);
+  }
+  if (threadIdx.x == 0) pk[L.dcm_off[k] + 6 * 2 * 64 * 8 / 2] = ldexpf(1.0f, -e);
+}
+
 hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s) {
   const ParamLayout& L = param_layout();
   hipError_t e = hipMemsetAsync(packed, 0, L.pk_total * sizeof(float), s);
@@ -325,6 +362,8 @@ hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s) {
   hipLaunchKernelGGL(pack_omega_conv_kernel, dim3(1), dim3(256), 0, s, raw, packed, L);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(pack_deconv_kernel, dim3(2), dim3(256), 0, s, raw, packed, L);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(pack_deconv_mfma_kernel, dim3(2), dim3(256), 0, s, raw, packed, L);
   return hipGetLastError();
 }
 

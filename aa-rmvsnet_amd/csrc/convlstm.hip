@@ -638,30 +638,36 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
 // segment, a partial last segment per row): 84 / 47 us per plane at the headline geometry
 // against 71 / 37 us here (profiles/r02_*).
 constexpr int kDpTH = 8, kDpTW = 32;
+// One block per 8 x 32 input tile: the tile and its bottom / right neighbours (9 x 33 px)
+// staged once in LDS channel-major, the 16 x 9 x 16 weights in LDS (broadcast reads).  A
+// thread takes two input pixels (rows ty and ty + 4) and one half of the output channels
+// (8), accumulates the 2 x 2 output quads of both pixels (deconv_px2: every weight read
+// feeds two pixels' FMAs; 67 vs 74 us at H/2 -> H for one pixel x 16 channels per thread,
+// bit-identical outputs), and stores the quads straight to NHWC.  The VALU reference for
+// deconv_mfma_kernel (the library's; tools/microbench/cell_bench A/Bs the two).
 // ABL: ablation bits for tools/microbench/cell_bench only (the library instantiates 0):
 // 1 no output stores, 2 no channel loop, 4 no input staging loads
 template <int ABL = 0>
-__global__ void __launch_bounds__(256) deconv_px_kernel(const float* __restrict__ in,
-                                                        const float* __restrict__ w,
-                                                        const float* __restrict__ bias, int Hi,
-                                                        int Wi, float* __restrict__ out,
-                                                        double* __restrict__ gn_part) {
-  constexpr int SH = kDpTH + 1, SW = kDpTW + 1;   // the tile + its bottom / right neighbours
-  __shared__ float tin[16][SH][SW];               // [ci][y][x] (row stride 33: conflict-free)
-  __shared__ float4 wsh[16 * 9 * 4];              // weights [ci][tap][co / 4] (broadcast reads)
+__global__ void __launch_bounds__(256) deconv_px2_kernel(const float* __restrict__ in,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ bias, int Hi,
+                                                         int Wi, float* __restrict__ out,
+                                                         double* __restrict__ gn_part) {
+  constexpr int SH = kDpTH + 1, SW = kDpTW + 1;
+  __shared__ float tin[16][SH][SW];
+  __shared__ float4 wsh[16 * 9 * 4];   // [ci][tap][co / 4]
   __shared__ float red[4 * 4];
   const int b = blockIdx.z, tid = threadIdx.x;
   const int y0 = blockIdx.y * kDpTH, x0 = blockIdx.x * kDpTW;
-  const int ty = tid / kDpTW, tx = tid % kDpTW;
-  const int iy = y0 + ty, ix = x0 + tx;
+  const int hc = tid >> 7, r = tid & 127;   // output channels 8 hc .. 8 hc + 7
+  const int tx = r & 31, tyb = r >> 5;      // pixels (tyb, tx) and (tyb + 4, tx)
+  const int ix = x0 + tx;
   const int Wo = 2 * Wi;
-  const bool ok = iy < Hi && ix < Wi;
   const float* ib = in + (size_t)b * 16 * Hi * Wi;
-  // stage: 16-B pieces (4 channels of one pixel), channel group fastest (coalesced NHWC)
   for (int i = tid; i < SH * SW * 4; i += 256) {
     const int c4 = i & 3, px = i >> 2, yy = px / SW, xx = px - yy * SW;
     const int gy = y0 + yy, gx = x0 + xx;
-    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);   // zero padding past the image
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
     if (!(ABL & 4) && gy < Hi && gx < Wi)
       q = *reinterpret_cast<const float4*>(ib + ((size_t)gy * Wi + gx) * 16 + 4 * c4);
     tin[4 * c4 + 0][yy][xx] = q.x;
@@ -671,61 +677,179 @@ __global__ void __launch_bounds__(256) deconv_px_kernel(const float* __restrict_
   }
   for (int i = tid; i < 16 * 9 * 4; i += 256) wsh[i] = reinterpret_cast<const float4*>(w)[i];
   __syncthreads();
-  float o[4][16];
+  float o[2][4][8];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int p = 0; p < 2; ++p)
 #pragma unroll
-    for (int co = 0; co < 16; ++co) o[q][co] = 0.f;
-  // one input channel per iteration; its 144 weights are LDS broadcast reads (as scalar
-  // loads they cost three full scalar-cache round trips per channel: deconv0 38 -> 29 us;
-  // deconv1 stays at 77 us, now bound by these 36 ds_read_b128 per channel)
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) o[p][q][c] = 0.f;
 #pragma unroll 1
   for (int ci = 0; ci < ((ABL & 2) ? 1 : 16); ++ci) {
-    const float v00 = tin[ci][ty][tx], v01 = tin[ci][ty][tx + 1];
-    const float v10 = tin[ci][ty + 1][tx], v11 = tin[ci][ty + 1][tx + 1];
-    const float4* wc = wsh + ci * 9 * 4;   // [tap][co / 4] (pack_deconv_kernel's [ci][tap][co])
+    float v[2][4];
 #pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4) {
+    for (int p = 0; p < 2; ++p) {
+      const int ty = tyb + 4 * p;
+      v[p][0] = tin[ci][ty][tx];
+      v[p][1] = tin[ci][ty][tx + 1];
+      v[p][2] = tin[ci][ty + 1][tx];
+      v[p][3] = tin[ci][ty + 1][tx + 1];
+    }
+    const float4* wc = wsh + ci * 9 * 4 + 2 * hc;
+#pragma unroll
+    for (int c4 = 0; c4 < 2; ++c4) {
       float4 kt[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) kt[t] = wc[t * 4 + c4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int co = 4 * c4 + u;
+        const int c = 4 * c4 + u;
         auto k = [&](int tap) {
           const float4 q = kt[tap];
           return u == 0 ? q.x : u == 1 ? q.y : u == 2 ? q.z : q.w;
         };
-        o[0][co] = fmaf(v00, k(4), o[0][co]);
-        o[1][co] = fmaf(v00, k(5), fmaf(v01, k(3), o[1][co]));
-        o[2][co] = fmaf(v00, k(7), fmaf(v10, k(1), o[2][co]));
-        o[3][co] = fmaf(v00, k(8), fmaf(v01, k(6), fmaf(v10, k(2), fmaf(v11, k(0), o[3][co]))));
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const float v00 = v[p][0], v01 = v[p][1], v10 = v[p][2], v11 = v[p][3];
+          o[p][0][c] = fmaf(v00, k(4), o[p][0][c]);
+          o[p][1][c] = fmaf(v00, k(5), fmaf(v01, k(3), o[p][1][c]));
+          o[p][2][c] = fmaf(v00, k(7), fmaf(v10, k(1), o[p][2][c]));
+          o[p][3][c] = fmaf(v00, k(8), fmaf(v01, k(6), fmaf(v10, k(2), fmaf(v11, k(0), o[p][3][c]))));
+        }
       }
     }
   }
   float part[4] = {0.f, 0.f, 0.f, 0.f};
-  if (ok) {
-    float* ob = out + (size_t)b * 16 * 4 * Hi * Wi;
+  float* ob = out + (size_t)b * 16 * 4 * Hi * Wi;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float4* d = reinterpret_cast<float4*>(ob + ((size_t)(2 * iy + (q >> 1)) * Wo + 2 * ix + (q & 1)) * 16);
+  for (int p = 0; p < 2; ++p) {
+    const int iy = y0 + tyb + 4 * p;
+    if (iy < Hi && ix < Wi) {
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        float r[4];
+      for (int q = 0; q < 4; ++q) {
+        float4* d = reinterpret_cast<float4*>(ob + ((size_t)(2 * iy + (q >> 1)) * Wo + 2 * ix + (q & 1)) * 16 + 8 * hc);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int co = 4 * c4 + u;
-          r[u] = o[q][co] + bias[co];
-          part[(co >> 3) * 2] += r[u];
-          part[(co >> 3) * 2 + 1] += r[u] * r[u];
+        for (int c4 = 0; c4 < 2; ++c4) {
+          float rr[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            rr[u] = o[p][q][4 * c4 + u] + bias[8 * hc + 4 * c4 + u];
+            part[2 * hc] += rr[u];
+            part[2 * hc + 1] += rr[u] * rr[u];
+          }
+          if (!(ABL & 1) || rr[0] == 1234.5f) d[c4] = make_float4(rr[0], rr[1], rr[2], rr[3]);
         }
-        if (!(ABL & 1) || r[0] == 1234.5f) d[c4] = make_float4(r[0], r[1], r[2], r[3]);
       }
     }
   }
   block_sum<4>(part, red);
-  // this block's GroupNorm partials (groups of 8 channels: sum, sumsq), reduced in a fixed
-  // order by gn_reduce_kernel: statistics independent of block timing
+  if (tid == 0) {
+    double* pp = gn_part + 4 * (((size_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pp[j] = part[j];
+  }
+}
+
+// deconv_mfma: the same transposed conv on the matrix cores.  Per 32 input pixels of a row
+// (one wave) and input neighbour set (v00, v01, v10, v11: the pixel, its right, lower and
+// lower-right neighbour), D[slot * 16 + co][px] += W_pair x V with the six tap pairs of
+// pack_deconv_mfma_kernel: acc01 holds output pixels (2y, 2x) | (2y, 2x + 1), acc23
+// (2y + 1, 2x) | (2y + 1, 2x + 1).  Each fp32 product as three split-fp16 products (w_hi
+// v_hi + w_hi v_lo + w_lo v_hi); V is staged x 2^14 (|h| < 1: tanh outputs),
+// the weights carry 2^e, both undone in the epilogue.  B fragments straight from the NHWC
+// input (lane: pixel l & 31, channels 8 (l >> 5) .. +7, 32 contiguous bytes).  Block: 4
+// waves x 2 rows = the 8 x 32 input tile of deconv_px2 (same GN partial grid).
+typedef _Float16 dhalf8 __attribute__((ext_vector_type(8)));
+template <int ABL = 0>
+__global__ void __launch_bounds__(256) deconv_mfma_kernel(const float* __restrict__ in,
+                                                          const float* __restrict__ wfrag,
+                                                          const float* __restrict__ bias, int Hi,
+                                                          int Wi, float* __restrict__ out,
+                                                          double* __restrict__ gn_part) {
+  __shared__ float red[4 * 4];
+  const int b = blockIdx.z, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int x0 = blockIdx.x * kDpTW;
+  const int n = lane & 31, hh = lane >> 5;   // B/D column (pixel), channel half
+  const int Wo = 2 * Wi;
+  const float* ib = in + (size_t)b * 16 * Hi * Wi;
+  const dhalf8* af = reinterpret_cast<const dhalf8*>(wfrag);
+  dhalf8 ah[6], al[6];
+#pragma unroll
+  for (int p = 0; p < 6; ++p) {
+    ah[p] = af[(p * 2 + 0) * 64 + lane];
+    al[p] = af[(p * 2 + 1) * 64 + lane];
+  }
+  const float inv = wfrag[6 * 2 * 64 * 8 / 2] * (1.0f / 16384.0f);
+  // B fragments of input pixel (y, x): channels 8 hh .. +7, x 2^14, split (zero outside)
+  auto bfrag = [&](int y, int x, dhalf8& bh, dhalf8& bl) {
+    float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
+    if (!(ABL & 4) && y < Hi && x < Wi) {
+      const float4* s = reinterpret_cast<const float4*>(ib + ((size_t)y * Wi + x) * 16 + 8 * hh);
+      q0 = s[0];
+      q1 = s[1];
+    }
+    const float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float t = v[j] * 16384.0f;
+      const _Float16 h = (_Float16)t;
+      bh[j] = h;
+      bl[j] = (_Float16)(t - (float)h);
+    }
+  };
+  float part[4] = {0.f, 0.f, 0.f, 0.f};
+  typedef float fx16 __attribute__((ext_vector_type(16)));
+#pragma unroll 1
+  for (int rr = 0; rr < 2; ++rr) {
+    const int iy = blockIdx.y * kDpTH + wave * 2 + rr;
+    if (iy >= Hi) break;
+    const int ix = x0 + n;
+    dhalf8 b00h, b00l, b01h, b01l, b10h, b10l, b11h, b11l;
+    bfrag(iy, ix, b00h, b00l);
+    bfrag(iy, ix + 1, b01h, b01l);
+    bfrag(iy + 1, ix, b10h, b10l);
+    bfrag(iy + 1, ix + 1, b11h, b11l);
+    fx16 a01, a23;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a01[r] = a23[r] = 0.f;
+    if (!(ABL & 2)) {
+      auto mm = [&](fx16 acc, int p, dhalf8 bh, dhalf8 bl) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[p], bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[p], bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[p], bh, acc, 0, 0, 0);
+        return acc;
+      };
+      a01 = mm(a01, 0, b00h, b00l);
+      a01 = mm(a01, 1, b01h, b01l);
+      a23 = mm(a23, 2, b00h, b00l);
+      a23 = mm(a23, 3, b01h, b01l);
+      a23 = mm(a23, 4, b10h, b10l);
+      a23 = mm(a23, 5, b11h, b11l);
+    }
+    if (ix < Wi) {
+      float* ob = out + (size_t)b * 16 * 4 * Hi * Wi;
+      // D row m = (r & 3) + 8 (r >> 2) + 4 hh: slot r >> 3, channels 4 hh + 8 ((r >> 2) & 1) + (r & 3)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {   // r = 4 g .. 4 g + 3
+        const int slot = g >> 1, c0 = 4 * hh + 8 * (g & 1), grp = g & 1;
+#pragma unroll
+        for (int acc_i = 0; acc_i < 2; ++acc_i) {
+          const fx16& A = acc_i ? a23 : a01;
+          const int oy = 2 * iy + acc_i, ox = 2 * ix + slot;
+          float v4[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            v4[u] = fmaf(A[4 * g + u], inv, bias[c0 + u]);
+            part[2 * grp] += v4[u];
+            part[2 * grp + 1] += v4[u] * v4[u];
+          }
+          float4* d = reinterpret_cast<float4*>(ob + ((size_t)oy * Wo + ox) * 16 + c0);
+          if (!(ABL & 1) || v4[0] == 1234.5f) *d = make_float4(v4[0], v4[1], v4[2], v4[3]);
+        }
+      }
+    }
+  }
+  block_sum<4>(part, red);
   if (tid == 0) {
     double* pp = gn_part + 4 * (((size_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
 #pragma unroll
@@ -1003,7 +1127,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
     {
       ProfScope ps(s, K_DECONV0);
-      hipLaunchKernelGGL(deconv_px_kernel<0>, grid, dim3(256), 0, s, ws.h[2][nxt], params + L.dct_off[0],
+      hipLaunchKernelGGL(deconv_mfma_kernel<0>, grid, dim3(256), 0, s, ws.h[2][nxt], params + L.dcm_off[0],
                          params + L.pk_off[P_D0B], Hi, Wi, ws.u0, ws.reg_part);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1033,7 +1157,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
     {
       ProfScope ps(s, K_DECONV1);
-      hipLaunchKernelGGL(deconv_px_kernel<0>, grid, dim3(256), 0, s, ws.h[3][nxt], params + L.dct_off[1],
+      hipLaunchKernelGGL(deconv_mfma_kernel<0>, grid, dim3(256), 0, s, ws.h[3][nxt], params + L.dcm_off[1],
                          params + L.pk_off[P_D1B], Hi, Wi, ws.u1, ws.reg_part);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;

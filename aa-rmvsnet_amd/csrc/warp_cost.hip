@@ -330,7 +330,9 @@ struct Box {
   int x0, y0, nx, ny;
 };
 
-// red: LDS scratch [kTileWaves][4]; must not be read by anyone before the barrier here
+// red: LDS scratch [NW][4] (NW: the block's waves); must not be read by anyone before the
+// barrier here
+template <int NW = kTileWaves>
 __device__ __forceinline__ Box box_reduce(int lx, int ly, int hx, int hy, int (*red)[4]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -348,7 +350,7 @@ __device__ __forceinline__ Box box_reduce(int lx, int ly, int hx, int hy, int (*
   }
   __syncthreads();
 #pragma unroll
-  for (int w = 0; w < kTileWaves; ++w) {
+  for (int w = 0; w < NW; ++w) {
     lx = min(lx, red[w][0]);
     ly = min(ly, red[w][1]);
     hx = max(hx, red[w][2]);
@@ -451,9 +453,9 @@ __device__ __forceinline__ void sample_pos_pair(const float* __restrict__ m, flo
 // (sample_pos_pair): no further gain; bits 4 / 8 (microbenchmark) 5 / 6 waves per SIMD
 // instead of 4: 0.485 / 0.578 ms (6 spills) vs 0.482 ms, so occupancy is not the limit
 // (the measured HBM traffic, 2.1 GB per plane, is close to the algorithmic 1.94 GB).
-constexpr int kXRows = 8;
-template <int XV = 0>
-__global__ void __launch_bounds__(2 * kXRows * kTileW)
+constexpr int kXRows = 4;   // the library's tile rows (XR): 256-thread blocks (339 vs 347 us with 8)
+template <int XV = 0, int XR = kXRows>
+__global__ void __launch_bounds__(2 * XR * kTileW)
 __attribute__((amdgpu_waves_per_eu((XV & 8) ? 6 : (XV & 4) ? 5 : 4))) cost_x_kernel(PipeArgs a,
                                                               const float* __restrict__ P,
                                                               const float* __restrict__ Rel) {
@@ -465,7 +467,7 @@ __attribute__((amdgpu_waves_per_eu((XV & 8) ? 6 : (XV & 4) ? 5 : 4))) cost_x_ker
   const int tile = seq / a.npl, kp = seq - tile * a.npl;
   const int tiles_x = (W + kTileW - 1) / kTileW;
   const int h = tid & 1, q = tid >> 1;
-  const int gy = (tile / tiles_x) * kXRows + q / kTileW, gx = (tile % tiles_x) * kTileW + q % kTileW;
+  const int gy = (tile / tiles_x) * XR + q / kTileW, gx = (tile % tiles_x) * kTileW + q % kTileW;
   if (tid < 3 * nsrc) {
     const int v = tid / 3, k = tid % 3;
     gs[v][k] = stat_read(a.st_prev + kp * a.st_kstride + st_index(b, v, k, nsrc), 4.0 * HW);
@@ -914,19 +916,31 @@ constexpr int kOmegaConvAbl = 0;
 // sq is staged x 2^-e (e from the sweep's |x| bound, ws.xbound: sq <= 4 max|feature|^2
 // <= bound) so that fp16 cannot overflow; the weights carry their own power-of-two scale.
 // ---------------------------------------------------------------------------
-constexpr int kMTileH = 16, kMTileW = 32, kMThreads = kMTileH * kMTileW;   // haloed tile
-constexpr int kMOutH = kMTileH - 2, kMOutW = kMTileW - 2;                  // output tile
-constexpr int kMYStride = 36;                                               // floats per pixel in Y
-constexpr int kMBoxPx = 1024;
+// TW: haloed tile width (32, or 16 for 256-thread blocks: 4 blocks per CU by LDS instead of 2).
+// Lane l of wave w holds haloed pixel 64 w + l = (hy, hx) = ((64 w + l) / TW, (64 w + l) % TW);
+// MFMA row group 0 / 1 of the wave is its lanes 0-31 / 32-63.
+constexpr int kMTileH = 16;
+constexpr int kMYStride = 36;   // floats per pixel in Y
+template <int TW>
+struct OmegaTile {
+  static constexpr int NT = kMTileH * TW;   // threads = haloed pixels
+  static constexpr int OUTH = kMTileH - 2, OUTW = TW - 2;
+  static constexpr int BOXPX = 2 * NT;      // LDS source-box capacity (32-B pixels)
+  static int tiles(int H, int W) { return ((W + OUTW - 1) / OUTW) * ((H + OUTH - 1) / OUTH); }
+};
+constexpr int kOmegaTW = 16;   // the library's tile width
 
 // ABL: ablation bits for the diagnostic harness only (tools/microbench/pipe_bench.cpp; the
 // library instantiates ABL = 0): 1 no MFMAs, 2 no box DMA, 4 no box sampling, 8 no reference
 // loads, 16 sampling positions without the homography divisions (the own pixel), 32 no Y
 // image / gather (t1 from the accumulators), 64 no statistics atomics, 128 no B-fragment loads
-template <int ABL = 0>
-__global__ void __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(4)))
+template <int ABL = 0, int TW = kOmegaTW>
+__global__ void __launch_bounds__(OmegaTile<TW>::NT) __attribute__((amdgpu_waves_per_eu(4)))
 omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restrict__ Rel,
                   const unsigned* __restrict__ xbound) {
+  using T = OmegaTile<TW>;
+  constexpr int kMThreads = T::NT, kMBoxPx = T::BOXPX, kMOutH = T::OUTH, kMOutW = T::OUTW;
+  if (blockDim.x != kMThreads) return;   // LDS images are sized for exactly this block
   constexpr int NB = (2 * kMBoxPx + kMThreads - 1) / kMThreads;   // box pieces per thread
   constexpr int YFL = kMThreads * kMYStride;                      // Y image floats
   static_assert(YFL >= (kMBoxPx + 1) * 8, "the box fits in the Y image space");
@@ -945,7 +959,7 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   const int v = vk / a.npl, kp = vk - v * a.npl;
   const int tiles_x = (W + kMOutW - 1) / kMOutW;
   const int y0 = (tile / tiles_x) * kMOutH, x0 = (tile % tiles_x) * kMOutW;
-  const int hy = 2 * wave + (lane >> 5), hx = lane & 31;   // haloed pixel of this lane
+  const int hy = tid / TW, hx = tid % TW;   // haloed pixel of this lane
   const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
   const bool in_img = gy >= 0 && gy < H && gx >= 0 && gx < W;
   const bool interior = in_img && hy >= 1 && hy <= kMOutH && hx >= 1 && hx <= kMOutW;
@@ -976,7 +990,7 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     }
     box_extend(tf, H, W, lx, ly, bhx, bhy);
   }
-  const Box bx = box_reduce(lx, ly, bhx, bhy, red);
+  const Box bx = box_reduce<kMThreads / 64>(lx, ly, bhx, bhy, red);
   const bool lds = bx.nx * bx.ny <= min(kMBoxPx, a.box_cap);
   const uint32_t zp = lds ? (uint32_t)kMBoxPx : fbytes / 32u;
   const TapP tp = tap_p(tf, in_img, H, W, lds, bx, zp);
@@ -1108,8 +1122,8 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int px = (r & 3) + 8 * (r >> 2) + rb;
-      yimg[((2 * wave) * kMTileW + px) * kMYStride + col] = acc0[r];
-      yimg[((2 * wave + 1) * kMTileW + px) * kMYStride + col] = acc1[r];
+      yimg[(64 * wave + px) * kMYStride + col] = acc0[r];
+      yimg[(64 * wave + 32 + px) * kMYStride + col] = acc1[r];
     }
   }
   __syncthreads();
@@ -1125,7 +1139,7 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int tap = u < 4 ? u : u + 1;
-      const int q = (hy + tap / 3 - 1) * kMTileW + hx + tap % 3 - 1;
+      const int q = (hy + tap / 3 - 1) * TW + hx + tap % 3 - 1;
       const float4 yv = *reinterpret_cast<const float4*>(yimg + q * kMYStride + 4 * u);
       g4[0] += yv.x;
       g4[1] += yv.y;
@@ -1351,10 +1365,11 @@ hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Work
                        dim3(kTileThreads), 0, s, a, a.params, a.rel);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   } else {
-    const int ntiles = ((g.W + kMOutW - 1) / kMOutW) * ((g.H + kMOutH - 1) / kMOutH);
+    const int ntiles = OmegaTile<kOmegaTW>::tiles(g.H, g.W);
     ProfScope ps(s, K_OMEGA_CONV);
     a.part_n = ntiles;
-    hipLaunchKernelGGL(omega_mfma_kernel<0>, dim3(ntiles * g.nsrc * n, 1, g.B), dim3(kMThreads), 0, s,
+    hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW>), dim3(ntiles * g.nsrc * n, 1, g.B),
+                       dim3(OmegaTile<kOmegaTW>::NT), 0, s,
                        a, a.params, a.rel, ws.xbound);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

@@ -4,6 +4,8 @@
 #include "../../aa-rmvsnet_amd/csrc/convlstm.hip"
 
 #include <cstdio>
+#include <cmath>
+#include <cstring>
 #include <vector>
 
 
@@ -77,12 +79,37 @@ int main() {
     double* gp; CK(hipMalloc(&gp, (size_t)grid.x * grid.y * 4 * 8));
     const double fld = 2.0 * 16 * 16 * 9 * Hi * Wi;
     auto dc = [&](auto kern) { return [=] { hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, f16a, wts, bias, Hi, Wi, hout, gp); return hipGetLastError(); }; };
-    run("deconv1 (H/2 -> H)", dc(deconv_px_kernel<0>), fld);
-    run("deconv1 no stores (1)", dc(deconv_px_kernel<1>), fld);
-    run("deconv1 no channel loop (2)", dc(deconv_px_kernel<2>), fld);
-    run("deconv1 no staging loads (4)", dc(deconv_px_kernel<4>), fld);
-    run("deconv1 no stores/loop (3)", dc(deconv_px_kernel<3>), fld);
-    run("deconv1 skeleton (7)", dc(deconv_px_kernel<7>), fld);
+    // packed parameters from one random raw blob: dct (VALU) and dcm (MFMA) of deconv_1
+    const ParamLayout& PL = param_layout();
+    float* raw = rnd_buf(PL.raw_total, 0.2f);
+    float* pk; CK(hipMalloc(&pk, PL.pk_total * 4));
+    CK(launch_pack_params(raw, pk, 0));
+    float* hin = rnd_buf(16 * HW / 4, 1.9f);   // |h| < 1 like the tanh outputs
+    auto dv = [&](auto kern, const float* wp) { return [=] { hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, hin, wp, pk + PL.pk_off[P_D1B], Hi, Wi, hout, gp); return hipGetLastError(); }; };
+    {
+      const size_t no = (size_t)16 * 4 * Hi * Wi;
+      std::vector<float> o1(no), o2(no);
+      std::vector<double> g1((size_t)grid.x * grid.y * 4), g2(g1.size());
+      CK(dv(deconv_px2_kernel<0>, pk + PL.dct_off[1])()); CK(hipDeviceSynchronize());
+      CK(hipMemcpy(o1.data(), hout, no * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(g1.data(), gp, g1.size() * 8, hipMemcpyDeviceToHost));
+      CK(hipMemset(hout, 0, no * 4));
+      CK(dv(deconv_mfma_kernel<0>, pk + PL.dcm_off[1])()); CK(hipDeviceSynchronize());
+      CK(hipMemcpy(o2.data(), hout, no * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(g2.data(), gp, g2.size() * 8, hipMemcpyDeviceToHost));
+      double mx = 0, mref = 0, gs1 = 0, gs2 = 0;
+      for (size_t i = 0; i < no; ++i) { mx = fmax(mx, fabs((double)o1[i] - o2[i])); mref = fmax(mref, fabs((double)o1[i])); }
+      for (size_t i = 0; i < g1.size(); i += 4) { gs1 += g1[i]; gs2 += g2[i]; }
+      printf("  deconv_mfma vs deconv_px2: max|diff| %.3g (max|out| %.3g), GN sum %.9g vs %.9g\n", mx, mref, gs1, gs2);
+    }
+    run("deconv1 mfma", dv(deconv_mfma_kernel<0>, pk + PL.dcm_off[1]), fld);
+    run("deconv1 mfma no stores (1)", dv(deconv_mfma_kernel<1>, pk + PL.dcm_off[1]), fld);
+    run("deconv1 mfma no MFMA (2)", dv(deconv_mfma_kernel<2>, pk + PL.dcm_off[1]), fld);
+    run("deconv1 (H/2 -> H)", dc(deconv_px2_kernel<0>), fld);
+    run("deconv1 no stores (1)", dc(deconv_px2_kernel<1>), fld);
+    run("deconv1 no channel loop (2)", dc(deconv_px2_kernel<2>), fld);
+    run("deconv1 no staging loads (4)", dc(deconv_px2_kernel<4>), fld);
+    run("deconv1 skeleton (7)", dc(deconv_px2_kernel<7>), fld);
   }
   run("cell0 h3 DB0 PIPE0", [&] { return run_cell_h3<0, 1, 8, 0, 0, 0>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 DB0 PIPE1", [&] { return run_cell_h3<0, 1, 8, 0, 0, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
