@@ -100,11 +100,13 @@ typedef struct aarmvs_sweep_args {
   float* cost_out;                        /* [B,D,H,W] regulariser output, or NULL */
   float* slice_out;                       /* debug: [B,32,H,W] last plane's cost slice, or NULL */
   float* omega_out;                       /* debug: [nsrc,B,H,W] last plane's omega weights, or NULL */
-  hipStream_t aux_stream;                 /* optional second stream, or NULL: the next plane's
-                                             omega conv + GroupNorm statistics run on it,
-                                             overlapping the current plane's cost slice and
-                                             regulariser step (event fork/join per plane; at
-                                             return all work is ordered on `stream`)   */
+  hipStream_t aux_stream;                 /* optional second stream, or NULL: the cost slices
+                                             are computed in groups of up to 16 planes, and
+                                             the next group's (omega conv, GroupNorm
+                                             statistics, cost_x) run on it beside the current
+                                             group's regulariser steps (events per group; at
+                                             return all work is ordered on `stream`; results
+                                             are bit-identical either way)             */
 } aarmvs_sweep_args;
 
 size_t aarmvs_sweep_workspace_bytes(int B, int H, int W, int nsrc);
