@@ -147,6 +147,21 @@ int main(int argc, char** argv) {
           for (int j = 0; j < 4; ++j) { double d = fabs((double)x[j] - y[j]); if (d > 0) { ++nd; mx = d > mx ? d : mx; } }
         }
         printf("omega_mfma npl=8 16x16 tiles, 256 threads           %8.3f ms/plane  (t1 vs 16x32: %zu differ, max %.3g)\n", ms2 / 5 / 8, nd, mx);
+        auto t16 = [&](const char* name, auto kern) {
+          for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, dim3(nt16 * nsrc * 8, 1, B), dim3(OmegaTile<16>::NT), 0, 0, a, dpar, drel, ws.xbound);
+          CK(hipDeviceSynchronize());
+          CK(hipEventRecord(e0));
+          for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(kern, dim3(nt16 * nsrc * 8, 1, B), dim3(OmegaTile<16>::NT), 0, 0, a, dpar, drel, ws.xbound);
+          CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+          float m3; CK(hipEventElapsedTime(&m3, e0, e1));
+          printf("omega_mfma npl=8 16x16 %-28s %8.3f ms/plane\n", name, m3 / 5 / 8);
+        };
+        t16("double-buffered box (256)", omega_mfma_kernel<256, 16>);
+        t16("no MFMA (1)", omega_mfma_kernel<1, 16>);
+        t16("no box DMA (2)", omega_mfma_kernel<2, 16>);
+        t16("no sampling (4)", omega_mfma_kernel<4, 16>);
+        t16("no Y image (32)", omega_mfma_kernel<32, 16>);
+        t16("skeleton (31)", omega_mfma_kernel<31, 16>);
       }
       ablate("no MFMA (1)", omega_mfma_kernel<1, 32>, t1b, stb);
       ablate("no box DMA (2)", omega_mfma_kernel<2, 32>, t1b, stb);
