@@ -76,6 +76,12 @@ SIGNATURES = {
     "aarmvs_unet_step": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),
     "aarmvs_softmax_depth": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "aarmvs_group_norm_scratch_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "aarmvs_group_norm_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                          ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "aarmvs_group_norm_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                           c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p]),
     "aarmvs_cost_slice": (c_int, [c_void_p, ctypes.POINTER(c_void_p), c_void_p, c_void_p, c_void_p,
                                   c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),

@@ -93,6 +93,60 @@ def homo_warp_backward(grad_out: torch.Tensor, rel: torch.Tensor, depth: torch.T
     return grad_src
 
 
+class _GroupNormHip(torch.autograd.Function):
+    """GroupNorm on NCHW fp32 device tensors through aarmvs_group_norm_forward/_backward
+    (fixed-order fp64 statistics).  Once differentiable (no double backward)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups: int, eps: float):
+        _require_device(x)
+        xc = x.contiguous()
+        B, C = xc.shape[:2]
+        HW = xc[0, 0].numel()
+        y = torch.empty_like(xc)
+        mr = torch.empty(B, groups, 2, device=xc.device)
+        scratch = torch.empty(lib().aarmvs_group_norm_scratch_bytes(B, C, HW), dtype=torch.uint8,
+                              device=xc.device)
+        w = weight.contiguous() if weight is not None else None
+        bb = bias.contiguous() if bias is not None else None
+        check(lib().aarmvs_group_norm_forward(xc.data_ptr(), w.data_ptr() if w is not None else None,
+                                              bb.data_ptr() if bb is not None else None, B, C, HW,
+                                              groups, float(eps), y.data_ptr(), mr.data_ptr(),
+                                              scratch.data_ptr(), _stream()), "group_norm_forward")
+        ctx.save_for_backward(xc, w if w is not None else xc.new_empty(0), mr)
+        ctx.groups, ctx.has_w, ctx.has_b = groups, w is not None, bb is not None
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gy):
+        xc, w, mr = ctx.saved_tensors
+        g = gy.contiguous()
+        B, C = xc.shape[:2]
+        HW = xc[0, 0].numel()
+        dx = torch.empty_like(xc)
+        s1 = torch.empty(B, C, device=xc.device)
+        s2 = torch.empty(B, C, device=xc.device)
+        scratch = torch.empty(lib().aarmvs_group_norm_scratch_bytes(B, C, HW), dtype=torch.uint8,
+                              device=xc.device)
+        check(lib().aarmvs_group_norm_backward(g.data_ptr(), xc.data_ptr(),
+                                               w.data_ptr() if ctx.has_w else None, mr.data_ptr(),
+                                               B, C, HW, ctx.groups, dx.data_ptr(), s1.data_ptr(),
+                                               s2.data_ptr(), scratch.data_ptr(), _stream()),
+              "group_norm_backward")
+        dw = s1.sum(0) if ctx.has_w else None
+        db = s2.sum(0) if ctx.has_b else None
+        return dx, dw, db, None, None
+
+
+def group_norm(x: torch.Tensor, groups: int, weight=None, bias=None, eps: float = 1e-5):
+    """F.group_norm(x, groups, weight, bias, eps) for fp32 device tensors on the HIP kernels
+    (forward and backward)."""
+    if x.dtype != torch.float32:
+        raise AarmvsError(f"aarmvs.group_norm: expected float32, got {x.dtype}")
+    return _GroupNormHip.apply(x, weight, bias, groups, eps)
+
+
 def softmax_depth(cost: torch.Tensor) -> torch.Tensor:
     _require_device(cost)
     c = cost.contiguous()

@@ -159,6 +159,16 @@ hipError_t launch_finalize(const SweepGeom& g, const Workspace& ws, float* depth
                            float* conf_out, hipStream_t s);
 hipError_t launch_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
                                 hipStream_t s);
+// GroupNorm of NCHW [B][C][HW] fp32 (group_norm.hip): mean_rstd [B][G][2]; gamma / beta may
+// be null (1 / 0); scratch of gn_scratch_bytes(B, C, HW); bwd also writes s1 = sum dy xhat and
+// s2 = sum dy per (b, c) (the per-sample dgamma / dbeta terms)
+size_t gn_scratch_bytes(int B, int C, int HW);
+hipError_t launch_group_norm_fwd(const float* x, const float* gamma, const float* beta, int B,
+                                 int C, int HW, int G, float eps, float* y, float* mean_rstd,
+                                 void* scratch, hipStream_t s);
+hipError_t launch_group_norm_bwd(const float* dy, const float* x, const float* gamma,
+                                 const float* mean_rstd, int B, int C, int HW, int G, float* dx,
+                                 float* s1, float* s2, void* scratch, hipStream_t s);
 
 int cu_count();
 

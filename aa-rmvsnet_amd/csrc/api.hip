@@ -694,6 +694,30 @@ int aarmvs_fusion_filter(const aarmvs_fusion_args* a, hipStream_t stream) {
   return e == hipSuccess ? AARMVS_OK : hip_fail(e, "fusion_filter");
 }
 
+size_t aarmvs_group_norm_scratch_bytes(int B, int C, int HW) {
+  return (B < 1 || C < 1 || HW < 1) ? 0 : gn_scratch_bytes(B, C, HW);
+}
+
+int aarmvs_group_norm_forward(const float* x, const float* gamma, const float* beta, int B, int C,
+                              int HW, int G, float eps, float* y, float* mean_rstd, void* scratch,
+                              hipStream_t stream) {
+  if (!x || !y || !mean_rstd || !scratch || B < 1 || C < 1 || HW < 1 || G < 1 || C % G != 0 ||
+      B > 65535 || C > 65535)
+    return fail(AARMVS_ERR_INVALID, "group_norm_forward: bad arguments (need G | C)");
+  hipError_t e = launch_group_norm_fwd(x, gamma, beta, B, C, HW, G, eps, y, mean_rstd, scratch, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "group_norm_forward");
+}
+
+int aarmvs_group_norm_backward(const float* dy, const float* x, const float* gamma,
+                               const float* mean_rstd, int B, int C, int HW, int G, float* dx,
+                               float* s1, float* s2, void* scratch, hipStream_t stream) {
+  if (!dy || !x || !mean_rstd || !dx || !s1 || !s2 || !scratch || B < 1 || C < 1 || HW < 1 ||
+      G < 1 || C % G != 0 || B > 65535 || C > 65535)
+    return fail(AARMVS_ERR_INVALID, "group_norm_backward: bad arguments (need G | C)");
+  hipError_t e = launch_group_norm_bwd(dy, x, gamma, mean_rstd, B, C, HW, G, dx, s1, s2, scratch, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "group_norm_backward");
+}
+
 int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW, hipStream_t stream) {
   if (!cost || !prob || B < 1 || D < 1 || HW < 1)
     return fail(AARMVS_ERR_INVALID, "softmax_depth: bad arguments");

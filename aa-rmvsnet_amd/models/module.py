@@ -86,35 +86,22 @@ def _groups(channels: int, group_channel: int) -> int:
 
 
 class GroupNorm(nn.GroupNorm):
-    """nn.GroupNorm (same parameters and state_dict keys) whose GPU forward takes the
-    per-group statistics with ATen's multi-block reductions.
+    """nn.GroupNorm (same parameters and state_dict keys) whose GPU forward and backward
+    run on the library's HIP GroupNorm kernels (aarmvs_group_norm_forward/_backward).
 
     ATen's ROCm group_norm reduces each (sample, group) row in ONE thread block
     (RowwiseMomentsCUDAKernel): at B=1 with one or two groups over a full-resolution plane
     that is one or two busy CUs -- 0.9 ms per call at 640x512, over half of a training
-    step's GPU time in the BPTT recompute (rocprofv3).  Here mean and
-    variance come from torch.mean / torch.var (grid-wide reductions) and the output is
-    ATen's own form y = x * (rstd * gamma) + (beta - mean * rstd * gamma), differentiated
-    by autograd.  On the CPU the reference's F.group_norm runs unchanged."""
+    step's GPU time in the BPTT recompute (rocprofv3).  The HIP kernels take
+    the statistics as grid-wide fixed-order fp64 reductions and return ATen's output form
+    y = x * (rstd * gamma) + (beta - mean * rstd * gamma).  On the CPU the reference's
+    F.group_norm runs unchanged."""
 
     def forward(self, x):
         if not x.is_cuda:
             return super().forward(x)
-        B, C = x.shape[:2]
-        G = self.num_groups
-        xg = x.reshape(B, G, -1)
-        var, mean = torch.var_mean(xg, dim=-1, unbiased=False, keepdim=True)
-        rstd = torch.rsqrt(var + self.eps)                      # [B, G, 1]
-        cg = C // G
-        if self.affine:
-            w = self.weight.view(1, G, cg)
-            a = rstd * w                                        # [B, G, cg]
-            b = self.bias.view(1, G, cg) - mean * a
-        else:
-            a = rstd.expand(B, G, cg)
-            b = -mean * a
-        y = x.reshape(B, G, cg, -1) * a.unsqueeze(-1) + b.unsqueeze(-1)
-        return y.reshape_as(x)
+        return _ops.group_norm(x, self.num_groups, self.weight if self.affine else None,
+                               self.bias if self.affine else None, self.eps)
 
 
 def convgnrelu(in_channels, out_channels, kernel_size=3, stride=1, dilation=1, bias=True,

@@ -156,6 +156,20 @@ int aarmvs_wta_update(const float* cost, const float* depth_d, float* max_prob, 
 int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
                          hipStream_t stream);
 
+/* GroupNorm (nn.GroupNorm, module.py:98-103, 245-287; FeatNet and the BPTT recompute of
+ * the omega chain and the U-Net deconvs) on NCHW fp32 x [B,C,HW] with G groups (G | C).
+ * gamma / beta [C] may be NULL (weight 1, bias 0).  mean_rstd: [B,G,2] out (forward) / in
+ * (backward).  scratch: aarmvs_group_norm_scratch_bytes(B,C,HW) bytes of device memory.
+ * Backward writes dx [B,C,HW] and, per (b,c), s1 = sum_hw dy*xhat and s2 = sum_hw dy
+ * (dgamma = sum_b s1, dbeta = sum_b s2).  Statistics are fixed-order fp64 reductions. */
+size_t aarmvs_group_norm_scratch_bytes(int B, int C, int HW);
+int aarmvs_group_norm_forward(const float* x, const float* gamma, const float* beta, int B, int C,
+                              int HW, int G, float eps, float* y, float* mean_rstd, void* scratch,
+                              hipStream_t stream);
+int aarmvs_group_norm_backward(const float* dy, const float* x, const float* gamma,
+                               const float* mean_rstd, int B, int C, int HW, int G, float* dx,
+                               float* s1, float* s2, void* scratch, hipStream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Depth-map fusion core of one reference view (fusion.py:71-220, the per-view part of
  * filter_depth after file I/O): for every reference pixel the geometric consistency
