@@ -76,6 +76,10 @@ SIGNATURES = {
     "aarmvs_unet_step": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),
     "aarmvs_softmax_depth": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "aarmvs_lstm_gates_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                          c_void_p]),
+    "aarmvs_lstm_gates_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                           c_void_p, c_void_p, c_void_p]),
     "aarmvs_group_norm_scratch_bytes": (c_size_t, [c_int, c_int, c_int]),
     "aarmvs_group_norm_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                           ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -139,6 +139,49 @@ class _GroupNormHip(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
+class _LstmGatesHip(torch.autograd.Function):
+    """ConvLSTMCell gates (module.py:83-90) on the HIP kernels: (z, c_prev) -> (h, c)."""
+
+    @staticmethod
+    def forward(ctx, z, c_prev):
+        _require_device(z, c_prev)
+        zc, cp = z.contiguous(), c_prev.contiguous()
+        B, C4 = zc.shape[:2]
+        hid = C4 // 4
+        HW = zc[0, 0].numel()
+        if C4 != 4 * hid or tuple(cp.shape) != (B, hid) + tuple(zc.shape[2:]):
+            raise AarmvsError(f"aarmvs.lstm_gates: z {tuple(zc.shape)} vs c {tuple(cp.shape)}")
+        h = torch.empty_like(cp)
+        c = torch.empty_like(cp)
+        check(lib().aarmvs_lstm_gates_forward(zc.data_ptr(), cp.data_ptr(), B, hid, HW, h.data_ptr(),
+                                              c.data_ptr(), _stream()), "lstm_gates_forward")
+        ctx.save_for_backward(zc, cp)
+        return h, c
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dh, dc):
+        zc, cp = ctx.saved_tensors
+        B, C4 = zc.shape[:2]
+        hid, HW = C4 // 4, zc[0, 0].numel()
+        dh = dh.contiguous() if dh is not None else None
+        dc = dc.contiguous() if dc is not None else None
+        dz = torch.empty_like(zc)
+        dcp = torch.empty_like(cp)
+        check(lib().aarmvs_lstm_gates_backward(zc.data_ptr(), cp.data_ptr(),
+                                               dh.data_ptr() if dh is not None else None,
+                                               dc.data_ptr() if dc is not None else None, B, hid, HW,
+                                               dz.data_ptr(), dcp.data_ptr(), _stream()),
+              "lstm_gates_backward")
+        return dz, dcp
+
+
+def lstm_gates(z: torch.Tensor, c_prev: torch.Tensor):
+    """(h, c) = ConvLSTMCell's gate math on the conv output z [B,4*hid,H,W] and c_prev
+    [B,hid,H,W] (fp32 device tensors), forward and backward on the HIP kernels."""
+    return _LstmGatesHip.apply(z, c_prev)
+
+
 def group_norm(x: torch.Tensor, groups: int, weight=None, bias=None, eps: float = 1e-5):
     """F.group_norm(x, groups, weight, bias, eps) for fp32 device tensors on the HIP kernels
     (forward and backward)."""

@@ -166,6 +166,13 @@ size_t gn_scratch_bytes(int B, int C, int HW);
 hipError_t launch_group_norm_fwd(const float* x, const float* gamma, const float* beta, int B,
                                  int C, int HW, int G, float eps, float* y, float* mean_rstd,
                                  void* scratch, hipStream_t s);
+// ConvLSTMCell gate math (lstm_train.hip): z [B][4 hid][HW] -> h, c [B][hid][HW]; backward
+// from dh, dc (either may be null: zero) to dz and dc_prev
+hipError_t launch_lstm_gates_fwd(const float* z, const float* c_prev, int B, int hid, int HW,
+                                 float* h, float* c, hipStream_t s);
+hipError_t launch_lstm_gates_bwd(const float* z, const float* c_prev, const float* dh,
+                                 const float* dc, int B, int hid, int HW, float* dz, float* dc_prev,
+                                 hipStream_t s);
 hipError_t launch_group_norm_bwd(const float* dy, const float* x, const float* gamma,
                                  const float* mean_rstd, int B, int C, int HW, int G, float* dx,
                                  float* s1, float* s2, void* scratch, hipStream_t s);

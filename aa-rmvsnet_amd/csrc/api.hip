@@ -718,6 +718,22 @@ int aarmvs_group_norm_backward(const float* dy, const float* x, const float* gam
   return e == hipSuccess ? AARMVS_OK : hip_fail(e, "group_norm_backward");
 }
 
+int aarmvs_lstm_gates_forward(const float* z, const float* c_prev, int B, int hid, int HW, float* h,
+                              float* c, hipStream_t stream) {
+  if (!z || !c_prev || !h || !c || B < 1 || hid < 1 || HW < 1)
+    return fail(AARMVS_ERR_INVALID, "lstm_gates_forward: bad arguments");
+  hipError_t e = launch_lstm_gates_fwd(z, c_prev, B, hid, HW, h, c, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "lstm_gates_forward");
+}
+
+int aarmvs_lstm_gates_backward(const float* z, const float* c_prev, const float* dh, const float* dc,
+                               int B, int hid, int HW, float* dz, float* dc_prev, hipStream_t stream) {
+  if (!z || !c_prev || !dz || !dc_prev || B < 1 || hid < 1 || HW < 1)
+    return fail(AARMVS_ERR_INVALID, "lstm_gates_backward: bad arguments");
+  hipError_t e = launch_lstm_gates_bwd(z, c_prev, dh, dc, B, hid, HW, dz, dc_prev, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "lstm_gates_backward");
+}
+
 int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW, hipStream_t stream) {
   if (!cost || !prob || B < 1 || D < 1 || HW < 1)
     return fail(AARMVS_ERR_INVALID, "softmax_depth: bad arguments");

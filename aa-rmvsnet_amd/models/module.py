@@ -71,6 +71,9 @@ class ConvLSTMCell(nn.Module):
     def forward(self, input_tensor, cur_state):
         h, c = cur_state
         z = self.conv(torch.cat([input_tensor, h], dim=1))
+        if z.is_cuda and z.dtype == torch.float32:
+            # the gate math of :83-90 in one HIP kernel each way (the BPTT recompute)
+            return _ops.lstm_gates(z, c)
         zi, zf, zo, zg = torch.split(z, self.hidden_dim, dim=1)
         c_next = torch.sigmoid(zf) * c + torch.sigmoid(zi) * torch.tanh(zg)
         return torch.sigmoid(zo) * torch.tanh(c_next), c_next

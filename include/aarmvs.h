@@ -162,6 +162,15 @@ int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
  * (backward).  scratch: aarmvs_group_norm_scratch_bytes(B,C,HW) bytes of device memory.
  * Backward writes dx [B,C,HW] and, per (b,c), s1 = sum_hw dy*xhat and s2 = sum_hw dy
  * (dgamma = sum_b s1, dbeta = sum_b s2).  Statistics are fixed-order fp64 reductions. */
+/* ConvLSTMCell gate math (module.py:76-92) for the BPTT recompute: from the conv output z
+ * [B,4*hid,HW] (gates i, f, o, g in channel blocks) and c_prev [B,hid,HW] to h, c
+ * [B,hid,HW]; backward from dh, dc (either may be NULL: zero) to dz [B,4*hid,HW] and
+ * dc_prev [B,hid,HW], recomputing the gates from z. */
+int aarmvs_lstm_gates_forward(const float* z, const float* c_prev, int B, int hid, int HW, float* h,
+                              float* c, hipStream_t stream);
+int aarmvs_lstm_gates_backward(const float* z, const float* c_prev, const float* dh, const float* dc,
+                               int B, int hid, int HW, float* dz, float* dc_prev, hipStream_t stream);
+
 size_t aarmvs_group_norm_scratch_bytes(int B, int C, int HW);
 int aarmvs_group_norm_forward(const float* x, const float* gamma, const float* beta, int B, int C,
                               int HW, int G, float eps, float* y, float* mean_rstd, void* scratch,
