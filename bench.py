@@ -304,7 +304,7 @@ def train_bench(dev, planes=(4, 8), reps: int = 2):
                 s_per_plane=round(per_plane, 4), s_fixed=round(fixed, 3),
                 projected_s_per_step_d192=round(fixed + D_full * per_plane, 2),
                 note="D truncated to the measured counts; D=192 projected linearly",
-                backward="reverse-plane recompute in PyTorch on the GPU + HIP warp scatter + HIP GroupNorm",
+                backward="reverse-plane recompute on the GPU: MIOpen convs, HIP warp scatter, GroupNorm and LSTM gates",
                 loss_finite=ok)
 
 
