@@ -105,6 +105,9 @@ int main() {
   CHECK(aarmvs_unet_step(dummy, 1, 8, 9, 1, 0, dummy, dummy, dummy, nullptr) == AARMVS_ERR_INVALID);
   CHECK(aarmvs_softmax_depth(dummy, dummy, 1, 0, 64, nullptr) == AARMVS_ERR_INVALID);
   CHECK(aarmvs_softmax_depth(nullptr, dummy, 1, 4, 64, nullptr) == AARMVS_ERR_INVALID);
+  CHECK(aarmvs_lstm_gates_forward(nullptr, dummy, 1, 8, 64, dummy, dummy, nullptr) == AARMVS_ERR_INVALID);
+  CHECK(aarmvs_lstm_gates_backward(dummy, dummy, nullptr, nullptr, 1, 0, 64, dummy, dummy, nullptr) ==
+        AARMVS_ERR_INVALID);
   CHECK(aarmvs_group_norm_scratch_bytes(0, 16, 64) == 0);
   CHECK(aarmvs_group_norm_scratch_bytes(1, 16, 64) > 0);
   CHECK(aarmvs_group_norm_forward(dummy, nullptr, nullptr, 1, 16, 64, 3, 1e-5f, dummy, dummy, dummy,
