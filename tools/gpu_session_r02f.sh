@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2e measurement session: smoke, bench lines (headline with every leg, configs 2 and 5,
+# Round-2f measurement session: smoke, bench lines (headline with every leg, configs 2 and 5,
 # B=2), rocprofv3 kernel stats of the headline command, PMC byte passes (32 planes = two
 # plane groups, so per-launch bytes match the headline's 16-plane launches).
 source tools/gpu_round.sh
