@@ -44,6 +44,7 @@ from evidential.models import EvidentialModule, EvidentialShapeError
 from evidential.models import *  # noqa: F401,F403  (the reference: drmvsnet.py:5)
 
 from .module import *  # noqa: F401,F403  (reference re-exports models.module names)
+from .module import _HomoWarp
 from .module import (ConvLSTMCell, convgnrelu, deConvGnReLU, deformconvgnrelu,
                      homo_warping_depthwise, resnet_block_gn)
 
@@ -227,8 +228,27 @@ class _SweepTrain(torch.autograd.Function):
         ctx.sweep = sweep
         ctx.geom = (B, H, W, nsrc)
         ctx.meta = (ref_proj, src_projs, depth_values, nsrc)
+        ctx.rel = rel
         ctx.save_for_backward(ref, *srcs, *snaps)
         return cost
+
+    @staticmethod
+    def _plane(model, params, ref_l, srcs_l, rel, depth_d, hidden, gcost, gstate):
+        """One plane's recompute + vector-Jacobian product: gradients w.r.t. ref, srcs,
+        params and the incoming hidden state (None entries where unused)."""
+        x = model._cost_slice_rel(ref_l, srcs_l, rel, depth_d)
+        # UNetConvLSTM.forward replaces the list entries, so pass a shallow copy; idx 0 (plane
+        # 0) starts from _init_hidden's zero states, any other idx from `hidden`
+        cost, new_hidden = model.cost_regularization(
+            x, None if hidden is None else [list(hc) for hc in hidden], 0 if hidden is None else 1)
+        outs, gouts = [cost.squeeze(1)], [gcost]
+        if gstate is not None:
+            for hc, ghc in zip(new_hidden, gstate):
+                outs += list(hc)
+                gouts += list(ghc)
+        flat_hidden = [] if hidden is None else [t for hc in hidden for t in hc]
+        return torch.autograd.grad(outs, [ref_l] + srcs_l + list(params) + flat_hidden, gouts,
+                                   allow_unused=True)
 
     @staticmethod
     def backward(ctx, grad_cost):
@@ -245,42 +265,42 @@ class _SweepTrain(torch.autograd.Function):
         g_ref = torch.zeros_like(ref)
         g_srcs = [torch.zeros_like(s) for s in srcs]
         g_params = [torch.zeros_like(p) for p in params]
-        g_state = None
+        nparam = len(params)
+
+        def accumulate(grads):
+            if grads[0] is not None:
+                g_ref.add_(grads[0])
+            for i in range(nsrc):
+                if grads[1 + i] is not None:
+                    g_srcs[i].add_(grads[1 + i])
+            for i in range(nparam):
+                gp = grads[1 + nsrc + i]
+                if gp is not None:
+                    g_params[i].add_(gp)
+
+        def state_grads(grads, like):
+            gh = grads[1 + nsrc + nparam:]
+            return [[gh[2 * k] if gh[2 * k] is not None else torch.zeros_like(like[k][0]),
+                     gh[2 * k + 1] if gh[2 * k + 1] is not None else torch.zeros_like(like[k][1])]
+                    for k in range(len(like))]
+
+        rel = ctx.rel
         with torch.enable_grad():
             ref_l = ref.detach().requires_grad_(True)
             srcs_l = [s.detach().requires_grad_(True) for s in srcs]
-            for d in reversed(range(D)):
+            g_state = None
+            for d in range(D - 1, -1, -1):
                 if d > 0:
                     hidden = [[t.detach().contiguous().requires_grad_(True) for t in hc]
                               for hc in states[d - 1]]
-                    flat_hidden = [t for hc in hidden for t in hc]
                 else:
-                    hidden, flat_hidden = None, []
-                x = model._cost_slice_torch(ref_l, srcs_l, ref_proj, src_projs, depth_values[:, d])
-                # UNetConvLSTM.forward replaces the list entries, so pass a shallow copy
-                cost, new_hidden = model.cost_regularization(
-                    x, None if hidden is None else [list(hc) for hc in hidden], d)
-                outs = [cost.squeeze(1)]
-                gouts = [grad_cost[:, d]]
-                if g_state is not None:
-                    for hc, ghc in zip(new_hidden, g_state):
-                        outs += list(hc)
-                        gouts += list(ghc)
-                inputs = [ref_l] + srcs_l + list(params)
-                grads = torch.autograd.grad(outs, inputs + flat_hidden, gouts, allow_unused=True)
-                g_ref += grads[0] if grads[0] is not None else 0
-                for i in range(nsrc):
-                    if grads[1 + i] is not None:
-                        g_srcs[i] += grads[1 + i]
-                for i, p in enumerate(params):
-                    gp = grads[1 + nsrc + i]
-                    if gp is not None:
-                        g_params[i] += gp
+                    hidden = None
+                grads = _SweepTrain._plane(model, params, ref_l, srcs_l, rel,
+                                           depth_values[:, d].contiguous(), hidden,
+                                           grad_cost[:, d].contiguous(), g_state)
+                accumulate(grads)
                 if hidden is not None:
-                    gh = grads[1 + nsrc + len(params):]
-                    g_state = [[gh[2 * k] if gh[2 * k] is not None else torch.zeros_like(hidden[k][0]),
-                                gh[2 * k + 1] if gh[2 * k + 1] is not None else torch.zeros_like(hidden[k][1])]
-                               for k in range(len(hidden))]
+                    g_state = state_grads(grads, hidden)
         return (None, None, None, None, None, g_ref, *g_srcs, *g_params)
 
 
@@ -329,6 +349,16 @@ class EMVSNet(nn.Module):
             sw = _ops.DepthSweep({k: p.detach() for k, p in zip(_ops.SWEEP_KEYS, params)}, device)
             self._sweep_cache = (key, sw)
         return self._sweep_cache[1]
+
+    def _cost_slice_rel(self, ref, srcs, rel, depth):
+        """_cost_slice_torch with the relative projections precomputed on the device (rel
+        [nsrc,B,12], DepthSweep.relative): no host round trip per call."""
+        acc = None
+        for v, src in enumerate(srcs):
+            sq = (_HomoWarp.apply(src, rel[v], depth.reshape(-1)) - ref).pow(2)
+            term = (self.omega(sq) + 1) * sq
+            acc = term if acc is None else acc + term
+        return -1 * (acc / len(srcs))
 
     def _cost_slice_torch(self, ref, srcs, ref_proj, src_projs, depth):
         """-(sum_v (1+w_v)(warp_v - ref)^2)/(N-1), drmvsnet.py:307-319 (training recompute)."""

@@ -173,3 +173,4 @@ def test_training_backward_matches_cpu_autograd():
             continue
         tol = 1e-4 * max(np.abs(gr).max(), 1e-3 * gmax)
         np.testing.assert_allclose(p.grad.cpu().numpy(), gr, atol=tol, err_msg=k)
+
