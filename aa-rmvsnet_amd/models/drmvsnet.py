@@ -234,9 +234,10 @@ class _SweepTrain(torch.autograd.Function):
 
     @staticmethod
     def _plane(model, params, ref_l, srcs_l, rel, depth_d, hidden, gcost, gstate):
-        """One plane's recompute + vector-Jacobian product: gradients w.r.t. ref, srcs,
-        params and the incoming hidden state (None entries where unused)."""
-        x = model._cost_slice_rel(ref_l, srcs_l, rel, depth_d)
+        """One plane's recompute + vector-Jacobian product: gradients w.r.t. ref, the stacked
+        source views srcs_l [nsrc,B,C,H,W], params and the incoming hidden state (None
+        entries where unused)."""
+        x = model._cost_slice_views(ref_l, srcs_l, rel, depth_d)
         # UNetConvLSTM.forward replaces the list entries, so pass a shallow copy; idx 0 (plane
         # 0) starts from _init_hidden's zero states, any other idx from `hidden`
         cost, new_hidden = model.cost_regularization(
@@ -247,7 +248,7 @@ class _SweepTrain(torch.autograd.Function):
                 outs += list(hc)
                 gouts += list(ghc)
         flat_hidden = [] if hidden is None else [t for hc in hidden for t in hc]
-        return torch.autograd.grad(outs, [ref_l] + srcs_l + list(params) + flat_hidden, gouts,
+        return torch.autograd.grad(outs, [ref_l, srcs_l] + list(params) + flat_hidden, gouts,
                                    allow_unused=True)
 
     @staticmethod
@@ -263,23 +264,23 @@ class _SweepTrain(torch.autograd.Function):
         params = _sweep_params(model)
         D = depth_values.shape[1]
         g_ref = torch.zeros_like(ref)
-        g_srcs = [torch.zeros_like(s) for s in srcs]
+        srcs_stack = torch.stack(srcs)   # [nsrc,B,C,H,W]: one warp / omega pass for all views
+        g_srcs = torch.zeros_like(srcs_stack)
         g_params = [torch.zeros_like(p) for p in params]
         nparam = len(params)
 
         def accumulate(grads):
             if grads[0] is not None:
                 g_ref.add_(grads[0])
-            for i in range(nsrc):
-                if grads[1 + i] is not None:
-                    g_srcs[i].add_(grads[1 + i])
+            if grads[1] is not None:
+                g_srcs.add_(grads[1])
             for i in range(nparam):
-                gp = grads[1 + nsrc + i]
+                gp = grads[2 + i]
                 if gp is not None:
                     g_params[i].add_(gp)
 
         def state_grads(grads, like):
-            gh = grads[1 + nsrc + nparam:]
+            gh = grads[2 + nparam:]
             return [[gh[2 * k] if gh[2 * k] is not None else torch.zeros_like(like[k][0]),
                      gh[2 * k + 1] if gh[2 * k + 1] is not None else torch.zeros_like(like[k][1])]
                     for k in range(len(like))]
@@ -287,7 +288,7 @@ class _SweepTrain(torch.autograd.Function):
         rel = ctx.rel
         with torch.enable_grad():
             ref_l = ref.detach().requires_grad_(True)
-            srcs_l = [s.detach().requires_grad_(True) for s in srcs]
+            srcs_l = srcs_stack.detach().requires_grad_(True)
             g_state = None
             for d in range(D - 1, -1, -1):
                 if d > 0:
@@ -301,7 +302,7 @@ class _SweepTrain(torch.autograd.Function):
                 accumulate(grads)
                 if hidden is not None:
                     g_state = state_grads(grads, hidden)
-        return (None, None, None, None, None, g_ref, *g_srcs, *g_params)
+        return (None, None, None, None, None, g_ref, *g_srcs.unbind(0), *g_params)
 
 
 class _SoftmaxDepth(torch.autograd.Function):
@@ -350,15 +351,21 @@ class EMVSNet(nn.Module):
             self._sweep_cache = (key, sw)
         return self._sweep_cache[1]
 
-    def _cost_slice_rel(self, ref, srcs, rel, depth):
-        """_cost_slice_torch with the relative projections precomputed on the device (rel
-        [nsrc,B,12], DepthSweep.relative): no host round trip per call."""
-        acc = None
-        for v, src in enumerate(srcs):
-            sq = (_HomoWarp.apply(src, rel[v], depth.reshape(-1)) - ref).pow(2)
-            term = (self.omega(sq) + 1) * sq
-            acc = term if acc is None else acc + term
-        return -1 * (acc / len(srcs))
+    def _cost_slice_views(self, ref, srcs, rel, depth):
+        """_cost_slice_torch for the stacked source views srcs [nsrc,B,C,H,W] with the
+        relative projections precomputed on the device (rel [nsrc,B,12],
+        DepthSweep.relative): the views ride the batch axis of one warp and one omega pass
+        (the omega GroupNorms normalise per sample, so this is the per-view arithmetic), and
+        there is no host round trip."""
+        nv, B, C, H, W = srcs.shape
+        warped = _HomoWarp.apply(srcs.reshape(nv * B, C, H, W), rel.reshape(nv * B, 12),
+                                 depth.reshape(-1).repeat(nv))
+        sq = (warped.view(nv, B, C, H, W) - ref).pow(2)
+        term = (self.omega(sq.view(nv * B, C, H, W)).view(nv, B, 1, H, W) + 1) * sq
+        acc = term[0]
+        for v in range(1, nv):   # the reference's view order (drmvsnet.py:309-318)
+            acc = acc + term[v]
+        return -1 * (acc / nv)
 
     def _cost_slice_torch(self, ref, srcs, ref_proj, src_projs, depth):
         """-(sum_v (1+w_v)(warp_v - ref)^2)/(N-1), drmvsnet.py:307-319 (training recompute)."""
