@@ -31,7 +31,7 @@ import numpy as np
 import torch
 from torch.utils.data import DataLoader, Subset
 
-from .dist import env, shard_range
+from .dist import env, local_device_index, shard_range
 from .fusion import save_pfm
 
 
@@ -76,7 +76,10 @@ def save_depth(args, rank: int = 0, world: int = 1, device=None, model=None) -> 
     """Run rank's shard of the eval set; returns the reference-view filenames it wrote."""
     from datasets import find_dataset_def
     from models import EMVSNet
-    device = torch.device(device or f"cuda:{env()[1]}")
+    device = torch.device(device or f"cuda:{local_device_index(env()[1])}")
+    if device.type == "cuda":
+        # libaarmvs launches on the current device's stream: make it this rank's GPU
+        torch.cuda.set_device(device)
     ds = find_dataset_def(args.dataset)(args.testpath, args.testlist, "test", args.view_num,
                                         args.numdepth, args.interval_scale,
                                         inverse_depth=args.inverse_depth, adaptive_scaling=True,

@@ -8,6 +8,7 @@ path has no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import functools
 
 import torch
 
@@ -20,6 +21,31 @@ SWEEP_KEYS = tuple(SWEEP_SHAPES.keys())  # raw-blob order (include/aarmvs.h)
 
 def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
+
+
+def _device_of(args, kwargs):
+    for a in list(args) + list(kwargs.values()):
+        if isinstance(a, DepthSweep):
+            return a.device
+        if torch.is_tensor(a) and a.is_cuda:
+            return a.device
+        if isinstance(a, torch.device):
+            return a
+    return None
+
+
+def _on_tensor_device(fn):
+    """Runs ``fn`` with the current device set to its first device tensor's (or its
+    DepthSweep's) device, so ``_stream()`` is that device's current stream and the library's
+    hipGetDevice() agrees with the tensors, whatever device the caller left current."""
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        dev = _device_of(args, kwargs)
+        if dev is None or dev.type != "cuda" or dev.index is None:
+            return fn(*args, **kwargs)
+        with torch.cuda.device(dev):
+            return fn(*args, **kwargs)
+    return wrapper
 
 
 def _ptr(t: torch.Tensor | None) -> int | None:
@@ -51,6 +77,7 @@ def relative_projection(src_proj: torch.Tensor, ref_proj: torch.Tensor) -> torch
     return torch.matmul(s, torch.inverse(r))[:, :3, :4].contiguous()
 
 
+@_on_tensor_device
 def pack_params(params: dict, device) -> torch.Tensor:
     """Flatten the 48 sweep tensors (checkpoint keys) and pack them on the device."""
     missing = [k for k in SWEEP_KEYS if k not in params]
@@ -66,6 +93,7 @@ def pack_params(params: dict, device) -> torch.Tensor:
     return packed
 
 
+@_on_tensor_device
 def homo_warp(src_fea: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor) -> torch.Tensor:
     """homo_warping_depthwise on the GPU for precomputed rel [B,3,4] and depth [B]."""
     _require_device(src_fea)
@@ -79,6 +107,7 @@ def homo_warp(src_fea: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor) -> 
     return out
 
 
+@_on_tensor_device
 def homo_warp_backward(grad_out: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor,
                        src_shape) -> torch.Tensor:
     """d loss / d src_fea of homo_warp: bilinear scatter-add of grad_out (fp32 atomics)."""
@@ -98,6 +127,7 @@ class _GroupNormHip(torch.autograd.Function):
     (fixed-order fp64 statistics).  Once differentiable (no double backward)."""
 
     @staticmethod
+    @_on_tensor_device
     def forward(ctx, x, weight, bias, groups: int, eps: float):
         _require_device(x)
         xc = x.contiguous()
@@ -119,6 +149,7 @@ class _GroupNormHip(torch.autograd.Function):
 
     @staticmethod
     @torch.autograd.function.once_differentiable
+    @_on_tensor_device
     def backward(ctx, gy):
         xc, w, mr = ctx.saved_tensors
         g = gy.contiguous()
@@ -143,6 +174,7 @@ class _LstmGatesHip(torch.autograd.Function):
     """ConvLSTMCell gates (module.py:83-90) on the HIP kernels: (z, c_prev) -> (h, c)."""
 
     @staticmethod
+    @_on_tensor_device
     def forward(ctx, z, c_prev):
         _require_device(z, c_prev)
         zc, cp = z.contiguous(), c_prev.contiguous()
@@ -160,6 +192,7 @@ class _LstmGatesHip(torch.autograd.Function):
 
     @staticmethod
     @torch.autograd.function.once_differentiable
+    @_on_tensor_device
     def backward(ctx, dh, dc):
         zc, cp = ctx.saved_tensors
         B, C4 = zc.shape[:2]
@@ -190,6 +223,7 @@ def group_norm(x: torch.Tensor, groups: int, weight=None, bias=None, eps: float 
     return _GroupNormHip.apply(x, weight, bias, groups, eps)
 
 
+@_on_tensor_device
 def softmax_depth(cost: torch.Tensor) -> torch.Tensor:
     _require_device(cost)
     c = cost.contiguous()
@@ -200,6 +234,7 @@ def softmax_depth(cost: torch.Tensor) -> torch.Tensor:
     return out
 
 
+@_on_tensor_device
 def wta_update(cost: torch.Tensor, depth_d: torch.Tensor, max_prob: torch.Tensor,
                depth_map: torch.Tensor, exp_sum: torch.Tensor) -> None:
     """In-place online WTA update of one plane (aarmvs_wta_update, drmvsnet.py:324-334):
@@ -266,6 +301,7 @@ class DepthSweep:
         rel = torch.stack([relative_projection(sp, ref_proj) for sp in src_projs])  # [nsrc,B,3,4]
         return rel.reshape(len(src_projs), B, 12).to(self.device).contiguous()
 
+    @_on_tensor_device
     def __call__(self, ref_fea, src_feas, ref_proj, src_projs, depth_values, *,
                  want_depth=True, want_cost=False, d_range=None, debug=False, cost_out=None,
                  rel=None):
@@ -391,6 +427,7 @@ class DepthSweep:
             out.append(pair)
         return out
 
+    @_on_tensor_device
     def cost_slice(self, ref_fea, src_feas, ref_proj, src_projs, depth, want_omega=False):
         """One plane's cost slice x [B,32,H,W] (aarmvs_cost_slice; drmvsnet.py:307-319) at
         depth [B]; returns (x, omega [nsrc,B,H,W] or None).  Uses this object's workspace."""
@@ -417,6 +454,7 @@ class DepthSweep:
                                       x.data_ptr(), _ptr(om), _stream()), "cost_slice")
         return x, om
 
+    @_on_tensor_device
     def unet_step(self, x: torch.Tensor, step: int, nsrc: int = 1) -> torch.Tensor:
         _require_device(x)
         x = x.contiguous()

@@ -72,6 +72,9 @@ def train(args, rank: int = 0, world: int = 1, device=None, log=print) -> dict:
     from evidential.models import loss_der
     from models import EMVSNet, mvsnet_cls_loss
     device = torch.device(device or f"cuda:{local_device_index(env()[1])}")
+    if device.type == "cuda":
+        # libaarmvs launches on the current device's stream: make it this rank's GPU
+        torch.cuda.set_device(device)
     torch.manual_seed(args.seed)
     init_process_group(device)
     ds = find_dataset_def(args.dataset)(args.trainpath, args.trainlist, "train", args.view_num,
@@ -98,7 +101,9 @@ def train(args, rank: int = 0, world: int = 1, device=None, log=print) -> dict:
         saved = sorted((f for f in os.listdir(args.logdir) if f.endswith(".ckpt")),
                        key=lambda f: int(f.split("_")[-1].split(".")[0]))
         state = torch.load(os.path.join(args.logdir, saved[-1]), map_location="cpu", weights_only=True)
-        model.load_state_dict(state["model"])
+        # a checkpoint saved at another world size has (or lacks) DDP's 'module.' prefix
+        core = model.module if isinstance(model, torch.nn.parallel.DistributedDataParallel) else model
+        core.load_state_dict(_strip_module(state["model"]))
         optimizer.load_state_dict(state["optimizer"])
         start_epoch = state["epoch"] + 1
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=args.epochs, eta_min=2e-06)

@@ -274,10 +274,6 @@ __device__ __forceinline__ size_t st_index(int b, int v, int k, int nsrc) {
 // omega_conv tiles are 32 pixels wide, 16 rows (one thread per pixel).
 constexpr int kTileW = 32, kTileH = 16, kTileThreads = kTileW * kTileH;
 constexpr int kTileWaves = kTileThreads / 64;
-constexpr int kCHH = kTileH + 2, kCHW = kTileW + 2;   // omega_conv haloed tile
-constexpr int kCRing = 2 * kCHW + 2 * kTileH;         // its halo-only (ring) pixels
-constexpr int kCBoxPx = 1024;   // omega_conv LDS source box: 32-B pixels (one chunk)
-static_assert(kCRing <= kTileThreads, "one ring pixel per thread at most");
 
 // XCD-aware tile order: blocks are dealt to the 8 XCDs round-robin, so XCD k takes the
 // k-th contiguous band of tiles and neighbouring tiles (which share source rows) share
@@ -587,24 +583,6 @@ typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-// split-fp16 sq image (MFMA A operand), 32 B per pixel: slot 0 the fp16 hi parts of the
-// 8 channels, slot 1 fp16(v - hi), the slots swapped when bit 3 of p is set (img_slot's
-// swizzle); channels 4h..4h+3 are halves 4h..4h+3 of each slot.  v is stored x 2^-4
-// (exact) so that |difference| up to 1024 stays in fp16 range.
-constexpr float kSqScale = 0.0625f;
-__device__ __forceinline__ void sq_st16(_Float16* img, uint32_t p, int h, float4 v) {
-  v.x *= kSqScale;
-  v.y *= kSqScale;
-  v.z *= kSqScale;
-  v.w *= kSqScale;
-  const half4 hi = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-  const half4 lo = {(_Float16)(v.x - (float)hi.x), (_Float16)(v.y - (float)hi.y),
-                    (_Float16)(v.z - (float)hi.z), (_Float16)(v.w - (float)hi.w)};
-  const uint32_t sw = (p >> 3) & 1u;
-  *reinterpret_cast<half4*>(img + p * 16u + 8u * sw + 4u * (uint32_t)h) = hi;
-  *reinterpret_cast<half4*>(img + p * 16u + 8u * (sw ^ 1u) + 4u * (uint32_t)h) = lo;
-}
-
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 // LDS-DMA, 16 B per lane: lane l of the wave lands at wave_dst + 16 l (wave_dst uniform);
 // an offset past the buffer's range loads zeros
@@ -615,286 +593,6 @@ __device__ __forceinline__ void dma_wait() {
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
 }
 
-// omega_conv: t1 of plane d_next for one (tile, view) per block.  Per 8-channel chunk c:
-// the chunk's source box (bounding box of the block's bilinear taps) and the haloed
-// (8+2) x 34 reference tile arrive in LDS by LDS-DMA, issued while the previous chunk's
-// conv runs; the squared difference on the haloed tile goes to the sq image (own pixel
-// by every thread, ring pixels by threads 0..kCRing-1); each thread accumulates its
-// pixel's conv3x3 32->4 over the chunks (fmaf chains, scalar weights, taps unrolled).
-// A box past kCBoxPx pixels is sampled from global memory instead.
-// ABL: ablation bits for the diagnostic harness only (tools/microbench/pipe_bench.cpp;
-// the library instantiates ABL = 0): 1 no conv, 2 no squared differences, 4 no box
-// loads, 8 conv tap loop rolled, 16 the eight off-centre taps on the matrix cores: per
-// chunk a GEMM y[q][tap, co] += sq[q][8 ch] x W[8 ch][tap, co] over the 612 haloed
-// pixels q (M tiles of 16, N = 8 taps x 4 co = 2 tiles of 16, v_mfma_f32_16x16x32_f16
-// with K = [sq hi | sq lo | sq hi | sq lo] x [W hi | W hi | W lo | W lo]: the four split
-// products), accumulated over the chunks in registers; then out[p] = sum over taps of
-// y[p + tap offset][tap] through LDS (two 16-column rounds); the centre tap stays a VALU
-// fmaf chain on the thread's own sq.  Parity-green but slower: 1.18 vs 0.73 ms per plane
-// (the accumulators need 3 waves per SIMD: 8 waves per CU at 16-row tiles), and 1.59 vs
-// 1.29 ms at 12-row tiles where both fit 12 waves per CU: the kernel is bound by block
-// latency (the chunk pipeline's DMA waits and barriers), not by the conv's VALU issue.
-template <int ABL = 0>
-__global__ void __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu((ABL & 16) ? 3 : 4)))
-omega_conv_kernel(PipeArgs a,
-                                                                  const float* __restrict__ P,
-                                                                  const float* __restrict__ Rel) {
-  constexpr int NHP = kCHH * kCHW;                                      // haloed tile pixels
-  constexpr int NB = (2 * kCBoxPx + kTileThreads - 1) / kTileThreads;   // box pieces per thread
-  constexpr int NR = (2 * NHP + kTileThreads - 1) / kTileThreads;       // ref pieces per thread
-  // one LDS array: source box | reference tile | sq tile (the MFMA epilogue's y image
-  // reuses the box and reference space)
-  __shared__ __attribute__((aligned(16))) float smem[(kCBoxPx + 1) * 8 + 2 * NHP * 8];
-  float* const box = smem;
-  float* const rt = smem + (kCBoxPx + 1) * 8;
-  float* const sqt = rt + NHP * 8;
-  __shared__ int red[kTileWaves][4];
-  __shared__ float wsum[kTileWaves][2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.z;
-  const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
-  // the views of one tile are consecutive blocks on one XCD: the reference tile is
-  // fetched from HBM once and re-read from that XCD's L2
-  const int seq = xcd_tile(blockIdx.x, gridDim.x);
-  const int tile = seq / (nsrc * a.npl), vk = seq - tile * (nsrc * a.npl);
-  const int v = vk / a.npl, kp = vk - v * a.npl;
-  const int tiles_x = (W + kTileW - 1) / kTileW;
-  const int y0 = (tile / tiles_x) * kTileH, x0 = (tile % tiles_x) * kTileW;
-  const int ty = tid / kTileW, tx = tid % kTileW;
-  const int gy = y0 + ty, gx = x0 + tx;
-  const bool inside = gy < H && gx < W;
-  const uint32_t own_hp = (uint32_t)((ty + 1) * kCHW + tx + 1);
-  // this thread's ring pixel
-  const bool has_ring = tid < kCRing;
-  int hy, hx;
-  if (tid < kCHW) {
-    hy = 0;
-    hx = tid;
-  } else if (tid < 2 * kCHW) {
-    hy = kCHH - 1;
-    hx = tid - kCHW;
-  } else if (tid < 2 * kCHW + kTileH) {
-    hy = 1 + tid - 2 * kCHW;
-    hx = 0;
-  } else {
-    hy = 1 + tid - 2 * kCHW - kTileH;
-    hx = kCHW - 1;
-  }
-  const int ry = y0 - 1 + hy, rx = x0 - 1 + hx;
-  const bool ring_in = has_ring && ry >= 0 && ry < H && rx >= 0 && rx < W;
-  const uint32_t ring_hp = (uint32_t)(hy * kCHW + hx);
-  if (tid < 8) box[kCBoxPx * 8 + tid] = 0.f;   // the zero pixel
-
-  const float dep = a.dvals[b * a.D + a.d_next + kp];
-  const float* __restrict__ m = Rel + 12 * (v * a.B + b);
-  const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);   // one view's c8 image
-  const uint32_t cbytes = (uint32_t)HW * 32u;                // one chunk image
-  const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(a.ref + (size_t)b * kC * HW, fbytes);
-  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.src[v] + (size_t)b * kC * HW, fbytes);
-  TapF tfo{}, tfr{};
-  int lx = INT_MAX, ly = INT_MAX, bhx = INT_MIN, bhy = INT_MIN;
-  if (inside) {
-    tfo = tap_f(m, dep, gx, gy, H, W);
-    box_extend(tfo, H, W, lx, ly, bhx, bhy);
-  }
-  if (ring_in) {
-    tfr = tap_f(m, dep, rx, ry, H, W);
-    box_extend(tfr, H, W, lx, ly, bhx, bhy);
-  }
-  const Box bx = box_reduce(lx, ly, bhx, bhy, red);
-  const bool lds = bx.nx * bx.ny <= min(kCBoxPx, a.box_cap);
-  const uint32_t zp = lds ? (uint32_t)kCBoxPx : fbytes / 32u;
-  const TapP to = tap_p(tfo, inside, H, W, lds, bx, zp), tr = tap_p(tfr, ring_in, H, W, lds, bx, zp);
-  // chunk-0 byte offsets of this thread's DMA pieces (chunk c adds c * cbytes)
-  const int items = (lds && !(ABL & 4)) ? bx.nx * bx.ny * 2 : 0;
-  const uint32_t mg = box_magic(bx.nx);
-  uint32_t boff[NB], roff[NR];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const int i = tid + j * kTileThreads, p = i >> 1, r = box_row(p, bx.nx, mg);
-    const uint32_t gp = __umul24((uint32_t)(bx.y0 + r), (uint32_t)W) + (uint32_t)bx.x0 +
-                        ((uint32_t)p - __umul24((uint32_t)r, (uint32_t)bx.nx));
-    boff[j] = gp * 32u + 16u * (uint32_t)img_half((uint32_t)p, i & 1);
-  }
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const int i = tid + j * kTileThreads, hp = i >> 1, py = hp / kCHW;
-    const int y = y0 - 1 + py, x = x0 - 1 + (hp - py * kCHW);
-    roff[j] = (y >= 0 && y < H && x >= 0 && x < W)
-                  ? (__umul24((uint32_t)y, (uint32_t)W) + (uint32_t)x) * 32u + 16u * (uint32_t)img_half((uint32_t)hp, i & 1)
-                  : fbytes;   // zero padding
-  }
-  auto stage = [&](int c) {
-    const uint32_t cb = (uint32_t)c * cbytes;
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-      if (tid + j * kTileThreads < items)
-        dma16(rsrc, box + (j * kTileThreads + wave * 64) * 4, boff[j] + cb);
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-      if (tid + j * kTileThreads < 2 * NHP)
-        dma16(rref, rt + (j * kTileThreads + wave * 64) * 4, roff[j] < cbytes ? roff[j] + cb : fbytes);
-  };
-  auto sample = [&](const TapP& t, int c, int h) {
-    if (lds)
-      return bil4(img_ld(box, t.pix[0], h), img_ld(box, t.pix[1], h), img_ld(box, t.pix[2], h),
-                  img_ld(box, t.pix[3], h), t);
-    const int s = 2 * c + h;
-    return bil4(ld_c8(rsrc, t.pix[0], s, HW), ld_c8(rsrc, t.pix[1], s, HW),
-                ld_c8(rsrc, t.pix[2], s, HW), ld_c8(rsrc, t.pix[3], s, HW), t);
-  };
-  const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]
-  const float* __restrict__ b0 = P + a.off_ob0;
-  // MFMA conv: M tiles t = wave + 8 i of the haloed tile (rows 16 t .. 16 t + 15 in
-  // haloed-pixel order; the last tile's rows past NHP re-read pixel NHP - 1 and are
-  // dropped), this lane's A row and slot (k8 group lane / 16: hi, lo, hi, lo)
-  constexpr bool MF = (ABL & 16) != 0;
-  constexpr int MT = (NHP + 15) / 16, MTW = (MT + kTileWaves - 1) / kTileWaves;
-  _Float16* sqh = reinterpret_cast<_Float16*>(sqt);
-  const half8* __restrict__ owb = reinterpret_cast<const half8*>(P + a.off_owb);
-  auto arow = [&](int i) {
-    const uint32_t q = (uint32_t)min(16 * (wave + kTileWaves * i) + (lane & 15), NHP - 1);
-    return q * 32u + 16u * (((uint32_t)(lane >> 4) & 1u) ^ ((q >> 3) & 1u));
-  };
-  floatx4 acc[MTW][2];
-#pragma unroll
-  for (int i = 0; i < MTW; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  stage(0);
-  dma_wait();
-  __syncthreads();
-  float o4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-#pragma unroll
-    for (int h = 0; h < 2 && !(ABL & 2); ++h) {
-      const float4 so = sqdiff4(sample(to, c, h), img_ld(rt, own_hp, h));
-      if constexpr (MF) {
-        sq_st16(sqh, own_hp, h, so);
-        // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel
-        const float qq[4] = {so.x, so.y, so.z, so.w};
-        const float* wt = w0t + (4 * kC + 8 * c + 4 * h) * 4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int co = 0; co < 4; ++co) o4[co] = fmaf(qq[j], wt[j * 4 + co], o4[co]);
-      } else {
-        img_st(sqt, own_hp, h, so);
-      }
-      if (has_ring) {
-        const float4 sr = sqdiff4(sample(tr, c, h), img_ld(rt, ring_hp, h));
-        if (MF) sq_st16(sqh, ring_hp, h, sr);
-        else img_st(sqt, ring_hp, h, sr);
-      }
-      // MFMA conv: keep the halves' gathers from being hoisted together (their registers
-      // would be live alongside the accumulators)
-      if constexpr (MF) __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();   // sq visible; this chunk's box / reference reads are done
-    if (c < 3) stage(c + 1);
-    // omega.reweight_network.0.0: conv3x3 32->4, pad 1 (input channels 8c..8c+7)
-    auto conv_tap = [&](int tap) {
-      const uint32_t hp = own_hp + (uint32_t)((tap / 3 - 1) * kCHW + (tap % 3 - 1));
-      const float4 qa = img_ld(sqt, hp, 0), qb = img_ld(sqt, hp, 1);
-      const float qq[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
-      const float* wt = w0t + (tap * kC + 8 * c) * 4;   // [j][co], contiguous
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int co = 0; co < 4; ++co) o4[co] = fmaf(qq[j], wt[j * 4 + co], o4[co]);
-    };
-    // fully unrolled: the LDS reads and weight loads of later taps are issued ahead
-    // (0.72 vs 0.82 ms per plane at the headline geometry with a rolled loop)
-    if constexpr (ABL & 1) {
-    } else if constexpr (MF) {
-      const half8 bf0 = owb[(c * 2 + 0) * 64 + lane], bf1 = owb[(c * 2 + 1) * 64 + lane];
-#pragma unroll
-      for (int i = 0; i < MTW; ++i) {
-        if (wave + kTileWaves * i < MT) {
-          const half8 af = *reinterpret_cast<const half8*>(reinterpret_cast<const char*>(sqh) + arow(i));
-          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf0, acc[i][0], 0, 0, 0);
-          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf1, acc[i][1], 0, 0, 0);
-        }
-      }
-    } else if constexpr ((ABL & 8) != 0) {
-#pragma unroll 1
-      for (int tap = 0; tap < 9; ++tap) conv_tap(tap);
-    } else {
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) conv_tap(tap);
-    }
-    if (c < 3) {
-      dma_wait();
-      __syncthreads();   // next chunk's images visible; the conv's sq reads are done
-    }
-  }
-  if constexpr (MF) {
-    // y image [haloed pixel][20 floats] over the box and reference space (last read in
-    // chunk 3's sq phase): D[row = 4 (lane / 16) + r][col = lane % 16] of tile t, column
-    // n = 4 (tap slot) + co; N tile k holds tap slots 4k .. 4k + 3 (taps 0..3, 5..8)
-    constexpr int YS = 20;
-    static_assert(NHP * YS <= (kCBoxPx + 1) * 8 + NHP * 8, "y image fits the box + reference space");
-    float* const y = smem;
-    float g4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (k) __syncthreads();   // round 0's gathers are done
-#pragma unroll
-      for (int i = 0; i < MTW; ++i) {
-        if (wave + kTileWaves * i < MT) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int q = 16 * (wave + kTileWaves * i) + 4 * (lane >> 4) + r;
-            if (q < NHP) y[q * YS + (lane & 15)] = acc[i][k][r];
-          }
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int tap = 4 * k + u < 4 ? 4 * k + u : 4 * k + u + 1;
-        const uint32_t q = own_hp + (uint32_t)((tap / 3 - 1) * kCHW + (tap % 3 - 1));
-        const float4 yv = *reinterpret_cast<const float4*>(y + q * YS + 4 * u);
-        g4[0] += yv.x;
-        g4[1] += yv.y;
-        g4[2] += yv.z;
-        g4[3] += yv.w;
-      }
-    }
-    const float isc = P[a.off_owb_scale] * (1.0f / kSqScale);
-#pragma unroll
-    for (int co = 0; co < 4; ++co) o4[co] = fmaf(g4[co], isc, o4[co]);
-  }
-  float ps = 0.f, pss = 0.f;
-  if (inside) {
-    float4 out;
-    out.x = o4[0] + b0[0];
-    out.y = o4[1] + b0[1];
-    out.z = o4[2] + b0[2];
-    out.w = o4[3] + b0[3];
-    a.t1_next[kp * a.t1_kstride + ((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
-    ps = (out.x + out.y) + (out.z + out.w);
-    pss = (out.x * out.x + out.y * out.y) + (out.z * out.z + out.w * out.w);
-  }
-  ps = wave_sum(ps);
-  pss = wave_sum(pss);
-  if (lane == 0) {
-    wsum[wave][0] = ps;
-    wsum[wave][1] = pss;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    double s0 = 0.0, s1 = 0.0;
-    for (int w = 0; w < kTileWaves; ++w) {
-      s0 += wsum[w][0];
-      s1 += wsum[w][1];
-    }
-    part_put(a, kp, b, v, tile, s0, s1);
-  }
-}
-
-// the library's omega_conv variant (0: VALU conv)
-constexpr int kOmegaConvAbl = 0;
 
 // ---------------------------------------------------------------------------
 // omega_mfma: t1 of plane d_next for one (tile, view) per block with the conv3x3 32->4 on
@@ -1301,14 +999,6 @@ static int pipe_box_cap() {
   return (s && *s) ? std::max(4, std::atoi(s)) : INT_MAX;
 }
 
-// omega conv variant: 2 (default) omega_mfma, the conv3x3 on the matrix cores (split-fp16,
-// parity-green in every GPU test; 703-715 vs 718-753 us per plane at the headline in two
-// A/B runs on two boxes, profiles/r02_*); 1 the VALU omega_conv (AARMVS_OMEGA=valu)
-static int omega_variant() {
-  const char* s = std::getenv("AARMVS_OMEGA");
-  return (s && std::strcmp(s, "valu") == 0) ? 1 : 2;
-}
-
 static PipeArgs pipe_args_c8(const CostArgs& ca, const SweepGeom& g, const Workspace& ws) {
   PipeArgs a = pipe_args(ca, g, ws);
   // the pipeline reads the c8 copies of the features in the workspace
@@ -1357,14 +1047,7 @@ hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Work
   // the group's statistics accumulate from zero
   if ((e = hipMemsetAsync(ws.omega_stats, 0, (size_t)n * ws.omega_stats_bytes, s)) != hipSuccess)
     return e;
-  if (omega_variant() == 1) {
-    const int ntiles = ((g.W + kTileW - 1) / kTileW) * ((g.H + kTileH - 1) / kTileH);
-    ProfScope ps(s, K_OMEGA_CONV);
-    a.part_n = ntiles;
-    hipLaunchKernelGGL(omega_conv_kernel<kOmegaConvAbl>, dim3(ntiles * g.nsrc * n, 1, g.B),
-                       dim3(kTileThreads), 0, s, a, a.params, a.rel);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  } else {
+  {
     const int ntiles = OmegaTile<kOmegaTW>::tiles(g.H, g.W);
     ProfScope ps(s, K_OMEGA_CONV);
     a.part_n = ntiles;

@@ -101,7 +101,8 @@ class GroupNorm(nn.GroupNorm):
     F.group_norm runs unchanged."""
 
     def forward(self, x):
-        if not x.is_cuda:
+        if not x.is_cuda or x.dtype != torch.float32:
+            # CPU, and the dtypes the HIP kernels do not take (autocast, gradcheck in fp64)
             return super().forward(x)
         return _ops.group_norm(x, self.num_groups, self.weight if self.affine else None,
                                self.bias if self.affine else None, self.eps)

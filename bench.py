@@ -122,14 +122,18 @@ def kernel_table(prof: dict, planes: int, B: int, N: int, H: int, W: int):
 
 
 def load_traffic(workload: str, kernel: str):
-    """HBM bytes per launch of `kernel` from the committed PMC summary, or None."""
+    """(HBM bytes per launch of `kernel`, the PMC run they come from) from the committed
+    rocprofv3 --pmc summary (tools/pmc_summarize.py), or (None, None).  Not measured in this
+    run: PMC passes need their own rocprofv3 runs (MI355X_MICROARCH.md §HBM)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             tab = json.load(f)
-        return tab.get(workload, {}).get(kernel)
+        v = tab.get(workload, {}).get(kernel)
+        return v, (f"profiles/pmc_traffic.json: {tab.get('_source', 'unlabelled PMC run')}"
+                   if v is not None else None)
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
 def make_inputs(cfg, B, seed, device):
@@ -260,52 +264,49 @@ def e2e_bench(N: int, H: int, W: int, D: int, B: int, dev, reps: int = 2):
                 images=f"[{B},{N},3,{H},{W}] ~N(0,1)", depth_finite=ok)
 
 
-def train_bench(dev, planes=(4, 8), reps: int = 2):
-    """Training-step time at config 4's geometry (BASELINE configs[3]: 640x512, N=3, one
-    sample per GPU): the drop-in EMVSNet train forward (FeatNet + the HIP sweep with state
-    snapshots), softmax, mvsnet_cls_loss, and the backward (reverse-plane recompute, DESIGN
-    §6).  Timed at two truncated depth counts; D=192 is projected linearly from them (the
-    sweep and its recompute are uniform per plane)."""
+def train_bench(dev, D: int = 192, reps: int = 2):
+    """Training-step time at config 4 as stated (BASELINE configs[3]: 640x512, N=3, D=192, one
+    sample per GPU; train.py:288-307): the drop-in EMVSNet train forward (FeatNet + the HIP
+    sweep), softmax, mvsnet_cls_loss and the backward through the whole 192-plane recurrence,
+    random-init weights, synthetic images.  Wall time with the device synchronised, `reps`
+    steps after one warm-up step; peak device memory of the step."""
     from models.drmvsnet import EMVSNet, mvsnet_cls_loss
-    B, N, H, W, D_full = 1, 3, 512, 640, 192
+    B, N, H, W = 1, 3, 512, 640
     g = torch.Generator(device="cpu").manual_seed(0)
     imgs = torch.randn(B, N, 3, H, W, generator=g).to(dev)
-    sc = syn.scene(B, N, H, W, D_full, seed=0)
+    sc = syn.scene(B, N, H, W, D, seed=0)
     proj = torch.from_numpy(sc["proj_matrices"]).to(dev)
-    times = {}
-    for D in planes:
-        torch.manual_seed(0)
-        model = EMVSNet(D, image_scale=1.0, max_h=H, max_w=W, evidential=False).to(dev).train()
-        dv = torch.from_numpy(sc["depth_values"][:, :D].copy()).to(dev)
-        depth_gt = dv[:, D // 2].reshape(B, 1, 1).expand(B, H, W).contiguous()
-        mask = torch.ones(B, H, W, device=dev)
+    torch.manual_seed(0)
+    model = EMVSNet(D, image_scale=1.0, max_h=H, max_w=W, evidential=False).to(dev).train()
+    dv = torch.from_numpy(sc["depth_values"]).to(dev)
+    depth_gt = dv[:, D // 2].reshape(B, 1, 1).expand(B, H, W).contiguous()
+    mask = torch.ones(B, H, W, device=dev)
 
-        def step():
-            model.zero_grad(set_to_none=True)
-            prob, _, _ = model(imgs, proj, dv)
-            loss = mvsnet_cls_loss(prob, depth_gt, mask, dv)[0]
-            loss.backward()
-            return loss
+    def step():
+        model.zero_grad(set_to_none=True)
+        prob, _, _ = model(imgs, proj, dv)
+        loss = mvsnet_cls_loss(prob, depth_gt, mask, dv)[0]
+        loss.backward()
+        return loss
 
-        step()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            loss = step()
-        torch.cuda.synchronize()
-        times[D] = (time.perf_counter() - t0) / reps
-        ok = bool(torch.isfinite(loss))
-        del model
-    (d0, t0_), (d1, t1_) = sorted(times.items())
-    per_plane = (t1_ - t0_) / (d1 - d0)
-    fixed = t0_ - d0 * per_plane
+    step()
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    peak = torch.cuda.max_memory_allocated(dev)
+    ok = bool(torch.isfinite(loss)) and all(
+        p.grad is None or bool(torch.isfinite(p.grad).all()) for p in model.parameters())
+    del model
     return dict(metric="training step (forward + mvsnet_cls_loss + backward), 1 sample / GPU",
-                config="dtu_train_640x512_n3_d192", s_per_step_measured={str(k): round(v, 3) for k, v in times.items()},
-                s_per_plane=round(per_plane, 4), s_fixed=round(fixed, 3),
-                projected_s_per_step_d192=round(fixed + D_full * per_plane, 2),
-                note="D truncated to the measured counts; D=192 projected linearly",
-                backward="reverse-plane recompute on the GPU: MIOpen convs, HIP warp scatter, GroupNorm and LSTM gates",
-                loss_finite=ok)
+                config="dtu_train_640x512_n3_d192", D=D, s_per_step=round(dt, 4),
+                ms_per_plane=round(dt / D * 1e3, 3), steps_timed=reps,
+                peak_device_gb=round(peak / 1e9, 2),
+                backward=getattr(EMVSNet, "BACKWARD_PATH", "see DESIGN.md §6"),
+                loss_and_grads_finite=ok)
 
 
 def spawn_ranks(n: int) -> int:
@@ -363,8 +364,10 @@ def main():
                     help="run the sweep's main stream at high priority (aux stream normal)")
     ap.add_argument("--no-fusion", action="store_true",
                     help="skip the depth-map fusion measurement (the next §8 row)")
-    ap.add_argument("--train", action="store_true",
-                    help="also time a config-4 training step (train_bench)")
+    ap.add_argument("--no-train", action="store_true",
+                    help="skip the config-4 training step (train_bench, D=192)")
+    ap.add_argument("--train-planes", type=int, default=192,
+                    help="depth planes of the training step (BASELINE configs[3]: 192)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end EMVSNet.forward figure (FeatNet + sweep)")
     ap.add_argument("--planes", type=int, default=0,
@@ -443,10 +446,11 @@ def main():
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["share"])
         r = kernels[dom]
-        traffic = load_traffic(args.config, dom)
+        traffic, traffic_src = load_traffic(args.config, dom)
         roofline = dict(kernel=dom, bound=r["bound"], achieved=r["achieved"],
                         peak=HBM_PEAK_GBS if r["bound"] == "hbm" else r["peak"],
                         unit=r["unit"], frac=r["frac"], traffic=traffic,
+                        traffic_source=traffic_src,
                         per_launch=r["per_launch"], avg_us=r["avg_us"],
                         timing=f"separate pass, {prof_steps} step(s), one stream, hipEvents per launch")
         # the warp + aggregation path as a whole (every launch that produces the cost
@@ -484,8 +488,8 @@ def main():
         e2e = e2e_bench(N, H, W, D, B, dev)
 
     train = None
-    if rank == 0 and world == 1 and args.train:
-        train = train_bench(dev)
+    if rank == 0 and world == 1 and not args.no_train:
+        train = train_bench(dev, D=args.train_planes)
 
     if rank == 0:
         line = {
@@ -499,7 +503,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32 (cells, deconvs, omega conv: 3x f16-split MFMA, lo*lo dropped; "
+                     "fp32 accumulate)",
             "data": "synthetic (seeded numpy features ~N(0,1), SURVEY 8d cameras, "
                     + ("random-init weights)" if args.random_weights else "model_dtu_v2 weights)"),
             "config": {"workload": args.config, "ref_views_per_gpu": B, "views": N, "H": H, "W": W,

@@ -104,13 +104,16 @@ def homo_warp(src_fea: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor,
     ``fast`` samples with ``F.grid_sample`` itself (the reference's own call,
     module.py:36-37, align_corners=False as torch>=1.3 defaults) instead of the explicit
     gather: the same ATen kernel the reference runs, used by the CPU timing baseline
-    (bench.py) so that it costs what the reference costs.
+    (bench.py) so that it costs what the reference costs.  With ``fast`` a
+    float64 ``src_fea`` is sampled in float64 (on the reference's fp32 grid): the fp64
+    anchor of the gradient tests.
     """
     H, W = src_fea.shape[2:]
     gx, gy = homography_grid(rel, depth, H, W)
     if fast:
         grid = torch.stack((gx, gy), dim=3)
-        return F.grid_sample(src_fea.float(), grid, mode="bilinear", padding_mode="zeros",
+        src = src_fea if src_fea.dtype == torch.float64 else src_fea.float()
+        return F.grid_sample(src, grid.to(src.dtype), mode="bilinear", padding_mode="zeros",
                              align_corners=False)
     return bilinear_zeros(src_fea.float(), gx, gy)
 

@@ -249,6 +249,107 @@ def gen_ckpt(drm, mod, out):
     out.append("real_weights_sweep.npz")
 
 
+def _real_core_weights():
+    """The shipped model_dtu_v2 core, read with weights_only=True."""
+    ck = torch.load(os.path.join(REF, "checkpoints", "model_dtu_v2.ckpt"), map_location="cpu",
+                    weights_only=True)
+    return ck["model"]
+
+
+class _CostRecorder(nn.Module):
+    """Wraps the reference's UNetConvLSTM and keeps every plane's cost_reg (the tensors the
+    reference stacks at drmvsnet.py:320/341); the call itself is passed through unchanged."""
+
+    def __init__(self, inner):
+        super().__init__()
+        self.inner = inner
+        self.costs = []
+
+    def forward(self, x, hidden, d):
+        cost, hidden = self.inner(x, hidden, d)
+        self.costs.append(cost.detach().clone())
+        return cost, hidden
+
+
+def _real_eval_sweep(drm, sd, B, N, H, W, D, seed, head_scale=None):
+    """Eval-mode EMVSNet.forward (drmvsnet.py:300-345) with the real core weights on
+    identity-FeatNet features; returns the scene, the outputs, the recorded cost volume and
+    F.softmax over it (exactly drmvsnet.py:341-342 on the same tensors)."""
+    sc = syn.scene(B, N, H, W, D, seed=seed)
+    model = drm.EMVSNet(disparity_level=D, image_scale=1.0, max_h=H, max_w=W, return_depth=True)
+    sd = dict(sd)
+    if head_scale is not None:
+        sc_w, sc_b = head_scale
+        sd["cost_regularization.conv_0.weight"] = sd["cost_regularization.conv_0.weight"] * sc_w
+        sd["cost_regularization.conv_0.bias"] = sd["cost_regularization.conv_0.bias"] * sc_w + sc_b
+    model.load_state_dict(sd, strict=False)
+    model.feature = nn.Identity()
+    model.evidential = _NoEvidential()
+    rec = _CostRecorder(model.cost_regularization)
+    model.cost_regularization = rec
+    model.eval()
+    imgs = t(np.moveaxis(sc["features"], 0, 1))
+    with torch.no_grad():
+        res = model(imgs, t(sc["proj_matrices"]), t(sc["depth_values"]))
+    cost = torch.stack(rec.costs, dim=1).squeeze(2)
+    prob = torch.softmax(cost, dim=1)
+    return sc, res, cost.numpy(), prob.numpy()
+
+
+# Long-D cases at BASELINE's view counts and depth counts (configs 2, 3, 5), on a small frame
+# so the reference finishes on the CPU; the real model_dtu_v2 core weights.
+LONG_CASES = {"long_n5_d256.npz": (5, 256, 51), "long_n7_d512.npz": (7, 512, 52),
+              "long_n11_d898.npz": (11, 898, 53)}
+LONG_HW = (96, 128)
+
+
+def gen_long(drm, mod, out):
+    """The whole recurrence over BASELINE's depth counts: N=5/D=256, N=7/D=512 and
+    N=11/D=898 (nsrc=10) at 96x128, run by the reference with the real weights.  Stored:
+    depth and confidence (the eval outputs), the per-plane cost subsampled every 8 px (the
+    softmax at those pixels follows from it) and the per-plane mean softmax probability."""
+    sd = _real_core_weights()
+    H, W = LONG_HW
+    for name, (N, D, seed) in LONG_CASES.items():
+        sc, res, cost, prob = _real_eval_sweep(drm, sd, 1, N, H, W, D, seed)
+        np.savez_compressed(os.path.join(HERE, name), depth=res["depth"].numpy(),
+                            conf=res["photometric_confidence"].numpy(),
+                            cost_sub=cost[:, :, ::8, ::8].copy(),
+                            prob_plane_mean=prob.mean(axis=(2, 3)), seed=seed,
+                            shape=np.array([1, N, H, W, D]),
+                            digest=syn.array_digest(sc["features"], sc["proj_matrices"],
+                                                    sc["depth_values"]))
+        out.append(name)
+
+
+# conv_0 (the head, drmvsnet.py:117) scaled so that exp(cost) overflows fp32 on part of the
+# planes and pixels: cost' = OVF_SCALE * cost + OVF_SHIFT.
+OVF_SCALE, OVF_SHIFT = 4.0, 221.0
+
+
+def gen_overflow(drm, mod, out):
+    """The WTA's exp(cost) without max-subtraction (drmvsnet.py:324-339) driven past fp32
+    overflow: where exp(cost) = inf the arithmetic select gives max_prob = inf, then NaN
+    (0 * inf) at the next overflowing plane; exp_sum = inf; conf = NaN or 0.  Stored: depth,
+    conf (NaN kept), per pixel the number of planes whose exp(cost) overflows and the
+    smallest |cost - ln(FLT_MAX)| over the planes (to tell borderline pixels); real weights,
+    N=3, 48x64, D=32."""
+    sd = _real_core_weights()
+    B, N, H, W, D = 1, 3, 48, 64, 32
+    sc, res, cost, prob = _real_eval_sweep(drm, sd, B, N, H, W, D, 61,
+                                           head_scale=(OVF_SCALE, OVF_SHIFT))
+    conf = res["photometric_confidence"].numpy()
+    ovf = np.isinf(np.exp(cost.astype(np.float32)))
+    margin = np.abs(cost.astype(np.float64) - np.log(np.finfo(np.float32).max)).min(axis=1)
+    np.savez_compressed(os.path.join(HERE, "wta_overflow.npz"), depth=res["depth"].numpy(),
+                        conf=conf, n_overflow=ovf.sum(axis=1).astype(np.uint8),
+                        margin=margin.astype(np.float32), seed=61, shape=np.array([B, N, H, W, D]),
+                        head_scale=np.array([OVF_SCALE, OVF_SHIFT], np.float32),
+                        digest=syn.array_digest(sc["features"], sc["proj_matrices"],
+                                                sc["depth_values"]))
+    out.append("wta_overflow.npz")
+
+
 def gen_evidential(drm, mod, out):
     """The evidential head (evidential/models.py:183-459) and loss_der (:517-558), which the
     reference's drivers consume (train.py:297-304, eval.py:151-153): the full EMVSNet
@@ -330,7 +431,7 @@ def gen_datasets(drm, mod, out):
 
 
 GENERATORS = (gen_warp, gen_slice_omega, gen_unet, gen_sweeps, gen_config1, gen_e2e, gen_ckpt,
-              gen_evidential, gen_datasets)
+              gen_evidential, gen_datasets, gen_long, gen_overflow)
 
 
 def main():

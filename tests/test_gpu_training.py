@@ -40,66 +40,70 @@ def _model(D, H, W, wseed):
     return m.to(DEV)
 
 
-def _oracle_grads(feats, proj, dv, P_cpu, R):
-    """CPU autograd of the oracle's fp32 restatement (F.grid_sample warp)."""
+def _oracle_grads(feats, proj, dv, P_cpu, R, dtype=torch.float32):
+    """CPU autograd of the oracle's restatement (F.grid_sample warp) in `dtype`: float32 is the
+    reference's own arithmetic, float64 the anchor both are measured against."""
     from oracle import sweep_oracle as orc
     N, B, C, H, W = feats.shape
-    fc = feats.clone().requires_grad_(True)
+    fc = feats.to(dtype).clone().requires_grad_(True)
+    P = {k: v.detach().to(dtype).clone().requires_grad_(True) for k, v in P_cpu.items()}
     rels = [orc.relative_projection(proj[:, v], proj[:, 0]) for v in range(1, N)]
-    state = orc.init_state(B, H, W)
+    state = [(h.to(dtype), c.to(dtype)) for h, c in orc.init_state(B, H, W)]
     costs = []
     for d in range(dv.shape[1]):
-        x = orc.cost_slice(fc[0], [fc[v] for v in range(1, N)], rels, dv[:, d], P_cpu, fast=True)
-        cost, state = orc.unet_step(x, state, P_cpu)
+        x = orc.cost_slice(fc[0], [fc[v] for v in range(1, N)], rels, dv[:, d], P, fast=True)
+        cost, state = orc.unet_step(x, state, P)
         costs.append(cost)
     prob = torch.softmax(torch.stack(costs, 1).squeeze(2), dim=1)
-    (prob * R).sum().backward()
-    return prob.detach(), fc.grad
+    (prob * R.to(dtype)).sum().backward()
+    return prob.detach(), fc.grad, {k: v.grad for k, v in P.items()}
+
+
+def _rel_err(a, ref):
+    a, ref = np.asarray(a, np.float64).ravel(), np.asarray(ref, np.float64).ravel()
+    return float(np.linalg.norm(a - ref) / max(np.linalg.norm(ref), 1e-300))
 
 
 def test_config4_full_frame_training_backward_matches_cpu_autograd():
-    """640x512, N=3 (configs[3]) over the first 4 of D=192's hypotheses."""
+    """640x512, N=3 (configs[3]) over the first 4 of D=192's hypotheses, every gradient
+    anchored to float64 CPU autograd of the oracle: per tensor, the GPU's relative L2 error
+    against float64 must be at most twice the float32 CPU autograd's (the reference's own
+    arithmetic) error against float64, plus 1e-6 for tensors where float32 is exact to
+    round-off (the split-fp16 products' ~2^-21)."""
     B, N, H, W, D = 1, 3, 512, 640, 4
     sc = syn.scene(B, N, H, W, 192, seed=404)
     dv = torch.from_numpy(sc["depth_values"][:, :D].copy())
     m = _model(D, H, W, 8)
-    P_cpu = {k: v.detach().cpu().clone().requires_grad_(True)
-             for k, v in m.named_parameters() if k in syn.SWEEP_SHAPES}
+    P_cpu = {k: v.detach().cpu().clone() for k, v in m.named_parameters() if k in syn.SWEEP_SHAPES}
     feats = torch.from_numpy(sc["features"])
     proj = torch.from_numpy(sc["proj_matrices"])
     R = torch.randn(B, D, H, W, generator=torch.Generator().manual_seed(3))
-    prob_c, gref = _oracle_grads(feats, proj, dv, P_cpu, R)
+    prob32, gf32, gp32 = _oracle_grads(feats, proj, dv, P_cpu, R, torch.float32)
+    prob64, gf64, gp64 = _oracle_grads(feats, proj, dv, P_cpu, R, torch.float64)
 
     imgs = torch.from_numpy(np.moveaxis(sc["features"], 0, 1).copy()).to(DEV).requires_grad_(True)
     prob, _, _ = m(imgs, proj.to(DEV), dv.to(DEV))
-    np.testing.assert_allclose(prob.detach().cpu().numpy(), prob_c.numpy(), atol=1e-5)
+    np.testing.assert_allclose(prob.detach().cpu().numpy(), prob64.numpy(), atol=1e-5)
     (prob * R.to(DEV)).sum().backward()
-    gi = imgs.grad.cpu().numpy()
-    gref = np.moveaxis(gref.numpy(), 0, 1)
-    # At 327k pixels x 4 planes a few points sit within fp32 noise of a branch (a ReLU in the
-    # omega/GroupNorm chain, a bilinear tap's floor()): GPU and CPU then take different,
-    # equally valid subgradients there.  Everything else must agree at 1e-4 of the scale.
-    gm = np.abs(gref).max()
-    off = np.abs(gi - gref) > 1e-4 * gm
-    assert off.mean() < 1e-4, off.mean()
-    np.testing.assert_allclose(gi, gref, atol=1e-2 * gm)
-    # parameter gradients are sums over 327k pixels x 4 planes of terms that cancel (each
-    # conv here feeds a GroupNorm, whose input gradient is mean-free per group): fp32
-    # summation order (MIOpen on the GPU, oneDNN on the CPU, both run to run
-    # nondeterministic in their reductions) and the tie points above move single entries by
-    # up to ~1% of the tensor's scale.  At this size the check is per tensor: relative L2
-    # error and direction; the entry-wise 1e-4 check is
-    # test_gpu_models.py::test_training_backward_matches_cpu_autograd (16 x 24).
+    report = {}
+    checks = [("features", imgs.grad.cpu().numpy(), np.moveaxis(gf32.numpy(), 0, 1),
+               np.moveaxis(gf64.numpy(), 0, 1))]
     for k, p in m.named_parameters():
-        if k not in P_cpu:
-            continue
-        g, gr = p.grad.cpu().double().numpy().ravel(), P_cpu[k].grad.double().numpy().ravel()
-        if k == "cost_regularization.conv_0.bias":   # true gradient 0 (softmax over D)
-            continue
-        nr = np.linalg.norm(gr)
-        assert np.linalg.norm(g - gr) <= 1e-2 * nr, (k, np.linalg.norm(g - gr) / nr)
-        assert float(g @ gr) >= (1 - 1e-4) * np.linalg.norm(g) * nr, k
-        assert np.abs(g - gr).max() <= 2e-2 * np.abs(gr).max(), k
+        if k in P_cpu and k != "cost_regularization.conv_0.bias":   # true gradient 0 (softmax)
+            checks.append((k, p.grad.cpu().numpy(), gp32[k].numpy(), gp64[k].numpy()))
+    bad = []
+    for k, g_gpu, g32, g64 in checks:
+        e_gpu, e_cpu = _rel_err(g_gpu, g64), _rel_err(g32, g64)
+        report[k] = (e_gpu, e_cpu)
+        if not e_gpu <= 2.0 * e_cpu + 1e-6:
+            bad.append((k, e_gpu, e_cpu))
+    print("\nrelative L2 error vs float64 (gpu, cpu fp32):")
+    for k, (a, b) in report.items():
+        print(f"  {k:48s} {a:.3e} {b:.3e}")
+    assert not bad, bad
+    # the conv_0 bias: its float64 gradient is ~0; the GPU's must be as small as float32's
+    gb = m.cost_regularization.conv_0.bias.grad.abs().max().item()
+    assert gb <= 2.0 * gp32["cost_regularization.conv_0.bias"].abs().max().item() + 1e-6
 
 
 def test_second_backward_through_freed_graph_raises():

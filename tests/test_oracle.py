@@ -148,3 +148,58 @@ def test_fast_sweep_matches_real_weight_fixture():
     assert rel_l1(out["depth"].numpy(), g["depth"]) <= 1e-3
     np.testing.assert_allclose(out["conf"].numpy(), g["conf"], atol=1e-4)
     np.testing.assert_allclose(out["prob"].numpy()[:, :, ::4, ::4], g["prob_sub"], atol=1e-5)
+
+
+def _real_P():
+    g = load("real_weights_sweep.npz")
+    return {k[2:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("w:")}
+
+
+def _long_inputs(g):
+    B, N, H, W, D = (int(x) for x in g["shape"])
+    sc = syn.scene(B, N, H, W, D, seed=int(g["seed"]))
+    assert syn.array_digest(sc["features"], sc["proj_matrices"], sc["depth_values"]) == str(g["digest"])
+    feats = torch.from_numpy(sc["features"])
+    proj = torch.from_numpy(sc["proj_matrices"])
+    return (feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+            [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]))
+
+
+def test_fast_sweep_matches_long_d256_fixture():
+    """The whole recurrence over config 2's N=5, D=256 (long_n5_d256.npz, made by running the
+    reference with the model_dtu_v2 weights at 96x128).  The N=7/D=512 and N=11/D=898
+    fixtures are checked against the HIP sweep in tests/test_gpu_long.py."""
+    g = load("long_n5_d256.npz")
+    out = orc.sweep(*_long_inputs(g), _real_P(), fast=True)
+    assert rel_l1(out["depth"].numpy(), g["depth"]) <= 1e-3
+    np.testing.assert_allclose(out["conf"].numpy(), g["conf"], atol=1e-4)
+    np.testing.assert_allclose(out["cost"].numpy()[:, :, ::8, ::8], g["cost_sub"], atol=1e-4, rtol=1e-5)
+    np.testing.assert_allclose(out["prob"].numpy().mean(axis=(2, 3)), g["prob_plane_mean"], atol=1e-6)
+
+
+def overflow_params():
+    """The real weights with the head conv_0 scaled as in make_golden.gen_overflow."""
+    g = load("wta_overflow.npz")
+    s, b = (float(x) for x in g["head_scale"])
+    P = _real_P()
+    P["cost_regularization.conv_0.weight"] = P["cost_regularization.conv_0.weight"] * s
+    P["cost_regularization.conv_0.bias"] = P["cost_regularization.conv_0.bias"] * s + b
+    return P
+
+
+def test_wta_overflow_semantics_match_reference():
+    """exp(cost) without max-subtraction (drmvsnet.py:324) past fp32 overflow: inf max_prob,
+    then NaN from 0 * inf in the arithmetic select (:328), inf exp_sum -> NaN/0 confidence.
+    The fixture has pixels that never overflow, overflow once and overflow repeatedly."""
+    g = load("wta_overflow.npz")
+    n = g["n_overflow"]
+    assert (n == 0).any() and (n == 1).any() and (n >= 2).any()
+    out = orc.sweep(*_long_inputs(g), overflow_params(), want_volume=False)
+    conf = out["conf"].numpy()
+    ok = g["margin"] > 1e-3          # pixels whose costs all stay clear of ln(FLT_MAX)
+    assert ok.mean() > 0.99
+    np.testing.assert_array_equal(np.isnan(conf)[ok], np.isnan(g["conf"])[ok])
+    assert np.isnan(g["conf"][n >= 1]).all()
+    fin = ok & ~np.isnan(g["conf"])
+    np.testing.assert_allclose(conf[fin], g["conf"][fin], atol=1e-4)
+    assert rel_l1(out["depth"].numpy()[ok], g["depth"][ok]) <= 1e-3

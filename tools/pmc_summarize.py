@@ -54,6 +54,8 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--workload", default="dtu_eval_1600x1184_n7_d512")
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--source", required=True,
+                    help="which PMC run these are (round, command), carried into bench.py's line")
     args = ap.parse_args()
     fetch = load(args.fetch_dir, "FETCH_SIZE")
     write = load(args.write_dir, "WRITE_SIZE")
@@ -70,6 +72,7 @@ def main():
             tab = json.load(f)
     tab[args.workload] = {k: v["hbm_bytes"] for k, v in rows.items()}
     tab.setdefault("_detail", {})[args.workload] = rows
+    tab["_source"] = args.source
     with open(args.out, "w") as f:
         json.dump(tab, f, indent=1, sort_keys=True)
 
