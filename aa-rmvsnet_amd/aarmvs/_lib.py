@@ -16,6 +16,12 @@ LIB_PATH = os.path.join(_HERE, "libaarmvs.so")
 c_int, c_size_t, c_void_p, c_char_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
 
 
+class TrainRecord(ctypes.Structure):
+    """Mirror of ``aarmvs_train_record``."""
+    _fields_ = [("x", c_void_p), ("state", c_void_p), ("z", c_void_p), ("u", c_void_p),
+                ("stats", c_void_p)]
+
+
 class SweepArgs(ctypes.Structure):
     """Mirror of ``aarmvs_sweep_args``."""
     _fields_ = [
@@ -33,6 +39,28 @@ class SweepArgs(ctypes.Structure):
         ("slice_out", c_void_p),
         ("omega_out", c_void_p),
         ("aux_stream", c_void_p),
+        ("record", ctypes.POINTER(TrainRecord)),
+    ]
+
+
+class BackwardArgs(ctypes.Structure):
+    """Mirror of ``aarmvs_backward_args``."""
+    _fields_ = [
+        ("B", c_int), ("C", c_int), ("H", c_int), ("W", c_int), ("nsrc", c_int), ("D", c_int),
+        ("ref_fea", c_void_p),
+        ("src_fea", c_void_p * MAX_SRC),
+        ("rel_proj", c_void_p),
+        ("depth_values", c_void_p),
+        ("packed_params", c_void_p),
+        ("record", ctypes.POINTER(TrainRecord)),
+        ("grad_cost", c_void_p),
+        ("grad_ref", c_void_p),
+        ("grad_src", c_void_p * MAX_SRC),
+        ("grad_params", c_void_p),
+        ("grad_x", c_void_p),
+        ("workspace", c_void_p),
+        ("scratch", c_void_p),
+        ("regulariser_only", c_int),
     ]
 
 
@@ -72,6 +100,9 @@ SIGNATURES = {
                                           c_void_p, c_void_p]),
     "aarmvs_sweep_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "aarmvs_sweep": (c_int, [ctypes.POINTER(SweepArgs), c_void_p]),
+    "aarmvs_train_record_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "aarmvs_backward_scratch_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "aarmvs_sweep_backward": (c_int, [ctypes.POINTER(BackwardArgs), c_void_p]),
     "aarmvs_state_ptr": (c_void_p, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
     "aarmvs_unet_step": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),

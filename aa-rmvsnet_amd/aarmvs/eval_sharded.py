@@ -78,6 +78,8 @@ def save_depth(args, rank: int = 0, world: int = 1, device=None, model=None) -> 
     from models import EMVSNet
     device = torch.device(device or f"cuda:{local_device_index(env()[1])}")
     if device.type == "cuda":
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
         # libaarmvs launches on the current device's stream: make it this rank's GPU
         torch.cuda.set_device(device)
     ds = find_dataset_def(args.dataset)(args.testpath, args.testlist, "test", args.view_num,

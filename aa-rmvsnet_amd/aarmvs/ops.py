@@ -287,7 +287,8 @@ class DepthSweep:
             if n == 0:
                 raise AarmvsError(f"aarmvs: invalid sweep geometry B={B} H={H} W={W} nsrc={nsrc} "
                                   "(H and W must be multiples of 4, 1 <= nsrc <= 16)")
-            self._ws.clear()   # one live geometry at a time keeps HBM use bounded
+            self._ws = {k: v for k, v in self._ws.items() if k[0] == "bwd" and k[1:] == key}
+            # one live geometry at a time keeps HBM use bounded
             ws = torch.empty(n, dtype=torch.uint8, device=self.device)
             self._ws[key] = ws
         return ws
@@ -301,16 +302,39 @@ class DepthSweep:
         rel = torch.stack([relative_projection(sp, ref_proj) for sp in src_projs])  # [nsrc,B,3,4]
         return rel.reshape(len(src_projs), B, 12).to(self.device).contiguous()
 
+    @staticmethod
+    def record_buffers(B: int, H: int, W: int, D: int, device) -> dict:
+        """Device buffers of a training record (aarmvs_train_record) for D planes: the cost
+        slices, D + 1 regulariser state slabs, the gate pre-activations, the deconv outputs and
+        their GroupNorm statistics (~1 KB per pixel and plane at B = 1)."""
+        L = lib()
+        out = {}
+        for i, (name, count) in enumerate((("x", D), ("state", D + 1), ("z", D), ("u", D),
+                                           ("stats", D))):
+            n = L.aarmvs_train_record_bytes(B, H, W, i)
+            if n == 0:
+                raise AarmvsError(f"aarmvs: invalid record geometry B={B} H={H} W={W}")
+            out[name] = torch.empty(n * count, dtype=torch.uint8, device=device)
+        return out
+
+    @staticmethod
+    def _record_struct(rec: dict):
+        r = _lib.TrainRecord()
+        r.x, r.state, r.z, r.u, r.stats = (rec[k].data_ptr() for k in ("x", "state", "z", "u", "stats"))
+        return r
+
     @_on_tensor_device
     def __call__(self, ref_fea, src_feas, ref_proj, src_projs, depth_values, *,
                  want_depth=True, want_cost=False, d_range=None, debug=False, cost_out=None,
-                 rel=None):
+                 rel=None, record=None):
         """Returns dict(depth, conf, cost, slice, omega) (entries None when not requested).
 
         ``d_range=(d0, d1)`` runs planes d0..d1-1 only (d0 == 0 resets the hidden state;
         later ranges continue from the state the previous call left in the workspace).
         ``cost_out`` is an optional caller-owned [B,D,H,W] buffer for the regulariser output.
         ``rel`` is an optional precomputed ``self.relative(ref_proj, src_projs, B)``.
+        ``record`` (``record_buffers(B, H, W, D)``) keeps every plane's tensors for
+        ``backward`` (the training forward).
         """
         ref = ref_fea.contiguous()
         srcs = [s.contiguous() for s in src_feas]
@@ -369,9 +393,73 @@ class DepthSweep:
         a.slice_out = _ptr(out["slice"])
         a.omega_out = _ptr(out["omega"])
         a.aux_stream = self._aux.cuda_stream if self._aux is not None else None
+        rec_struct = None
+        if record is not None:
+            rec_struct = self._record_struct(record)
+            a.record = ctypes.pointer(rec_struct)
         check(lib().aarmvs_sweep(ctypes.byref(a), _stream()), "sweep")
-        out["_keepalive"] = (rel, dv, srcs, ref)
+        out["_keepalive"] = (rel, dv, srcs, ref, rec_struct)
         return out
+
+    @_on_tensor_device
+    def backward(self, ref_fea, src_feas, rel, depth_values, record, grad_cost, *,
+                 regulariser_only=False, want_grad_x=False):
+        """Backward of a recorded training sweep (aarmvs_sweep_backward): from dL/dcost
+        [B,D,H,W] to (grad_ref [B,32,H,W], [grad_src [B,32,H,W]] per view, {sweep parameter
+        name: gradient}, grad_x [D,B,H,W,32] NHWC or None).  ``regulariser_only`` stops after
+        the regulariser (debug: grad_ref/grad_src are None, the omega.* gradients zero)."""
+        ref = ref_fea.contiguous()
+        srcs = [t.contiguous() for t in src_feas]
+        _require_device(ref, *srcs, grad_cost)
+        B, C, H, W = ref.shape
+        nsrc = len(srcs)
+        dv = depth_values.to(ref.device, torch.float32).contiguous()
+        D = dv.shape[1]
+        g = grad_cost.contiguous()
+        if tuple(g.shape) != (B, D, H, W):
+            raise AarmvsError(f"aarmvs: grad_cost must be [B={B},D={D},H={H},W={W}], got {tuple(g.shape)}")
+        ws = self.workspace(B, H, W, nsrc)
+        L = lib()
+        key = ("bwd", B, H, W, nsrc)
+        scratch = self._ws.get(key)
+        if scratch is None:
+            n = L.aarmvs_backward_scratch_bytes(B, H, W, nsrc)
+            if n == 0:
+                raise AarmvsError(f"aarmvs: invalid backward geometry B={B} H={H} W={W} nsrc={nsrc}")
+            scratch = torch.empty(n, dtype=torch.uint8, device=ref.device)
+            self._ws[key] = scratch
+        grad_ref = None if regulariser_only else torch.empty_like(ref)
+        grad_src = None if regulariser_only else [torch.empty_like(t) for t in srcs]
+        grad_params = torch.empty(L.aarmvs_param_count(), device=ref.device)
+        grad_x = torch.empty(D, B, H, W, C, device=ref.device) if want_grad_x else None
+        a = _lib.BackwardArgs()
+        a.B, a.C, a.H, a.W, a.nsrc, a.D = B, C, H, W, nsrc, D
+        a.ref_fea = ref.data_ptr()
+        for i, t in enumerate(srcs):
+            a.src_fea[i] = t.data_ptr()
+            if grad_src is not None:
+                a.grad_src[i] = grad_src[i].data_ptr()
+        a.rel_proj = rel.data_ptr()
+        a.depth_values = dv.data_ptr()
+        a.packed_params = self.packed.data_ptr()
+        rs = self._record_struct(record)
+        a.record = ctypes.pointer(rs)
+        a.grad_cost = g.data_ptr()
+        a.grad_ref = _ptr(grad_ref)
+        a.grad_params = grad_params.data_ptr()
+        a.grad_x = _ptr(grad_x)
+        a.workspace = ws.data_ptr()
+        a.scratch = scratch.data_ptr()
+        a.regulariser_only = 1 if regulariser_only else 0
+        check(L.aarmvs_sweep_backward(ctypes.byref(a), _stream()), "sweep_backward")
+        grads, off = {}, 0
+        for k in SWEEP_KEYS:
+            n = 1
+            for d in SWEEP_SHAPES[k]:
+                n *= d
+            grads[k] = grad_params[off: off + n].view(SWEEP_SHAPES[k])
+            off += n
+        return grad_ref, grad_src, grads, grad_x
 
     def state(self, B, H, W, nsrc, parity, cell, which) -> torch.Tensor:
         """View of a hidden/cell state inside the workspace (after a sweep call)."""
@@ -385,47 +473,6 @@ class DepthSweep:
         # stored NHWC (include/aarmvs.h); returned as the reference's NCHW view
         return ws[off: off + B * hid * (H // sc) * (W // sc) * 4].view(torch.float32).view(
             B, H // sc, W // sc, hid).permute(0, 3, 1, 2)
-
-    def snapshot_state(self, B, H, W, nsrc, parity):
-        """Copies of the regulariser's (h, c) per cell as left for the plane of `parity`."""
-        return [[self.state(B, H, W, nsrc, parity, k, 0).contiguous().clone(),
-                 self.state(B, H, W, nsrc, parity, k, 1).contiguous().clone()] for k in range(5)]
-
-    def _region(self, B, H, W, nsrc):
-        """(byte offset, bytes) of the workspace's contiguous state region (h ping-pong + c of
-        every cell; include/aarmvs.h aarmvs_state_ptr)."""
-        ws = self.workspace(B, H, W, nsrc)
-        L = lib()
-        begin = L.aarmvs_state_ptr(ws.data_ptr(), B, H, W, nsrc, 0, 0, 0)
-        end = L.aarmvs_state_ptr(ws.data_ptr(), B, H, W, nsrc, 0, 4, 1)
-        if not begin or not end:
-            raise AarmvsError("aarmvs: bad state query")
-        end += B * 8 * H * W * 4   # cell 4's c: [B,H,W,8]
-        return begin - ws.data_ptr(), end - begin
-
-    def snapshot_region(self, B, H, W, nsrc) -> torch.Tensor:
-        """One device copy of the whole regulariser state region (raw bytes)."""
-        off, n = self._region(B, H, W, nsrc)
-        return self.workspace(B, H, W, nsrc)[off: off + n].clone()
-
-    def region_states(self, snap: torch.Tensor, B, H, W, nsrc, parity):
-        """(h, c) per cell, NCHW views into a snapshot_region copy, as left for the plane of
-        `parity`."""
-        ws = self.workspace(B, H, W, nsrc)
-        off, _ = self._region(B, H, W, nsrc)
-        L = lib()
-        out = []
-        for k in range(5):
-            hid, sc = (16, 16, 16, 16, 8)[k], (1, 2, 4, 2, 1)[k]
-            n = B * hid * (H // sc) * (W // sc) * 4
-            pair = []
-            for which in (0, 1):
-                p = L.aarmvs_state_ptr(ws.data_ptr(), B, H, W, nsrc, parity, k, which)
-                o = p - ws.data_ptr() - off
-                pair.append(snap[o: o + n].view(torch.float32).view(
-                    B, H // sc, W // sc, hid).permute(0, 3, 1, 2))
-            out.append(pair)
-        return out
 
     @_on_tensor_device
     def cost_slice(self, ref_fea, src_feas, ref_proj, src_projs, depth, want_omega=False):

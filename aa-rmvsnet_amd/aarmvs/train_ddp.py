@@ -73,6 +73,8 @@ def train(args, rank: int = 0, world: int = 1, device=None, log=print) -> dict:
     from models import EMVSNet, mvsnet_cls_loss
     device = torch.device(device or f"cuda:{local_device_index(env()[1])}")
     if device.type == "cuda":
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
         # libaarmvs launches on the current device's stream: make it this rank's GPU
         torch.cuda.set_device(device)
     torch.manual_seed(args.seed)

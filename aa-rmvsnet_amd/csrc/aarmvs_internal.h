@@ -49,6 +49,11 @@ __host__ __device__ constexpr int cell_chunks(int k) { return (cell_cin(k) + 15)
 __host__ __device__ constexpr int cell_a_halves(int k) {   // per hi / lo
   return cell_chunks(k) * 9 * (kCellHid[k] / 8) * 64 * 8;
 }
+// BPTT input-gradient conv of cell k: K = 4 hid gate channels (16-channel chunks), M = cin
+// rows in 32-row m-tiles; halves per m-tile (hi and lo)
+__host__ __device__ constexpr int dg_chunks(int k) { return 4 * kCellHid[k] / 16; }
+__host__ __device__ constexpr int dg_mtiles(int k) { return (cell_cin(k) + 31) / 32; }
+__host__ __device__ constexpr int dg_mt_halves(int k) { return dg_chunks(k) * 9 * 2 * 64 * 8; }
 
 struct ParamLayout {
   size_t raw_off[P_COUNT];
@@ -64,6 +69,10 @@ struct ParamLayout {
   size_t dcm_off[2];        // deconv_0/1 as split-fp16 v_mfma_f32_32x32x16_f16 A fragments
                             // [6 tap pairs][hi, lo][64 lanes][8 halves], then 1 float: 2^-e
                             // (the fragments carry the power-of-two weight scale 2^e)
+  size_t dg_off[5];         // BPTT: each cell's input-gradient conv (the forward conv
+                            // transposed: taps flipped, in/out channels swapped) as split-fp16
+                            // A fragments [m-tile][chunk][tap][hi, lo][64 lanes][8 halves]
+  size_t dg_scale_off;      // 5 floats: 1 / (power-of-two scale) of those fragments
   size_t raw_total;
   size_t pk_total;
 };
@@ -148,11 +157,41 @@ hipError_t launch_omega_group(const CostArgs& a, const SweepGeom& g, const Works
 hipError_t launch_cost_x_group(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d0,
                                int n, float* x0, float* omega_out, int omega_k, hipStream_t s);
 
+// Where one regulariser step reads and writes its tensors (all NHWC): the eval sweep's
+// workspace ping-pong (c updated in place) or a training record's per-plane slabs
+// (unet_io_ws / unet_io_record).
+struct UnetIO {
+  const float* h_prev[5];
+  float* h_new[5];
+  const float* c_prev[5];
+  float* c_new[5];
+  float* z[5];          // gate pre-activations [B][Hk][Wk][4 hid], or null (eval)
+  float* u0;            // deconv_0 output [B][H/2][W/2][16] (pre-GN)
+  float* u1;            // deconv_1 output [B][H][W][16]
+  double* reg_stats;    // the two deconvs' GroupNorm statistics (reg_stat_index layout)
+  bool clear_stats;     // the head kernel zeroes reg_stats after use (eval: one shared set)
+};
+
+// Training record (aarmvs_train_record, include/aarmvs.h): per-plane slabs, in floats
+// (stats in doubles).  A state slab holds h then c of every cell; slab 0 is the zero initial
+// state (drmvsnet.py:133-134), slab d + 1 the state after plane d.
+struct TrainLayout {
+  size_t x_plane;
+  size_t state_slab, h_off[5], c_off[5];
+  size_t z_slab, z_off[5];
+  size_t u_slab, u0_off, u1_off;
+  size_t stats_slab;   // doubles
+  size_t cell_px[5];   // B * pixels of cell k
+};
+TrainLayout train_layout(int B, int H, int W);
+UnetIO unet_io_ws(const Workspace& ws, int parity);
+UnetIO unet_io_record(const TrainLayout& T, const aarmvs_train_record& r, int d);
+
 hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
-                            const Workspace& ws, int parity, hipStream_t s);
-hipError_t launch_head_wta(const float* params, const SweepGeom& g, const Workspace& ws,
-                           int parity, const float* depth_values, int d, float* cost_out,
-                           bool wta, hipStream_t s);
+                            const Workspace& ws, const UnetIO& io, hipStream_t s);
+hipError_t launch_head_wta(const float* params, const SweepGeom& g, const UnetIO& io,
+                           const Workspace& ws, const float* depth_values, int d,
+                           float* cost_out, bool wta, hipStream_t s);
 hipError_t launch_wta_update(const float* cost, const float* depth_d, float* max_prob,
                              float* depth, float* exp_sum, int B, int HW, hipStream_t s);
 hipError_t launch_finalize(const SweepGeom& g, const Workspace& ws, float* depth_out,
@@ -178,6 +217,42 @@ hipError_t launch_group_norm_bwd(const float* dy, const float* x, const float* g
                                  float* s1, float* s2, void* scratch, hipStream_t s);
 
 int cu_count();
+
+// Backward of the regulariser (bptt.hip) over every plane of a training record: the
+// parameter gradients of the cells / deconvs / head into the fp64 accumulators of its scratch
+// (written to grad_params as float at the end, the cost-slice part included if group_done
+// adds to them), and per group of planes dL/dx handed to group_done (planes g0 .. g0 + n - 1,
+// gx [n][B][H][W][32]) and copied to grad_x if set.
+struct BpttRun {
+  int B, H, W, D;
+  const float* packed;
+  const aarmvs_train_record* rec;
+  const float* grad_cost;      // [B][D][H][W]
+  const unsigned* xbound;      // float bits of a bound on |x| (the forward's fp16 guard bound)
+  void* scratch;               // bptt_scratch_bytes
+  float* grad_x;               // optional [D][B][H][W][32]
+  float* grad_params;          // optional [raw count]
+  hipError_t (*group_done)(void* ctx, int g0, int n, const float* gx, hipStream_t s);
+  void* ctx;
+};
+size_t bptt_scratch_bytes(int B, int H, int W);
+hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s);
+// the fp64 parameter-gradient accumulators inside a bptt scratch buffer
+double* bptt_gacc(void* scratch, int B, int H, int W);
+
+// Backward of the cost-slice stage (cost_bwd.hip): per group of planes, from dL/dx to the
+// omega.* parameter gradients (into gacc) and dL/d features (accumulated, written out by
+// cost_bwd_end).
+struct CostBwdCtx {
+  const aarmvs_backward_args* a;
+  Workspace ws;
+  void* scratch;      // cost_bwd_scratch_bytes
+  double* gacc;       // the regulariser's fp64 accumulators (raw layout)
+};
+size_t cost_bwd_scratch_bytes(int B, int H, int W, int nsrc);
+hipError_t cost_bwd_begin(CostBwdCtx& c, hipStream_t s);
+hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t s);
+hipError_t cost_bwd_end(CostBwdCtx& c, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Opt-in per-kernel timing (aarmvs_profile_*): hipEvents recorded on the launch

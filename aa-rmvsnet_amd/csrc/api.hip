@@ -56,6 +56,12 @@ const ParamLayout& param_layout() {
       l.dcm_off[k] = pk;
       pk += 6 * 2 * 64 * 8 / 2 + 64;   // halves -> floats, then the scale (64-float aligned)
     }
+    for (int k = 0; k < 5; ++k) {
+      l.dg_off[k] = pk;
+      pk += ((size_t)dg_mtiles(k) * dg_mt_halves(k) / 2 + 63) / 64 * 64;
+    }
+    l.dg_scale_off = pk;
+    pk += 64;
     l.raw_total = raw;
     l.pk_total = pk;
     return l;
@@ -351,6 +357,44 @@ __global__ void pack_deconv_mfma_kernel(const float* __restrict__ raw, float* __
   if (threadIdx.x == 0) pk[L.dcm_off[k] + 6 * 2 * 64 * 8 / 2] = ldexpf(1.0f, -e);
 }
 
+// BPTT input-gradient conv of each cell: dL/d[input] = conv3x3(dL/dz) with the forward
+// weight W[cz][ci][tap] (cz: gate channel, ci: input channel) transposed and flipped,
+// A[ci][cz, tap] = W[cz][ci][8 - tap].  Fragments [m-tile][chunk][tap][hi, lo][lane][8]: lane l
+// holds row ci = 32 mt + (l & 31), gate channels 16 chunk + 8 (l >> 5) .. +7; rows past cin are
+// zero.  Power-of-two scale per cell as for the forward fragments.  One block per cell.
+__global__ void __launch_bounds__(256) pack_dgrad_kernel(const float* __restrict__ raw,
+                                                         float* __restrict__ pk, ParamLayout L) {
+  __shared__ float red[4];
+  const int k = blockIdx.x;
+  const int hid = kCellHid[k], cin = cell_cin(k), cz = 4 * hid;
+  const float* w = raw + L.raw_off[P_C0W + 2 * k];   // [cz][cin][3][3]
+  const int n = cz * cin * 9;
+  float mx = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) mx = fmaxf(mx, fabsf(w[i]));
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  int e = 0;
+  if (mx > 0.f) {
+    e = (int)floorf(log2f(16384.0f / mx));
+    e = e < -20 ? -20 : (e > 20 ? 20 : e);
+  }
+  const float sc = ldexpf(1.0f, e);
+  if (threadIdx.x == 0) pk[L.dg_scale_off + k] = ldexpf(1.0f, -e);
+  const int nch = dg_chunks(k), mtn = dg_mtiles(k);
+  _Float16* f = reinterpret_cast<_Float16*>(pk + L.dg_off[k]);
+  const int total = mtn * dg_mt_halves(k);
+  for (int i = threadIdx.x; i < total; i += blockDim.x) {
+    const int j = i & 7, l = (i >> 3) & 63, hl = (i >> 9) & 1, rest = i >> 10;
+    const int tap = rest % 9, c = (rest / 9) % nch, mt = rest / (9 * nch);
+    const int ci = 32 * mt + (l & 31), z = 16 * c + 8 * (l >> 5) + j;
+    const float v = ci < cin ? w[(z * cin + ci) * 9 + (8 - tap)] * sc : 0.f;
+    const _Float16 vh = (_Float16)v;
+    f[i] = hl == 0 ? vh : (_Float16)(v - (float)vh);
+  }
+}
+
 hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s) {
   const ParamLayout& L = param_layout();
   hipError_t e = hipMemsetAsync(packed, 0, L.pk_total * sizeof(float), s);
@@ -364,6 +408,8 @@ hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s) {
   hipLaunchKernelGGL(pack_deconv_kernel, dim3(2), dim3(256), 0, s, raw, packed, L);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(pack_deconv_mfma_kernel, dim3(2), dim3(256), 0, s, raw, packed, L);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(pack_dgrad_kernel, dim3(5), dim3(256), 0, s, raw, packed, L);
   return hipGetLastError();
 }
 
@@ -455,6 +501,19 @@ size_t aarmvs_sweep_workspace_bytes(int B, int H, int W, int nsrc) {
   return carve_workspace(nullptr, B, H, W, nsrc).bytes;
 }
 
+size_t aarmvs_train_record_bytes(int B, int H, int W, int which) {
+  if (check_geom(B, H, W, 1) != AARMVS_OK) return 0;
+  const TrainLayout T = train_layout(B, H, W);
+  switch (which) {
+    case 0: return T.x_plane * sizeof(float);
+    case 1: return T.state_slab * sizeof(float);
+    case 2: return T.z_slab * sizeof(float);
+    case 3: return T.u_slab * sizeof(float);
+    case 4: return T.stats_slab * sizeof(double);
+    default: return 0;
+  }
+}
+
 float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int plane_parity,
                         int cell, int which) {
   if (!workspace || cell < 0 || cell > 4 || check_geom(B, H, W, nsrc) != AARMVS_OK) return nullptr;
@@ -484,6 +543,10 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     return fail(AARMVS_ERR_INVALID, "sweep: null pointer argument");
   for (int v = 0; v < a->nsrc; ++v)
     if (!a->src_fea[v]) return fail(AARMVS_ERR_INVALID, "sweep: null src_fea pointer");
+  const aarmvs_train_record* rec = a->record;
+  if (rec && (!rec->x || !rec->state || !rec->z || !rec->u || !rec->stats))
+    return fail(AARMVS_ERR_INVALID, "sweep: training record with a null buffer");
+  const TrainLayout T = train_layout(a->B, a->H, a->W);
 
   SweepGeom g{a->B, a->H, a->W, a->nsrc, a->D, cu_count()};
   Workspace ws = carve_workspace(a->workspace, a->B, a->H, a->W, a->nsrc);
@@ -540,6 +603,8 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
       return sweep_fail(e, "sweep: wta init");
     if ((e = hipMemsetAsync(ws.omega_stats, 0, ws.stats_bytes, stream)) != hipSuccess)
       return sweep_fail(e, "sweep: stats init");
+    if (rec && (e = hipMemsetAsync(rec->state, 0, T.state_slab * sizeof(float), stream)) != hipSuccess)
+      return sweep_fail(e, "sweep: record state init");
     // c8 copies of the features for the cost stage
     const int HW = a->H * a->W;
     // (each copy also folds 8 max|feature|^2 into ws.xbound: cell 0's fp16 range guard)
@@ -550,6 +615,11 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
           hipSuccess)
         return sweep_fail(e, "sweep: c8 copy");
   }
+  // a record's statistics slabs accumulate from zero (gn_reduce fills slot 0 of each)
+  if (rec && (e = hipMemsetAsync(rec->stats + (size_t)a->d_begin * T.stats_slab, 0,
+                                 (size_t)(a->d_end - a->d_begin) * T.stats_slab * sizeof(double),
+                                 stream)) != hipSuccess)
+    return sweep_fail(e, "sweep: record stats init");
   if (aux) {   // fork: the aux stream starts after everything enqueued on `stream` so far
     if ((e = hipEventRecord(ev[4], stream)) != hipSuccess ||
         (e = hipStreamWaitEvent(aux, ev[4], 0)) != hipSuccess)
@@ -563,7 +633,8 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   int gi = 0;
   for (int g0 = a->d_begin; g0 < a->d_end; g0 += G, ++gi) {
     const int n = std::min(G, a->d_end - g0);
-    float* const xs = ws.xg[gi & 1];
+    // the group's cost slices: two alternating workspace slots, or the record's planes
+    float* const xs = rec ? rec->x + (size_t)g0 * T.x_plane : ws.xg[gi & 1];
     // cost stage: its slots were last read by group gi - 2's regulariser steps
     if (aux && gi >= 2 && (e = hipStreamWaitEvent(aux, ev_used[gi & 1], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: event wait");
@@ -580,13 +651,14 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     for (int k = 0; k < n; ++k) {
       const int d = g0 + k;
       const float* xd = xs + (size_t)k * ws.x_plane;
+      const UnetIO io = rec ? unet_io_record(T, *rec, d) : unet_io_ws(ws, d & 1);
       if (d == d_last && a->slice_out) {
         e = launch_layout(xd, a->slice_out, a->B, kC, a->H * a->W, false, stream);
         if (e != hipSuccess) return sweep_fail(e, "sweep: slice copy");
       }
-      if ((e = launch_unet_step(xd, params, g, ws, d & 1, stream)) != hipSuccess)
+      if ((e = launch_unet_step(xd, params, g, ws, io, stream)) != hipSuccess)
         return sweep_fail(e, "sweep: regulariser step");
-      if ((e = launch_head_wta(params, g, ws, d & 1, a->depth_values, d, a->cost_out, wta,
+      if ((e = launch_head_wta(params, g, io, ws, a->depth_values, d, a->cost_out, wta,
                                stream)) != hipSuccess)
         return sweep_fail(e, "sweep: head/wta");
     }
@@ -602,6 +674,67 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     if ((e = launch_finalize(g, ws, a->depth_out, a->conf_out, stream)) != hipSuccess)
       return sweep_fail(e, "sweep: finalize");
   }
+  return AARMVS_OK;
+}
+
+size_t aarmvs_backward_scratch_bytes(int B, int H, int W, int nsrc) {
+  if (check_geom(B, H, W, nsrc) != AARMVS_OK) return 0;
+  return bptt_scratch_bytes(B, H, W) + cost_bwd_scratch_bytes(B, H, W, nsrc);
+}
+
+int aarmvs_sweep_backward(const aarmvs_backward_args* a, hipStream_t stream) {
+  if (!a) return fail(AARMVS_ERR_INVALID, "sweep_backward: null args");
+  int rc = check_geom(a->B, a->H, a->W, a->nsrc);
+  if (rc) return rc;
+  if (a->C != kC) return fail(AARMVS_ERR_INVALID, "sweep_backward: feature channels C must be 32");
+  if (a->D < 1 || !a->ref_fea || !a->rel_proj || !a->depth_values || !a->packed_params ||
+      !a->record || !a->grad_cost || !a->workspace || !a->scratch)
+    return fail(AARMVS_ERR_INVALID, "sweep_backward: null pointer argument or D < 1");
+  const aarmvs_train_record* rec = a->record;
+  if (!rec->x || !rec->state || !rec->z || !rec->u || !rec->stats)
+    return fail(AARMVS_ERR_INVALID, "sweep_backward: training record with a null buffer");
+  for (int v = 0; v < a->nsrc; ++v)
+    if (!a->src_fea[v]) return fail(AARMVS_ERR_INVALID, "sweep_backward: null src_fea pointer");
+  if (!a->regulariser_only && !a->grad_ref)
+    return fail(AARMVS_ERR_INVALID, "sweep_backward: grad_ref is required (the cost-slice part)");
+  Workspace ws = carve_workspace(a->workspace, a->B, a->H, a->W, a->nsrc);
+  hipError_t e;
+  // the c8 feature copies and the fp16 guard bound of the forward, recomputed (the workspace
+  // may have served another sweep since)
+  const int HW = a->H * a->W;
+  if ((e = hipMemsetAsync(ws.xbound, 0, sizeof(unsigned), stream)) != hipSuccess)
+    return hip_fail(e, "sweep_backward: bound init");
+  if ((e = launch_to_c8(a->ref_fea, ws.feat8[0], a->B, HW, stream, ws.xbound)) != hipSuccess)
+    return hip_fail(e, "sweep_backward: c8 copy");
+  for (int v = 0; v < a->nsrc; ++v)
+    if ((e = launch_to_c8(a->src_fea[v], ws.feat8[1 + v], a->B, HW, stream, ws.xbound)) != hipSuccess)
+      return hip_fail(e, "sweep_backward: c8 copy");
+  char* scratch = static_cast<char*>(a->scratch);
+  const size_t breg = bptt_scratch_bytes(a->B, a->H, a->W);
+  CostBwdCtx cctx{};
+  cctx.a = a;
+  cctx.ws = ws;
+  cctx.scratch = scratch + breg;
+  cctx.gacc = bptt_gacc(scratch, a->B, a->H, a->W);
+  if (!a->regulariser_only && (e = cost_bwd_begin(cctx, stream)) != hipSuccess)
+    return hip_fail(e, "sweep_backward: cost-slice init");
+  BpttRun r{};
+  r.B = a->B;
+  r.H = a->H;
+  r.W = a->W;
+  r.D = a->D;
+  r.packed = static_cast<const float*>(a->packed_params);
+  r.rec = rec;
+  r.grad_cost = a->grad_cost;
+  r.xbound = ws.xbound;
+  r.scratch = scratch;
+  r.grad_x = a->grad_x;
+  r.grad_params = a->grad_params;
+  r.group_done = a->regulariser_only ? nullptr : cost_bwd_group;
+  r.ctx = &cctx;
+  if ((e = bptt_regulariser(r, stream)) != hipSuccess) return hip_fail(e, "sweep_backward");
+  if (!a->regulariser_only && (e = cost_bwd_end(cctx, stream)) != hipSuccess)
+    return hip_fail(e, "sweep_backward: cost-slice gradients");
   return AARMVS_OK;
 }
 
@@ -672,10 +805,11 @@ int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
     return hip_fail(e, "unet_step: bound reset");
   if ((e = launch_layout(x, ws.x, B, kC, H * W, true, stream, ws.xbound)) != hipSuccess)
     return hip_fail(e, "unet_step: x layout");
-  if ((e = launch_unet_step(ws.x, params, g, ws, step & 1, stream)) != hipSuccess)
+  const UnetIO io = unet_io_ws(ws, step & 1);
+  if ((e = launch_unet_step(ws.x, params, g, ws, io, stream)) != hipSuccess)
     return hip_fail(e, "unet_step");
   // head conv only (no WTA): cost_out is [B,1,H,W] == [B,D=1,H,W] at plane 0
-  if ((e = launch_head_wta(params, g, ws, step & 1, nullptr, 0, cost_out, false, stream)) !=
+  if ((e = launch_head_wta(params, g, io, ws, nullptr, 0, cost_out, false, stream)) !=
       hipSuccess)
     return hip_fail(e, "unet_step: head");
   return AARMVS_OK;

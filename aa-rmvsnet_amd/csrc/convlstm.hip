@@ -42,7 +42,9 @@ struct CellArgs {
   ChanSrc part[3];
   int nparts;
   float* h_new;
-  float* c;
+  float* c;             // c' out ([B][H][W][HID]); the eval sweep updates c in place (c_in == c)
+  const float* c_in;    // c of the previous plane
+  float* z_out;         // training record: the gate pre-activations (conv + bias) [B][H][W][4 HID], or null
   const float* wpk;     // packed A operands [K/2][MT][64]
   const float* bias;    // [4*hid]
   const unsigned* xbound;   // cell 0: float bits of a bound on |x| (fp16 range guard), or null
@@ -341,7 +343,7 @@ __device__ __forceinline__ void cell_c_load(const CellArgs& a, int b, int yw, in
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (y < a.H && x < a.W)
         v = *reinterpret_cast<const float4*>(
-            a.c + (((size_t)b * a.H + y) * a.W + x) * C::HID + m * 8 + 4 * hi);
+            a.c_in + (((size_t)b * a.H + y) * a.W + x) * C::HID + m * 8 + 4 * hi);
       cst[m][r][0] = v.x;
       cst[m][r][1] = v.y;
       cst[m][r][2] = v.z;
@@ -381,6 +383,19 @@ __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 
         const size_t o = pix * HID + m * 8 + 4 * hi;
         *reinterpret_cast<float4*>(a.c + o) = make_float4(cn[0], cn[1], cn[2], cn[3]);
         *reinterpret_cast<float4*>(a.h_new + o) = make_float4(hn[0], hn[1], hn[2], hn[3]);
+        if (a.z_out) {   // gates i, f, o, g of channels m*8 + 4 hi .. +3 (module.py:83)
+          float* zo = a.z_out + pix * (4 * HID) + m * 8 + 4 * hi;
+#pragma unroll
+          for (int gt = 0; gt < 4; ++gt) {
+            float zz[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int ch = m * 8 + 4 * hi + q;
+              zz[q] = fmaf(acc[m][r][4 * gt + q], inv_scale, a.bias[gt * HID + ch]);
+            }
+            *reinterpret_cast<float4*>(zo + gt * HID) = make_float4(zz[0], zz[1], zz[2], zz[3]);
+          }
+        }
       }
     }
   }
@@ -1086,10 +1101,74 @@ hipError_t launch_layout(const float* in, float* out, int B, int C, int HW, bool
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
-hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
-                            const Workspace& ws, int parity, hipStream_t s) {
-  const ParamLayout& L = param_layout();
+TrainLayout train_layout(int B, int H, int W) {
+  TrainLayout T{};
+  auto al = [](size_t n) { return (n + 63) / 64 * 64; };
+  const size_t HW = (size_t)H * W;
+  const size_t px[5] = {HW, HW / 4, HW / 16, HW / 4, HW};
+  for (int k = 0; k < 5; ++k) T.cell_px[k] = (size_t)B * px[k];
+  T.x_plane = (size_t)B * HW * kC;
+  size_t o = 0;
+  for (int k = 0; k < 5; ++k) {
+    T.h_off[k] = o;
+    o += al(T.cell_px[k] * kCellHid[k]);
+    T.c_off[k] = o;
+    o += al(T.cell_px[k] * kCellHid[k]);
+  }
+  T.state_slab = o;
+  o = 0;
+  for (int k = 0; k < 5; ++k) {
+    T.z_off[k] = o;
+    o += al(T.cell_px[k] * 4 * kCellHid[k]);
+  }
+  T.z_slab = o;
+  T.u0_off = 0;
+  T.u1_off = al((size_t)B * (HW / 4) * 16);
+  T.u_slab = T.u1_off + al((size_t)B * HW * 16);
+  T.stats_slab = (size_t)B * 4 * kSlots * 2;
+  return T;
+}
+
+UnetIO unet_io_ws(const Workspace& ws, int parity) {
   const int cur = parity & 1, nxt = cur ^ 1;
+  UnetIO io{};
+  for (int k = 0; k < 5; ++k) {
+    io.h_prev[k] = ws.h[k][cur];
+    io.h_new[k] = ws.h[k][nxt];
+    io.c_prev[k] = ws.c[k];
+    io.c_new[k] = ws.c[k];
+    io.z[k] = nullptr;
+  }
+  io.u0 = ws.u0;
+  io.u1 = ws.u1;
+  io.reg_stats = ws.reg_stats;
+  io.clear_stats = true;
+  return io;
+}
+
+UnetIO unet_io_record(const TrainLayout& T, const aarmvs_train_record& r, int d) {
+  UnetIO io{};
+  const float* s0 = r.state + (size_t)d * T.state_slab;
+  float* s1 = r.state + (size_t)(d + 1) * T.state_slab;
+  float* z = r.z + (size_t)d * T.z_slab;
+  for (int k = 0; k < 5; ++k) {
+    io.h_prev[k] = s0 + T.h_off[k];
+    io.c_prev[k] = s0 + T.c_off[k];
+    io.h_new[k] = s1 + T.h_off[k];
+    io.c_new[k] = s1 + T.c_off[k];
+    io.z[k] = z + T.z_off[k];
+  }
+  float* u = r.u + (size_t)d * T.u_slab;
+  io.u0 = u + T.u0_off;
+  io.u1 = u + T.u1_off;
+  io.reg_stats = r.stats + (size_t)d * T.stats_slab;
+  io.clear_stats = false;
+  return io;
+}
+
+hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
+                            const Workspace& ws, const UnetIO& io, hipStream_t s) {
+  const ParamLayout& L = param_layout();
   const int H = g.H, W = g.W, B = g.B, cu = g.cu_count;
   hipError_t e;
   auto cell = [&](int k, std::initializer_list<ChanSrc> parts, int scale) {
@@ -1097,8 +1176,10 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     int i = 0;
     for (const ChanSrc& p : parts) a.part[i++] = p;
     a.nparts = i;
-    a.h_new = ws.h[k][nxt];
-    a.c = ws.c[k];
+    a.h_new = io.h_new[k];
+    a.c = io.c_new[k];
+    a.c_in = io.c_prev[k];
+    a.z_out = io.z[k];
     a.wpk = params + L.h3_off[k];   // split-fp16 A fragments
     a.bias = params + L.pk_off[P_C0B + 2 * k];
     a.B = B;
@@ -1106,18 +1187,26 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a.W = W / scale;
     return a;
   };
+  // per-batch-element views of a cell's outputs (cells 3 and 4 are launched per element)
+  auto per_b = [](CellArgs& a, int b, size_t px, int hid) {
+    a.B = 1;
+    a.h_new += b * hid * px;
+    a.c += b * hid * px;
+    a.c_in += b * hid * px;
+    if (a.z_out) a.z_out += b * 4 * hid * px;
+  };
   // cell 0: [x, h0] @ H
   CellArgs a0 = cell(0, {{x, 32, SRC_PLAIN, nullptr, nullptr, nullptr},
-                         {ws.h[0][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
+                         {io.h_prev[0], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
   a0.xbound = ws.xbound;
   if ((e = run_cell_h3<0>(a0, params + L.h3_scale_off + 0, cu, K_CELL0, s)) != hipSuccess) return e;
   // cell 1: [maxpool(h0'), h1] @ H/2
-  CellArgs a1 = cell(1, {{ws.h[0][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},
-                         {ws.h[1][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 2);
+  CellArgs a1 = cell(1, {{io.h_new[0], 16, SRC_POOL, nullptr, nullptr, nullptr},
+                         {io.h_prev[1], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 2);
   if ((e = run_cell_h3<1>(a1, params + L.h3_scale_off + 1, cu, K_CELL1, s)) != hipSuccess) return e;
   // cell 2: [maxpool(h1'), h2] @ H/4
-  CellArgs a2 = cell(2, {{ws.h[1][nxt], 16, SRC_POOL, nullptr, nullptr, nullptr},
-                         {ws.h[2][cur], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
+  CellArgs a2 = cell(2, {{io.h_new[1], 16, SRC_POOL, nullptr, nullptr, nullptr},
+                         {io.h_prev[2], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
   if ((e = run_cell_h3<2>(a2, params + L.h3_scale_off + 2, cu, K_CELL2, s)) != hipSuccess) return e;
   // GroupNorm statistics are per batch element, so the deconvs and the two cells that
   // consume their normalised output are launched per batch element.
@@ -1127,28 +1216,26 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
     {
       ProfScope ps(s, K_DECONV0);
-      hipLaunchKernelGGL(deconv_mfma_kernel<0>, grid, dim3(256), 0, s, ws.h[2][nxt], params + L.dcm_off[0],
-                         params + L.pk_off[P_D0B], Hi, Wi, ws.u0, ws.reg_part);
+      hipLaunchKernelGGL(deconv_mfma_kernel<0>, grid, dim3(256), 0, s, io.h_new[2], params + L.dcm_off[0],
+                         params + L.pk_off[P_D0B], Hi, Wi, io.u0, ws.reg_part);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     ProfScope pr(s, K_GN_REDUCE);
     hipLaunchKernelGGL(gn_reduce_kernel, dim3(B), dim3(256), 0, s, ws.reg_part, (int)(grid.x * grid.y),
-                       ws.reg_stats + reg_stat_index(0, 0, 0),
+                       io.reg_stats + reg_stat_index(0, 0, 0),
                        (int)(reg_stat_index(1, 0, 0) - reg_stat_index(0, 0, 0)));
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // cell 3: [gnrelu(u0), h1', h3] @ H/2
   for (int b = 0; b < B; ++b) {
-    const double* st = ws.reg_stats + reg_stat_index(b, 0, 0);
+    const double* st = io.reg_stats + reg_stat_index(b, 0, 0);
     const size_t hq = (size_t)(H / 2) * (W / 2);
-    CellArgs a3 = cell(3, {{ws.u0 + b * 16 * hq, 16, SRC_GNRELU, st, params + L.pk_off[P_D0GW],
+    CellArgs a3 = cell(3, {{io.u0 + b * 16 * hq, 16, SRC_GNRELU, st, params + L.pk_off[P_D0GW],
                             params + L.pk_off[P_D0GB]},
-                           {ws.h[1][nxt] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr},
-                           {ws.h[3][cur] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr}},
+                           {io.h_new[1] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr},
+                           {io.h_prev[3] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr}},
                        2);
-    a3.B = 1;
-    a3.h_new += b * 16 * hq;
-    a3.c += b * 16 * hq;
+    per_b(a3, b, hq, 16);
     if ((e = run_cell_h3<3>(a3, params + L.h3_scale_off + 3, cu, K_CELL3, s)) != hipSuccess) return e;
   }
   // deconv_1: h3' (H/2) -> u1 (H) + GN stats
@@ -1157,43 +1244,41 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
     {
       ProfScope ps(s, K_DECONV1);
-      hipLaunchKernelGGL(deconv_mfma_kernel<0>, grid, dim3(256), 0, s, ws.h[3][nxt], params + L.dcm_off[1],
-                         params + L.pk_off[P_D1B], Hi, Wi, ws.u1, ws.reg_part);
+      hipLaunchKernelGGL(deconv_mfma_kernel<0>, grid, dim3(256), 0, s, io.h_new[3], params + L.dcm_off[1],
+                         params + L.pk_off[P_D1B], Hi, Wi, io.u1, ws.reg_part);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     ProfScope pr(s, K_GN_REDUCE);
     hipLaunchKernelGGL(gn_reduce_kernel, dim3(B), dim3(256), 0, s, ws.reg_part, (int)(grid.x * grid.y),
-                       ws.reg_stats + reg_stat_index(0, 1, 0),
+                       io.reg_stats + reg_stat_index(0, 1, 0),
                        (int)(reg_stat_index(1, 1, 0) - reg_stat_index(0, 1, 0)));
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // cell 4: [gnrelu(u1), h0', h4] @ H
   for (int b = 0; b < B; ++b) {
-    const double* st = ws.reg_stats + reg_stat_index(b, 1, 0);
+    const double* st = io.reg_stats + reg_stat_index(b, 1, 0);
     const size_t hw = (size_t)H * W;
-    CellArgs a4 = cell(4, {{ws.u1 + b * 16 * hw, 16, SRC_GNRELU, st, params + L.pk_off[P_D1GW],
+    CellArgs a4 = cell(4, {{io.u1 + b * 16 * hw, 16, SRC_GNRELU, st, params + L.pk_off[P_D1GW],
                             params + L.pk_off[P_D1GB]},
-                           {ws.h[0][nxt] + b * 16 * hw, 16, SRC_PLAIN, nullptr, nullptr, nullptr},
-                           {ws.h[4][cur] + b * 8 * hw, 8, SRC_PLAIN, nullptr, nullptr, nullptr}},
+                           {io.h_new[0] + b * 16 * hw, 16, SRC_PLAIN, nullptr, nullptr, nullptr},
+                           {io.h_prev[4] + b * 8 * hw, 8, SRC_PLAIN, nullptr, nullptr, nullptr}},
                        1);
-    a4.B = 1;
-    a4.h_new += b * 8 * hw;
-    a4.c += b * 8 * hw;
+    per_b(a4, b, hw, 8);
     if ((e = run_cell_h3<4>(a4, params + L.h3_scale_off + 4, cu, K_CELL4, s)) != hipSuccess) return e;
   }
   return hipSuccess;
 }
 
-hipError_t launch_head_wta(const float* params, const SweepGeom& g, const Workspace& ws,
-                           int parity, const float* depth_values, int d, float* cost_out,
-                           bool wta, hipStream_t s) {
+hipError_t launch_head_wta(const float* params, const SweepGeom& g, const UnetIO& io,
+                           const Workspace& ws, const float* depth_values, int d,
+                           float* cost_out, bool wta, hipStream_t s) {
   const ParamLayout& L = param_layout();
-  const int nxt = (parity & 1) ^ 1;
   const int blocks = ((g.W + kHeadTW - 1) / kHeadTW) * ((g.H + kHeadTH - 1) / kHeadTH);
   ProfScope ps(s, K_HEAD_WTA);
-  hipLaunchKernelGGL(head_wta_kernel, dim3(blocks, g.B), dim3(256), 0, s, ws.h[4][nxt],
+  hipLaunchKernelGGL(head_wta_kernel, dim3(blocks, g.B), dim3(256), 0, s, io.h_new[4],
                      params + L.pk_off[P_HW], params + L.pk_off[P_HB], g.H, g.W, depth_values, d,
-                     g.D, cost_out, wta ? 1 : 0, ws.max_prob, ws.exp_sum, ws.depth, ws.reg_stats,
+                     g.D, cost_out, wta ? 1 : 0, ws.max_prob, ws.exp_sum, ws.depth,
+                     io.clear_stats ? io.reg_stats : nullptr,
                      (int)(ws.reg_stats_bytes / sizeof(double)));
   return hipGetLastError();
 }

@@ -1151,3 +1151,628 @@ hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t
 }
 
 }  // namespace aarmvs
+
+// ===========================================================================
+// Backward of the cost-slice stage (the BPTT's drmvsnet.py:307-319 part): from dL/dx of a
+// group of planes to the omega.* parameter gradients and dL/d(reference, source features).
+//   x = -(1/nsrc) sum_v (1 + w_v) sq_v,  sq_v = (warp_v - ref)^2,  w_v = omega(sq_v)
+//   dL/dsq_v = -(1 + w_v)/nsrc dL/dx + conv3x3^T(dL/dt1_v);  dL/dw_v = -(1/nsrc) sum_c dL/dx sq_v
+//   omega chain backward (sigmoid, 1x1 conv, ReLU, ResnetBlockGn with three GroupNorm(1,4)
+//   backwards, each needing a grid-wide sum per (plane, sample, view))
+//   dL/dwarp_v = 2 (warp_v - ref) dL/dsq_v;  dL/dref = -sum_v dL/dwarp_v;
+//   dL/dsrc_v = bilinear scatter of dL/dwarp_v (module.py:36: grid_sample's backward).
+// The forward's t1 and GroupNorm statistics are recomputed with launch_omega_group (bit
+// identical); every pixel's warp, sq and omega chain is recomputed with the forward's own
+// arithmetic (same helpers, contraction off), so the ReLU masks are the forward's.
+// Stages per group: cbw_chain<1> (dL/dw from the warp, dL/do; GN3 sums), <2> (GN2 sums),
+// <3> (GN1 sums), <4> (dL/dt1), each with a fixed-order reduce; cbw_feat (dL/dsq, the
+// feature gradients, the conv3x3 weight gradient).  Source gradients are scattered into an
+// LDS box per (tile, view) over the group's planes and flushed with global atomics.
+// ===========================================================================
+
+namespace aarmvs {
+
+// omega chain of one (pixel, view) with its intermediates (omega_weight's operations)
+struct OmegaChain {
+  float t[4], v1[4], aa[4], t2[4], v2[4], bb[4], t3[4], g3[4], s3[4], w;
+};
+__device__ __forceinline__ void omega_chain(const float4 q, const GnStat* gs, const OmegaP& o,
+                                            OmegaChain& c) {
+  c.t[0] = q.x;
+  c.t[1] = q.y;
+  c.t[2] = q.z;
+  c.t[3] = q.w;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float sc = gs[0].rstd * o.g0w[i];
+    const float sh = o.g0b[i] - gs[0].mean * sc;
+    c.v1[i] = c.t[i] * sc + sh;
+    c.aa[i] = fmaxf(c.v1[i], 0.0f);
+  }
+  conv1x1_4(c.aa, o.w1, o.b1, c.t2);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float sc = gs[1].rstd * o.g1w[i];
+    const float sh = o.g1b[i] - gs[1].mean * sc;
+    c.v2[i] = c.t2[i] * sc + sh;
+    c.bb[i] = fmaxf(c.v2[i], 0.0f);
+  }
+  conv1x1_4(c.bb, o.w2, o.b2, c.t3);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float sc = gs[2].rstd * o.g2w[i];
+    const float sh = o.g2b[i] - gs[2].mean * sc;
+    c.g3[i] = c.t3[i] * sc + sh;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    c.s3[i] = c.g3[i] + c.aa[i];
+    s = fmaf(o.wo[i], fmaxf(c.s3[i], 0.0f), s);
+  }
+  c.w = sigmoidf_(s + o.bo);
+}
+
+struct CbwArgs {
+  PipeArgs p;            // forward pipeline arguments (c8 features, rel, depths, params, t1, stats)
+  const float* gx;       // [n][B][HW][32] dL/dx of the group's planes
+  float* go;             // [n][B][nsrc][HW] dL/do (stage 1 out, later in)
+  float4* gt1;           // [n][B][nsrc][HW] dL/dt1 (stage 4 out)
+  const double* gsum;    // [n][B][nsrc][3][2] GroupNorm backward sums (stage 1: GN3, 2: GN2, 3: GN1)
+  double* part;          // [n][B][nsrc][pblk][32] per-block partial sums
+  int d0, pblk;
+};
+
+// columns of each stage's partial rows: 0, 1 = the GroupNorm sums of the stage's statistic;
+// then parameter-gradient sums (cbw_param_cols)
+template <int STAGE>
+__global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* __restrict__ P,
+                                                        const float* __restrict__ Rel) {
+  constexpr int NCOL = STAGE == 1 ? 15 : STAGE == 4 ? 4 : 30;
+  __shared__ float red[NCOL * 4];
+  __shared__ GnStat gs[3];
+  __shared__ float gm[3][2];   // per statistic: mean(g_xhat), mean(g_xhat xhat)
+  const PipeArgs& pa = a.p;
+  const int v = blockIdx.y, bk = blockIdx.z, b = bk % pa.B, k = bk / pa.B;
+  const int H = pa.H, W = pa.W, HW = H * W, nsrc = pa.nsrc;
+  const size_t kbv = ((size_t)k * pa.B + b) * nsrc + v;
+  if (threadIdx.x < 3)
+    gs[threadIdx.x] = stat_read(pa.st_prev + k * pa.st_kstride + st_index(b, v, threadIdx.x, nsrc), 4.0 * HW);
+  if (threadIdx.x >= 32 && threadIdx.x < 38) {
+    const int i = threadIdx.x - 32;   // statistic 2 - (i >> 1)... (GN3 = stat 2, GN2 = 1, GN1 = 0)
+    const int st = i >> 1;
+    gm[st][i & 1] = (float)(a.gsum[kbv * 6 + 2 * st + (i & 1)] / (4.0 * HW));
+  }
+  __syncthreads();
+  OmegaP o;
+  load_omega(pa, P, o);
+  float s[NCOL];
+#pragma unroll
+  for (int i = 0; i < NCOL; ++i) s[i] = 0.f;
+  const float* m = Rel + 12 * (v * pa.B + b);
+  const float dep = pa.dvals[b * pa.D + a.d0 + k];
+  const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);
+  const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(pa.ref + (size_t)b * kC * HW, fbytes);
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(pa.src[v] + (size_t)b * kC * HW, fbytes);
+  const float4* t1p = pa.t1_prev + k * pa.t1_kstride + ((size_t)b * nsrc + v) * HW;
+  float* gop = a.go + kbv * HW;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
+    OmegaChain c;
+    omega_chain(t1p[p], gs, o, c);
+    float g_o;
+    if (STAGE == 1) {
+      // dL/dw = -(1/nsrc) sum_c dL/dx sq (the warp and sq recomputed as cost_x does)
+      const int x = p % W, y = p / W;
+      const TapF tf = tap_f(m, dep, x, y, H, W);
+      const Box none{0, 0, 0, 0};
+      const TapP t = tap_p(tf, true, H, W, false, none, fbytes / 32u);
+      const float* gxp = a.gx + (((size_t)k * pa.B + b) * HW + p) * kC;
+      float dw = 0.f;
+#pragma unroll
+      for (int sl = 0; sl < 8; ++sl) {
+        const float4 g = bil4(ld_c8(rsrc, t.pix[0], sl, HW), ld_c8(rsrc, t.pix[1], sl, HW),
+                              ld_c8(rsrc, t.pix[2], sl, HW), ld_c8(rsrc, t.pix[3], sl, HW), t);
+        const float4 sq = sqdiff4(g, ld_c8(rref, (uint32_t)p, sl, HW));
+        const float4 gg = *reinterpret_cast<const float4*>(gxp + 4 * sl);
+        dw += gg.x * sq.x + gg.y * sq.y + gg.z * sq.z + gg.w * sq.w;
+      }
+      dw = -dw / (float)nsrc;
+      g_o = dw * c.w * (1.0f - c.w);
+      gop[p] = g_o;
+    } else {
+      g_o = gop[p];
+    }
+    float g_r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g_r[i] = c.s3[i] > 0.f ? o.wo[i] * g_o : 0.f;
+    // GN3 (statistic 2): y = g3 = gamma xhat + beta, dL/dy = g_r
+    float xh3[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xh3[i] = (c.t3[i] - gs[2].mean) * gs[2].rstd;
+    if (STAGE == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float gx3 = g_r[i] * o.g2w[i];
+        s[0] += gx3;
+        s[1] += gx3 * xh3[i];
+        s[2 + i] += g_o * fmaxf(c.s3[i], 0.0f);   // Wo
+        s[7 + i] += g_r[i] * xh3[i];               // gamma3
+        s[11 + i] += g_r[i];                       // beta3
+      }
+      s[6] += g_o;                                 // bo
+      continue;
+    }
+    float g_t3[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g_t3[i] = gs[2].rstd * (g_r[i] * o.g2w[i] - gm[2][0] - xh3[i] * gm[2][1]);
+    // t3 = W2 bb + b2
+    float g_n2[4], xh2[4];
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) {
+      float ga = 0.f;
+#pragma unroll
+      for (int co = 0; co < 4; ++co) ga = fmaf(o.w2[co * 4 + ci], g_t3[co], ga);
+      g_n2[ci] = c.v2[ci] > 0.f ? ga : 0.f;
+      xh2[ci] = (c.t2[ci] - gs[1].mean) * gs[1].rstd;
+    }
+    if (STAGE == 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float gx2 = g_n2[i] * o.g1w[i];
+        s[0] += gx2;
+        s[1] += gx2 * xh2[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[2 + i * 4 + j] += g_t3[i] * c.bb[j];   // W2[i][j]
+        s[18 + i] += g_t3[i];                                              // b2
+        s[22 + i] += g_n2[i] * xh2[i];                                     // gamma2
+        s[26 + i] += g_n2[i];                                              // beta2
+      }
+      continue;
+    }
+    float g_t2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g_t2[i] = gs[1].rstd * (g_n2[i] * o.g1w[i] - gm[1][0] - xh2[i] * gm[1][1]);
+    // t2 = W1 aa + b1; aa also feeds the residual (r = relu(g3 + aa))
+    float g_n1[4], xh1[4];
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) {
+      float ga = g_r[ci];
+#pragma unroll
+      for (int co = 0; co < 4; ++co) ga = fmaf(o.w1[co * 4 + ci], g_t2[co], ga);
+      g_n1[ci] = c.v1[ci] > 0.f ? ga : 0.f;
+      xh1[ci] = (c.t[ci] - gs[0].mean) * gs[0].rstd;
+    }
+    if (STAGE == 3) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float gx1 = g_n1[i] * o.g0w[i];
+        s[0] += gx1;
+        s[1] += gx1 * xh1[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[2 + i * 4 + j] += g_t2[i] * c.aa[j];   // W1[i][j]
+        s[18 + i] += g_t2[i];                                              // b1
+        s[22 + i] += g_n1[i] * xh1[i];                                     // gamma1
+        s[26 + i] += g_n1[i];                                              // beta1
+      }
+      continue;
+    }
+    float g_t1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      g_t1[i] = gs[0].rstd * (g_n1[i] * o.g0w[i] - gm[0][0] - xh1[i] * gm[0][1]);
+      s[i] += g_t1[i];   // b0
+    }
+    a.gt1[kbv * HW + p] = make_float4(g_t1[0], g_t1[1], g_t1[2], g_t1[3]);
+  }
+  block_sum<NCOL>(s, red);
+  if (threadIdx.x == 0) {
+    double* pp = a.part + (kbv * a.pblk + blockIdx.x) * 32;
+#pragma unroll
+    for (int i = 0; i < NCOL; ++i) pp[i] = s[i];
+  }
+}
+
+// GroupNorm-backward sums per (plane, b, v): columns 0, 1 of the stage's partial rows
+__global__ void cbw_gsum_kernel(const double* __restrict__ part, int pblk, double* __restrict__ gsum,
+                                int st) {
+  const size_t kbv = blockIdx.x;
+  const int c = threadIdx.x;
+  if (c >= 2) return;
+  double s = 0.0;
+  for (int i = 0; i < pblk; ++i) s += part[(kbv * pblk + i) * 32 + c];
+  gsum[kbv * 6 + 2 * st + c] = s;
+}
+
+// parameter columns -> gacc (fixed order: 8 strided row sets per column, then in order)
+struct CbwCols {
+  int c0, ncol;
+  int off[30];   // gacc index of column c0 + j
+};
+__global__ void __launch_bounds__(256) cbw_param_kernel(const double* __restrict__ part, int nrow,
+                                                        CbwCols cols, double* __restrict__ gacc) {
+  __shared__ double red[256];
+  const int t = threadIdx.x, j = t >> 3, r0 = t & 7;
+  double s = 0.0;
+  if (j < cols.ncol)
+    for (int r = r0; r < nrow; r += 8) s += part[(size_t)r * 32 + cols.c0 + j];
+  red[t] = s;
+  __syncthreads();
+  if (r0 == 0 && j < cols.ncol) {
+    double tot = 0.0;
+    for (int i = 0; i < 8; ++i) tot += red[t + i];
+    gacc[cols.off[j]] += tot;
+  }
+}
+
+// dL/dsq, the feature gradients and the conv3x3 weight gradient.  Block: a 16 x 16 tile of
+// one sample, all views and all planes of the group, one 8-channel chunk at a time; thread =
+// pixel.  dL/dref accumulates in registers over views and planes (one writer per pixel);
+// dL/dsrc goes to an LDS box per (view, chunk) covering the tile's bilinear taps over the
+// group's planes (corner positions bound them: the plane homography and the position along
+// a depth ray are monotone while z > 0), flushed with global atomics; taps outside the box,
+// or views whose box does not fit, use global atomics directly.  The conv3x3 weight gradient
+// gW0[co][c][tap] = sum_q dL/dt1[q - off(tap)][co] sq[q][c]: thread t < 216 owns (channel, tap)
+// pair t % 72 of the chunk and a third of the tile's pixels, summed in order at the end.
+constexpr int kFbT = 16, kFbBoxPx = 768;
+struct CbfArgs {
+  PipeArgs p;
+  const float* gx;          // [n][B][HW][32]
+  const float4* gt1;        // [n][B][nsrc][HW]
+  float* gsrc8;             // [nsrc][B][4][HW][8] dL/dsrc (c8 layout) accumulated
+  float* gref;              // [B][32][HW] dL/dref (NCHW) accumulated
+  float* wpart;             // [blocks][1152] conv3x3 weight-gradient partials [co][c][tap]
+  int d0, n;
+};
+
+__global__ void __launch_bounds__(256) cbw_feat_kernel(CbfArgs a, const float* __restrict__ P,
+                                                       const float* __restrict__ Rel) {
+  extern __shared__ __attribute__((aligned(16))) char lds_fb[];
+  float* w0s = reinterpret_cast<float*>(lds_fb);                          // [4][32][9]
+  float4* gts = reinterpret_cast<float4*>(lds_fb + 4608);                 // [18][18]
+  float* sqs = reinterpret_cast<float*>(lds_fb + 4608 + 5184);            // [256][8]
+  float* box = sqs + 256 * 8;                                             // [kFbBoxPx][8]
+  float* wsum = box + kFbBoxPx * 8;                                       // [4][72][3][4]
+  __shared__ GnStat gs[3];
+  __shared__ int bred[4][4];
+  __shared__ int bad;
+  const PipeArgs& pa = a.p;
+  const int tid = threadIdx.x, b = blockIdx.y;
+  const int H = pa.H, W = pa.W, HW = H * W, nsrc = pa.nsrc;
+  const int tiles_x = (W + kFbT - 1) / kFbT;
+  const int tx0 = (blockIdx.x % tiles_x) * kFbT, ty0 = (blockIdx.x / tiles_x) * kFbT;
+  const int lx = tid & 15, ly = tid >> 4;
+  const int x = tx0 + lx, y = ty0 + ly;
+  const bool in = x < W && y < H;
+  const int p = in ? y * W + x : 0;
+  for (int i = tid; i < 4 * 32 * 9; i += 256) w0s[i] = P[pa.off_ow0 + i];   // raw [co][c][tap]
+  OmegaP o;
+  load_omega(pa, P, o);
+  const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);
+  const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(pa.ref + (size_t)b * kC * HW, fbytes);
+  const int pair = tid % 72, sub = tid / 72;   // weight-gradient role (tid < 216)
+  const int pch = pair / 9, ptap = pair % 9;
+  const int q0 = sub * 86, q1 = min(256, q0 + 86);
+#pragma unroll 1
+  for (int c = 0; c < 4; ++c) {
+    float gref[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float wacc[4] = {0.f, 0.f, 0.f, 0.f};
+    const float4 rf0 = in ? ld_c8(rref, (uint32_t)p, 2 * c, HW) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 rf1 = in ? ld_c8(rref, (uint32_t)p, 2 * c + 1, HW) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+    for (int v = 0; v < nsrc; ++v) {
+      const float* m = Rel + 12 * (v * pa.B + b);
+      const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(pa.src[v] + (size_t)b * kC * HW, fbytes);
+      // this view's source box over the group's planes: tile corners x planes
+      int bx0 = INT_MAX, by0 = INT_MAX, bx1 = -1, by1 = -1;
+      if (tid == 0) bad = 0;
+      __syncthreads();
+      if (tid < 4 * a.n) {
+        const int cx = (tid & 1) ? min(tx0 + kFbT - 1, W - 1) : tx0;
+        const int cy = (tid & 2) ? min(ty0 + kFbT - 1, H - 1) : ty0;
+        const float dep = pa.dvals[b * pa.D + a.d0 + (tid >> 2)];
+        const float zc = (m[8] * (float)cx + m[9] * (float)cy + m[10]) * dep + m[11];
+        const TapF tf = tap_f(m, dep, cx, cy, H, W);
+        if (!(zc > 0.f) || !(tf.xf == tf.xf) || !(tf.yf == tf.yf) || fabsf(tf.xf) > 1e6f ||
+            fabsf(tf.yf) > 1e6f) {
+          bad = 1;
+        } else {
+          bx0 = max(0, (int)tf.xf);
+          by0 = max(0, (int)tf.yf);
+          bx1 = min(W - 1, (int)tf.xf + 1);
+          by1 = min(H - 1, (int)tf.yf + 1);
+        }
+      }
+      const Box bxr = box_reduce<4>(bx0, by0, bx1, by1, bred);
+      const bool use_box = !bad && bxr.nx > 0 && bxr.ny > 0 && bxr.nx * bxr.ny <= kFbBoxPx;
+      if (use_box)
+        for (int i = tid; i < bxr.nx * bxr.ny * 8; i += 256) box[i] = 0.f;
+#pragma unroll 1
+      for (int k = 0; k < a.n; ++k) {
+        __syncthreads();   // box zeroed / previous plane's LDS reads done
+        const size_t kbv = ((size_t)k * pa.B + b) * nsrc + v;
+        for (int i = tid; i < 18 * 18; i += 256) {
+          const int hy = i / 18, hx = i % 18, gy = ty0 - 1 + hy, gxx = tx0 - 1 + hx;
+          gts[i] = (gy >= 0 && gy < H && gxx >= 0 && gxx < W) ? a.gt1[kbv * HW + gy * W + gxx]
+                                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (tid < 3)
+          gs[tid] = stat_read(pa.st_prev + k * pa.st_kstride + st_index(b, v, tid, nsrc), 4.0 * HW);
+        __syncthreads();
+        float sqv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (in) {
+          const float dep = pa.dvals[b * pa.D + a.d0 + k];
+          const TapF tf = tap_f(m, dep, x, y, H, W);
+          const Box none{0, 0, 0, 0};
+          const TapP t = tap_p(tf, true, H, W, false, none, fbytes / 32u);
+          const float4 g0 = bil4(ld_c8(rsrc, t.pix[0], 2 * c, HW), ld_c8(rsrc, t.pix[1], 2 * c, HW),
+                                 ld_c8(rsrc, t.pix[2], 2 * c, HW), ld_c8(rsrc, t.pix[3], 2 * c, HW), t);
+          const float4 g1 = bil4(ld_c8(rsrc, t.pix[0], 2 * c + 1, HW), ld_c8(rsrc, t.pix[1], 2 * c + 1, HW),
+                                 ld_c8(rsrc, t.pix[2], 2 * c + 1, HW), ld_c8(rsrc, t.pix[3], 2 * c + 1, HW), t);
+          const float4 s0 = sqdiff4(g0, rf0), s1 = sqdiff4(g1, rf1);
+          const float wv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+          const float rv[8] = {rf0.x, rf0.y, rf0.z, rf0.w, rf1.x, rf1.y, rf1.z, rf1.w};
+          sqv[0] = s0.x; sqv[1] = s0.y; sqv[2] = s0.z; sqv[3] = s0.w;
+          sqv[4] = s1.x; sqv[5] = s1.y; sqv[6] = s1.z; sqv[7] = s1.w;
+          OmegaChain ch;
+          omega_chain(pa.t1_prev[k * pa.t1_kstride + ((size_t)b * nsrc + v) * HW + p], gs, o, ch);
+          const float* gxp = a.gx + (((size_t)k * pa.B + b) * HW + p) * kC + 8 * c;
+          const float dsc = -(ch.w + 1.0f) / (float)nsrc;
+          float gw[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float gsq = dsc * gxp[j];
+            const int cc = 8 * c + j;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+              const float4 gt = gts[(ly + 2 - tap / 3) * 18 + lx + 2 - tap % 3];
+              gsq = fmaf(w0s[(0 * 32 + cc) * 9 + tap], gt.x, gsq);
+              gsq = fmaf(w0s[(1 * 32 + cc) * 9 + tap], gt.y, gsq);
+              gsq = fmaf(w0s[(2 * 32 + cc) * 9 + tap], gt.z, gsq);
+              gsq = fmaf(w0s[(3 * 32 + cc) * 9 + tap], gt.w, gsq);
+            }
+            gw[j] = 2.0f * (wv[j] - rv[j]) * gsq;
+            gref[j] -= gw[j];
+          }
+          // bilinear scatter of dL/dwarp into the source view (grid_sample backward)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float xf = tf.xf + (float)(q & 1), yf = tf.yf + (float)(q >> 1);
+            const bool ok = (xf > -1.0f) && (xf < (float)W) && (yf > -1.0f) && (yf < (float)H);
+            if (!ok) continue;
+            const int xi = (int)xf, yi = (int)yf;
+            const float wt = tf.wt[q];
+            if (use_box && xi >= bxr.x0 && xi < bxr.x0 + bxr.nx && yi >= bxr.y0 && yi < bxr.y0 + bxr.ny) {
+              float* bp = box + ((yi - bxr.y0) * bxr.nx + (xi - bxr.x0)) * 8;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) atomicAdd(bp + j, wt * gw[j]);
+            } else {
+              float* gp = a.gsrc8 + ((((size_t)v * pa.B + b) * 4 + c) * HW + (size_t)yi * W + xi) * 8;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) atomicAdd(gp + j, wt * gw[j]);
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sqs[tid * 8 + j] = sqv[j];
+        __syncthreads();
+        if (tid < 216) {
+          const int dy = ptap / 3, dx = ptap % 3;
+          for (int qq = q0; qq < q1; ++qq) {
+            const float sv = sqs[qq * 8 + pch];
+            const float4 gt = gts[((qq >> 4) + 2 - dy) * 18 + (qq & 15) + 2 - dx];
+            wacc[0] = fmaf(gt.x, sv, wacc[0]);
+            wacc[1] = fmaf(gt.y, sv, wacc[1]);
+            wacc[2] = fmaf(gt.z, sv, wacc[2]);
+            wacc[3] = fmaf(gt.w, sv, wacc[3]);
+          }
+        }
+      }
+      __syncthreads();
+      if (use_box) {   // flush the box: 8 contiguous channels per source pixel
+        float* gb = a.gsrc8 + (((size_t)v * pa.B + b) * 4 + c) * HW * 8;
+        for (int i = tid; i < bxr.nx * bxr.ny * 8; i += 256) {
+          const int px = i >> 3, j = i & 7, ry = px / bxr.nx, rx = px % bxr.nx;
+          const float val = box[i];
+          if (val != 0.f) atomicAdd(gb + ((size_t)(bxr.y0 + ry) * W + bxr.x0 + rx) * 8 + j, val);
+        }
+      }
+    }
+    if (in) {
+      float* gr = a.gref + (size_t)b * kC * HW + p;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gr[(size_t)(8 * c + j) * HW] += gref[j];
+    }
+    if (tid < 216) {
+#pragma unroll
+      for (int co = 0; co < 4; ++co) wsum[((c * 72 + pair) * 3 + sub) * 4 + co] = wacc[co];
+    }
+  }
+  __syncthreads();
+  float* wp = a.wpart + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 1152;
+  for (int i = tid; i < 1152; i += 256) {   // i = (co * 32 + cc) * 9 + tap
+    const int tap = i % 9, cc = (i / 9) % 32, co = i / 288;
+    const int c = cc >> 3, pr = (cc & 7) * 9 + tap;
+    const float* ws3 = wsum + ((c * 72 + pr) * 3) * 4 + co;
+    wp[i] = (ws3[0] + ws3[4]) + ws3[8];
+  }
+}
+
+__global__ void __launch_bounds__(256) cbw_w0_reduce_kernel(const float* __restrict__ wpart, int nblk,
+                                                            double* __restrict__ gw) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 1152) return;
+  double s = 0.0;
+  for (int k = 0; k < nblk; ++k) s += wpart[(size_t)k * 1152 + i];
+  gw[i] += s;
+}
+
+// c8 [B][4][HW][8] -> NCHW [B][32][HW]
+__global__ void __launch_bounds__(256) c8_to_nchw_kernel(const float* __restrict__ src,
+                                                         float* __restrict__ dst, int HW) {
+  const int b = blockIdx.y;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < 32 * HW; i += gridDim.x * 256) {
+    const int p = i % HW, ch = i / HW;
+    dst[(size_t)b * 32 * HW + i] = src[(((size_t)b * 4 + (ch >> 3)) * HW + p) * 8 + (ch & 7)];
+  }
+}
+
+// ---- host side ----
+struct CostBwdLayout {
+  float* go;
+  float4* gt1;
+  double* gsum;
+  double* part;
+  float* wpart;
+  float* gsrc8;
+  size_t bytes;
+  int pblk, ntiles16;
+};
+
+static CostBwdLayout cost_bwd_layout(void* base, int B, int H, int W, int nsrc) {
+  CostBwdLayout L{};
+  char* p = static_cast<char*>(base);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* r = p ? p + off : nullptr;
+    off = (off + bytes + 255) / 256 * 256;
+    return r;
+  };
+  const size_t HW = (size_t)H * W;
+  const int G = kPlaneGroup;
+  L.pblk = std::max(1, std::min((int)((HW + 1023) / 1024), 8 * cu_count() / std::max(1, B * nsrc) + 1));
+  L.ntiles16 = ((W + kFbT - 1) / kFbT) * ((H + kFbT - 1) / kFbT);
+  L.go = reinterpret_cast<float*>(take((size_t)G * B * nsrc * HW * 4));
+  L.gt1 = reinterpret_cast<float4*>(take((size_t)G * B * nsrc * HW * 16));
+  L.gsum = reinterpret_cast<double*>(take((size_t)G * B * nsrc * 6 * 8));
+  L.part = reinterpret_cast<double*>(take((size_t)G * B * nsrc * L.pblk * 32 * 8));
+  L.wpart = reinterpret_cast<float*>(take((size_t)L.ntiles16 * B * 1152 * 4));
+  L.gsrc8 = reinterpret_cast<float*>(take((size_t)nsrc * B * 32 * HW * 4));
+  L.bytes = off;
+  return L;
+}
+
+size_t cost_bwd_scratch_bytes(int B, int H, int W, int nsrc) {
+  return cost_bwd_layout(nullptr, B, H, W, nsrc).bytes;
+}
+
+static CostArgs cost_args_of(const aarmvs_backward_args* a) {
+  CostArgs ca{};
+  ca.ref = a->ref_fea;
+  for (int v = 0; v < a->nsrc; ++v) ca.src[v] = a->src_fea[v];
+  ca.rel = a->rel_proj;
+  ca.depth_values = a->depth_values;
+  ca.params = static_cast<const float*>(a->packed_params);
+  return ca;
+}
+
+hipError_t cost_bwd_begin(CostBwdCtx& c, hipStream_t s) {
+  const aarmvs_backward_args* a = c.a;
+  CostBwdLayout L = cost_bwd_layout(c.scratch, a->B, a->H, a->W, a->nsrc);
+  hipError_t e;
+  const size_t HW = (size_t)a->H * a->W;
+  if ((e = hipMemsetAsync(L.gsrc8, 0, (size_t)a->nsrc * a->B * 32 * HW * 4, s)) != hipSuccess) return e;
+  if (a->grad_ref && (e = hipMemsetAsync(a->grad_ref, 0, (size_t)a->B * 32 * HW * 4, s)) != hipSuccess)
+    return e;
+  return hipSuccess;
+}
+
+hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t s) {
+  CostBwdCtx& c = *static_cast<CostBwdCtx*>(ctx);
+  const aarmvs_backward_args* a = c.a;
+  const ParamLayout& PL = param_layout();
+  CostBwdLayout L = cost_bwd_layout(c.scratch, a->B, a->H, a->W, a->nsrc);
+  const SweepGeom g{a->B, a->H, a->W, a->nsrc, a->D, cu_count()};
+  const CostArgs ca = cost_args_of(a);
+  hipError_t e;
+  // the forward's omega conv output and GroupNorm statistics of the group's planes
+  if ((e = launch_omega_group(ca, g, c.ws, g0, n, s)) != hipSuccess) return e;
+  CbwArgs ba{};
+  ba.p = pipe_args_c8(ca, g, c.ws);
+  group_strides(ba.p, c.ws, n);
+  ba.p.t1_prev = reinterpret_cast<const float4*>(c.ws.t1);
+  ba.p.st_prev = c.ws.omega_stats;
+  ba.gx = gx;
+  ba.go = L.go;
+  ba.gt1 = L.gt1;
+  ba.gsum = L.gsum;
+  ba.part = L.part;
+  ba.d0 = g0;
+  ba.pblk = L.pblk;
+  const dim3 grid(L.pblk, a->nsrc, a->B * n);
+  const int nkbv = n * a->B * a->nsrc, nrow = nkbv * L.pblk;
+  auto cols = [&](int c0, std::initializer_list<std::pair<int, int>> ranges) {
+    CbwCols cc{};
+    cc.c0 = c0;
+    int j = 0;
+    for (const auto& r : ranges)
+      for (int i = 0; i < r.second; ++i) cc.off[j++] = (int)PL.raw_off[r.first] + i;
+    cc.ncol = j;
+    return cc;
+  };
+  // stage 1: dL/do, GN3 sums; Wo, bo, gamma3, beta3
+  hipLaunchKernelGGL(cbw_chain_kernel<1>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(cbw_gsum_kernel, dim3(nkbv), dim3(64), 0, s, L.part, L.pblk, L.gsum, 2);
+  hipLaunchKernelGGL(cbw_param_kernel, dim3(1), dim3(256), 0, s, L.part, nrow,
+                     cols(2, {{P_OWO, 4}, {P_OBO, 1}, {P_OG2W, 4}, {P_OG2B, 4}}), c.gacc);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // stage 2: GN2 sums; W2, b2, gamma2, beta2
+  hipLaunchKernelGGL(cbw_chain_kernel<2>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(cbw_gsum_kernel, dim3(nkbv), dim3(64), 0, s, L.part, L.pblk, L.gsum, 1);
+  hipLaunchKernelGGL(cbw_param_kernel, dim3(1), dim3(256), 0, s, L.part, nrow,
+                     cols(2, {{P_OW2, 16}, {P_OB2, 4}, {P_OG1W, 4}, {P_OG1B, 4}}), c.gacc);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // stage 3: GN1 sums; W1, b1, gamma1, beta1
+  hipLaunchKernelGGL(cbw_chain_kernel<3>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(cbw_gsum_kernel, dim3(nkbv), dim3(64), 0, s, L.part, L.pblk, L.gsum, 0);
+  hipLaunchKernelGGL(cbw_param_kernel, dim3(1), dim3(256), 0, s, L.part, nrow,
+                     cols(2, {{P_OW1, 16}, {P_OB1, 4}, {P_OG0W, 4}, {P_OG0B, 4}}), c.gacc);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // stage 4: dL/dt1; b0
+  hipLaunchKernelGGL(cbw_chain_kernel<4>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(cbw_param_kernel, dim3(1), dim3(256), 0, s, L.part, nrow, cols(0, {{P_OB0, 4}}),
+                     c.gacc);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // dL/dsq -> features, conv3x3 weights
+  CbfArgs fa{};
+  fa.p = ba.p;
+  fa.gx = gx;
+  fa.gt1 = L.gt1;
+  fa.gsrc8 = L.gsrc8;
+  fa.gref = a->grad_ref;
+  fa.wpart = L.wpart;
+  fa.d0 = g0;
+  fa.n = n;
+  constexpr size_t lds = 4608 + 5184 + 256 * 8 * 4 + kFbBoxPx * 8 * 4 + 4 * 72 * 3 * 4 * 4;
+  static bool attr = false;
+  if (!attr) {
+    if ((e = hipFuncSetAttribute((const void*)cbw_feat_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds)) != hipSuccess)
+      return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(cbw_feat_kernel, dim3(L.ntiles16, a->B), dim3(256), lds, s, fa, ba.p.params, ba.p.rel);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(cbw_w0_reduce_kernel, dim3(5), dim3(256), 0, s, L.wpart, L.ntiles16 * a->B,
+                     c.gacc + PL.raw_off[P_OW0]);
+  return hipGetLastError();
+}
+
+hipError_t cost_bwd_end(CostBwdCtx& c, hipStream_t s) {
+  const aarmvs_backward_args* a = c.a;
+  CostBwdLayout L = cost_bwd_layout(c.scratch, a->B, a->H, a->W, a->nsrc);
+  const int HW = a->H * a->W;
+  for (int v = 0; v < a->nsrc; ++v) {
+    if (!a->grad_src[v]) continue;
+    hipLaunchKernelGGL(c8_to_nchw_kernel, dim3(std::min(4096, (32 * HW + 255) / 256), a->B), dim3(256), 0, s,
+                       L.gsrc8 + (size_t)v * a->B * 32 * HW, a->grad_src[v], HW);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace aarmvs

@@ -17,12 +17,10 @@ What runs where:
 * The D-loop (warp x (N-1), squared difference, omega re-weighting, accumulation,
   ConvLSTM U-Net step, online WTA, softmax over D) runs in libaarmvs.so
   (``aarmvs.ops.DepthSweep``).  There is no CPU fallback: CPU tensors raise.
-* Training (autograd through the sweep): the forward is the HIP sweep, which also
-  snapshots the regulariser's hidden state before every plane (~264 B/px/plane instead
-  of the reference's ~2.3 KB/px/plane of autograd activations).  The backward walks the
-  planes in reverse and recomputes each one with this module's PyTorch blocks on the
-  device (HIP warp + its HIP bilinear-scatter backward), i.e. truncation-free BPTT by
-  per-plane recomputation.
+* Training (autograd through the sweep): the forward is one HIP sweep call that keeps a
+  training record (~1 KB/px/plane instead of the reference's ~2.3 KB/px/plane of autograd
+  activations); the backward (BPTT through every plane, the omega/warp backward and all
+  parameter gradients) is the library's aarmvs_sweep_backward.
 * The evidential head (evidential/models.py) is this package's PyTorch
   restatement ``evidential.models.EvidentialModule``, attached by default with the
   reference's 221 ``evidential.*`` keys (311 keys in all, as the reference: its shipped
@@ -44,7 +42,6 @@ from evidential.models import EvidentialModule, EvidentialShapeError
 from evidential.models import *  # noqa: F401,F403  (the reference: drmvsnet.py:5)
 
 from .module import *  # noqa: F401,F403  (reference re-exports models.module names)
-from .module import _HomoWarp
 from .module import (ConvLSTMCell, convgnrelu, deConvGnReLU, deformconvgnrelu,
                      homo_warping_depthwise, resnet_block_gn)
 
@@ -203,12 +200,15 @@ def _sweep_params(model: "EMVSNet"):
 
 
 class _SweepTrain(torch.autograd.Function):
-    """cost volume [B,D,H,W] of the sweep; backward = reverse-plane recompute (BPTT).
+    """cost volume [B,D,H,W] of the sweep with its backward (BPTT) on the HIP library.
 
-    The forward is one HIP call per plane, snapshotting the regulariser state (one copy of
-    the workspace's state region) before each plane after the first; the snapshots are
-    saved with save_for_backward, so autograd frees them after the backward and a second
-    backward through a freed graph raises autograd's own error, as for any PyTorch op."""
+    The forward is ONE aarmvs_sweep call over all D planes with a training record (the cost
+    slices, every plane's regulariser state, gate pre-activations and deconv outputs: ~1 KB
+    per pixel and plane, instead of the reference's ~2.3 KB of autograd activations); the
+    backward is aarmvs_sweep_backward on that record (the recurrence's reverse sweep, the
+    cost-slice / omega / warp backward and every parameter gradient, drmvsnet.py:273-291
+    differentiated).  The record is saved with save_for_backward, so autograd frees it after
+    the backward and a second backward through a freed graph raises autograd's own error."""
 
     @staticmethod
     def forward(ctx, model, sweep, ref_proj, src_projs, depth_values, ref, *rest):
@@ -217,92 +217,28 @@ class _SweepTrain(torch.autograd.Function):
         B, C, H, W = ref.shape
         D = depth_values.shape[1]
         cost = torch.empty(B, D, H, W, device=ref.device)
-        rel = sweep.relative(ref_proj, src_projs, B)   # once per forward (no per-plane sync)
-        snaps = []
-        for d in range(D):
-            if d > 0:
-                snaps.append(sweep.snapshot_region(B, H, W, nsrc))
-            sweep(ref, srcs, ref_proj, src_projs, depth_values, want_depth=False,
-                  cost_out=cost, d_range=(d, d + 1), rel=rel)
-        ctx.model = model
+        rel = sweep.relative(ref_proj, src_projs, B)
+        rec = sweep.record_buffers(B, H, W, D, ref.device)
+        sweep(ref, srcs, ref_proj, src_projs, depth_values, want_depth=False, cost_out=cost,
+              rel=rel, record=rec)
         ctx.sweep = sweep
-        ctx.geom = (B, H, W, nsrc)
-        ctx.meta = (ref_proj, src_projs, depth_values, nsrc)
-        ctx.rel = rel
-        ctx.save_for_backward(ref, *srcs, *snaps)
+        ctx.nsrc = nsrc
+        ctx.nparams = len(params)
+        ctx.save_for_backward(ref, *srcs, rel, depth_values, rec["x"], rec["state"], rec["z"],
+                              rec["u"], rec["stats"])
         return cost
 
     @staticmethod
-    def _plane(model, params, ref_l, srcs_l, rel, depth_d, hidden, gcost, gstate):
-        """One plane's recompute + vector-Jacobian product: gradients w.r.t. ref, the stacked
-        source views srcs_l [nsrc,B,C,H,W], params and the incoming hidden state (None
-        entries where unused)."""
-        x = model._cost_slice_views(ref_l, srcs_l, rel, depth_d)
-        # UNetConvLSTM.forward replaces the list entries, so pass a shallow copy; idx 0 (plane
-        # 0) starts from _init_hidden's zero states, any other idx from `hidden`
-        cost, new_hidden = model.cost_regularization(
-            x, None if hidden is None else [list(hc) for hc in hidden], 0 if hidden is None else 1)
-        outs, gouts = [cost.squeeze(1)], [gcost]
-        if gstate is not None:
-            for hc, ghc in zip(new_hidden, gstate):
-                outs += list(hc)
-                gouts += list(ghc)
-        flat_hidden = [] if hidden is None else [t for hc in hidden for t in hc]
-        return torch.autograd.grad(outs, [ref_l, srcs_l] + list(params) + flat_hidden, gouts,
-                                   allow_unused=True)
-
-    @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, grad_cost):
-        model = ctx.model
-        ref_proj, src_projs, depth_values, nsrc = ctx.meta
         saved = ctx.saved_tensors
+        nsrc = ctx.nsrc
         ref, srcs = saved[0], list(saved[1:1 + nsrc])
-        B, H, W, _ = ctx.geom
-        snaps = saved[1 + nsrc:]
-        # planes d >= 1 start from the state plane d-1 left, in parity (d & 1)'s h buffers
-        states = [ctx.sweep.region_states(s, B, H, W, nsrc, (i + 1) & 1) for i, s in enumerate(snaps)]
-        params = _sweep_params(model)
-        D = depth_values.shape[1]
-        g_ref = torch.zeros_like(ref)
-        srcs_stack = torch.stack(srcs)   # [nsrc,B,C,H,W]: one warp / omega pass for all views
-        g_srcs = torch.zeros_like(srcs_stack)
-        g_params = [torch.zeros_like(p) for p in params]
-        nparam = len(params)
-
-        def accumulate(grads):
-            if grads[0] is not None:
-                g_ref.add_(grads[0])
-            if grads[1] is not None:
-                g_srcs.add_(grads[1])
-            for i in range(nparam):
-                gp = grads[2 + i]
-                if gp is not None:
-                    g_params[i].add_(gp)
-
-        def state_grads(grads, like):
-            gh = grads[2 + nparam:]
-            return [[gh[2 * k] if gh[2 * k] is not None else torch.zeros_like(like[k][0]),
-                     gh[2 * k + 1] if gh[2 * k + 1] is not None else torch.zeros_like(like[k][1])]
-                    for k in range(len(like))]
-
-        rel = ctx.rel
-        with torch.enable_grad():
-            ref_l = ref.detach().requires_grad_(True)
-            srcs_l = srcs_stack.detach().requires_grad_(True)
-            g_state = None
-            for d in range(D - 1, -1, -1):
-                if d > 0:
-                    hidden = [[t.detach().contiguous().requires_grad_(True) for t in hc]
-                              for hc in states[d - 1]]
-                else:
-                    hidden = None
-                grads = _SweepTrain._plane(model, params, ref_l, srcs_l, rel,
-                                           depth_values[:, d].contiguous(), hidden,
-                                           grad_cost[:, d].contiguous(), g_state)
-                accumulate(grads)
-                if hidden is not None:
-                    g_state = state_grads(grads, hidden)
-        return (None, None, None, None, None, g_ref, *g_srcs.unbind(0), *g_params)
+        rel, dv = saved[1 + nsrc], saved[2 + nsrc]
+        rec = dict(zip(("x", "state", "z", "u", "stats"), saved[3 + nsrc:]))
+        g_ref, g_srcs, g_par, _ = ctx.sweep.backward(ref, srcs, rel, dv, rec, grad_cost)
+        g_params = [g_par[k] for k in _ops.SWEEP_KEYS]
+        return (None, None, None, None, None, g_ref, *g_srcs, *g_params)
 
 
 class _SoftmaxDepth(torch.autograd.Function):
@@ -322,6 +258,11 @@ class _SoftmaxDepth(torch.autograd.Function):
 
 class EMVSNet(nn.Module):
     """drmvsnet.py:234-345 with the depth loop on libaarmvs (gfx950)."""
+
+    BACKWARD_PATH = ("aarmvs_sweep_backward (HIP): one recorded forward sweep, the BPTT "
+                     "(gate / input-gradient / GroupNorm / deconv kernels per plane, weight "
+                     "gradients per 16-plane group) and the cost-slice backward (omega chain, "
+                     "warp gather/scatter) on gfx950")
 
     def __init__(self, disparity_level, image_scale=0.25, max_h=960, max_w=480, return_depth=False,
                  evidential=True):
@@ -350,31 +291,6 @@ class EMVSNet(nn.Module):
             sw = _ops.DepthSweep({k: p.detach() for k, p in zip(_ops.SWEEP_KEYS, params)}, device)
             self._sweep_cache = (key, sw)
         return self._sweep_cache[1]
-
-    def _cost_slice_views(self, ref, srcs, rel, depth):
-        """_cost_slice_torch for the stacked source views srcs [nsrc,B,C,H,W] with the
-        relative projections precomputed on the device (rel [nsrc,B,12],
-        DepthSweep.relative): the views ride the batch axis of one warp and one omega pass
-        (the omega GroupNorms normalise per sample, so this is the per-view arithmetic), and
-        there is no host round trip."""
-        nv, B, C, H, W = srcs.shape
-        warped = _HomoWarp.apply(srcs.reshape(nv * B, C, H, W), rel.reshape(nv * B, 12),
-                                 depth.reshape(-1).repeat(nv))
-        sq = (warped.view(nv, B, C, H, W) - ref).pow(2)
-        term = (self.omega(sq.view(nv * B, C, H, W)).view(nv, B, 1, H, W) + 1) * sq
-        acc = term[0]
-        for v in range(1, nv):   # the reference's view order (drmvsnet.py:309-318)
-            acc = acc + term[v]
-        return -1 * (acc / nv)
-
-    def _cost_slice_torch(self, ref, srcs, ref_proj, src_projs, depth):
-        """-(sum_v (1+w_v)(warp_v - ref)^2)/(N-1), drmvsnet.py:307-319 (training recompute)."""
-        acc = None
-        for src, sp in zip(srcs, src_projs):
-            sq = (homo_warping_depthwise(src, sp, ref_proj, depth) - ref).pow(2)
-            term = (self.omega(sq) + 1) * sq
-            acc = term if acc is None else acc + term
-        return -1 * (acc / len(srcs))
 
     def _check_geometry(self, H, W):
         reg = self.cost_regularization

@@ -84,6 +84,26 @@ int aarmvs_homo_warp_backward(const float* grad_out, const float* rel_proj, cons
  * Replaces, per plane d: homo_warping_depthwise x nsrc, (warp-ref)^2, omega
  * re-weighting, weighted accumulation, UNetConvLSTM.forward and the online WTA.
  * ------------------------------------------------------------------------- */
+/* Training record of a sweep (the BPTT's saved tensors; see aarmvs_sweep_backward):
+ * when aarmvs_sweep_args.record is set, the sweep keeps every plane's regulariser
+ * tensors in these caller-owned device buffers instead of overwriting its workspace copies.
+ * Per-plane slab sizes in bytes: aarmvs_train_record_bytes(B, H, W, which) with which =
+ *   0 x      [B,H,W,32] cost slice of the plane (NHWC);                 D slabs
+ *   1 state  h, c of the five cells (NHWC); slab 0 is the zero initial state
+ *            (drmvsnet.py:133-134), slab d+1 the state after plane d;  D+1 slabs
+ *   2 z      the five cells' gate pre-activations (conv + bias; i,f,o,g); D slabs
+ *   3 u      the two deconvs' outputs before GroupNorm;                  D slabs
+ *   4 stats  the two deconvs' GroupNorm statistics (fp64);               D slabs
+ * ~1 KB per pixel and plane at B = 1 (63 GB for 640x512, D = 192). */
+typedef struct aarmvs_train_record {
+  float* x;
+  float* state;
+  float* z;
+  float* u;
+  double* stats;
+} aarmvs_train_record;
+size_t aarmvs_train_record_bytes(int B, int H, int W, int which);
+
 typedef struct aarmvs_sweep_args {
   int B, C, H, W;                         /* C must be 32                         */
   int nsrc;                               /* N-1 source views                     */
@@ -107,10 +127,49 @@ typedef struct aarmvs_sweep_args {
                                              group's regulariser steps (events per group; at
                                              return all work is ordered on `stream`; results
                                              are bit-identical either way)             */
+  const aarmvs_train_record* record;      /* training record, or NULL (eval): the cost
+                                             slices and regulariser tensors of the planes
+                                             d_begin..d_end-1 go to its slabs           */
 } aarmvs_sweep_args;
 
 size_t aarmvs_sweep_workspace_bytes(int B, int H, int W, int nsrc);
 int aarmvs_sweep(const aarmvs_sweep_args* args, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Backward of a training sweep (the BPTT through drmvsnet.py:273-291): given the record
+ * of a forward over all D planes (aarmvs_sweep with `record`, d_begin = 0, d_end = D) and
+ * dL/dcost [B,D,H,W] (the sweep's cost volume, before the softmax), the gradients w.r.t.
+ * the sweep's parameters (raw-blob layout, aarmvs_param_count() floats: the omega.* and
+ * cost_regularization.* tensors), the reference features and the source features.
+ * Replaces autograd through homo_warping_depthwise, the omega network, the weighted
+ * accumulation and UNetConvLSTM.forward (module.py:6-38, 76-92, 252-287; drmvsnet.py:27-38,
+ * 119-167); no gradient flows to the projections or depths (module.py:15).
+ * Planes are processed last to first in groups of 16.  Parameter gradients are fixed-order
+ * fp64 sums (deterministic); grad_ref / grad_src are overwritten (NCHW [B,32,H,W]).
+ * grad_x (debug, or NULL): [D][B][H][W][32] dL/dx per plane (the cost slices, NHWC).
+ * regulariser_only (debug): skip the cost-slice part (grad_ref / grad_src untouched, the
+ * omega.* entries of grad_params zero).  `workspace` is the sweep workspace
+ * (aarmvs_sweep_workspace_bytes), `scratch` aarmvs_backward_scratch_bytes bytes.
+ * ------------------------------------------------------------------------- */
+typedef struct aarmvs_backward_args {
+  int B, C, H, W, nsrc, D;
+  const float* ref_fea;                   /* [B,C,H,W]                          */
+  const float* src_fea[AARMVS_MAX_SRC];   /* nsrc x [B,C,H,W]                   */
+  const float* rel_proj;                  /* [nsrc][B][12]                      */
+  const float* depth_values;              /* [B,D]                              */
+  const void* packed_params;
+  const aarmvs_train_record* record;
+  const float* grad_cost;                 /* [B,D,H,W]                          */
+  float* grad_ref;                        /* [B,C,H,W] out, or NULL             */
+  float* grad_src[AARMVS_MAX_SRC];        /* nsrc x [B,C,H,W] out, or NULL      */
+  float* grad_params;                     /* [aarmvs_param_count()] out, or NULL */
+  float* grad_x;                          /* debug out, or NULL                 */
+  void* workspace;
+  void* scratch;
+  int regulariser_only;
+} aarmvs_backward_args;
+size_t aarmvs_backward_scratch_bytes(int B, int H, int W, int nsrc);
+int aarmvs_sweep_backward(const aarmvs_backward_args* args, hipStream_t stream);
 
 /* Hidden state of the regulariser inside the workspace, for inspection/BPTT:
  * cell k in 0..4, which = 0 for h, 1 for c.  Valid after an aarmvs_sweep call;

@@ -1,0 +1,170 @@
+"""GPU tests of the training record and of aarmvs_sweep_backward (the BPTT on HIP, SURVEY
+§8f-1) against float64 CPU autograd of the oracle.
+
+* The recorded forward (one aarmvs_sweep call with an aarmvs_train_record) produces the eval
+  sweep's cost volume bit for bit, and its slabs hold the regulariser's tensors: the last
+  state slab equals the sweep's final state, the gate pre-activations equal the cell conv
+  recomputed in float64 from the recorded inputs.
+* The regulariser part alone (regulariser_only: dL/dx per plane and the cost_regularization.*
+  gradients) and the whole backward (dL/d features, every sweep parameter) match float64
+  autograd of the oracle through the same planes, per tensor in relative L2.
+
+Tolerances: the forward's cells and the backward's input-gradient convs run three-product
+split-fp16 MFMA (~2^-21 per product); per-tensor relative L2 <= 2e-5 against
+float64 (fp32 CPU autograd itself sits at ~1e-6 .. 1e-5 here).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from aarmvs import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+
+def rel_l2(a, ref):
+    a = np.asarray(a, np.float64).ravel()
+    ref = np.asarray(ref, np.float64).ravel()
+    return float(np.linalg.norm(a - ref) / max(np.linalg.norm(ref), 1e-300))
+
+
+def _setup(B, N, H, W, D, seed, wseed):
+    from aarmvs import ops
+    sc = syn.scene(B, N, H, W, D, seed=seed)
+    P = {k: torch.from_numpy(v) for k, v in syn.sweep_weights(wseed).items()}
+    feats = torch.from_numpy(sc["features"])
+    proj = torch.from_numpy(sc["proj_matrices"])
+    dv = torch.from_numpy(sc["depth_values"])
+    sw = ops.DepthSweep({k: v.to(DEV) for k, v in P.items()}, DEV)
+    fd = feats.to(DEV)
+    args = (fd[0], [fd[v] for v in range(1, N)], proj[:, 0], [proj[:, v] for v in range(1, N)], dv)
+    return sc, P, feats, proj, dv, sw, args
+
+
+def _record_forward(sw, args, B, H, W, D):
+    ref, srcs, ref_proj, src_projs, dv = args
+    rec = sw.record_buffers(B, H, W, D, DEV)
+    rel = sw.relative(ref_proj, src_projs, B)
+    cost = torch.empty(B, D, H, W, device=DEV)
+    sw(ref, srcs, ref_proj, src_projs, dv, want_depth=False, cost_out=cost, rel=rel, record=rec)
+    return cost, rec, rel
+
+
+def test_recorded_forward_matches_eval_sweep_and_holds_the_tensors():
+    from aarmvs import _lib
+    B, N, H, W, D = 1, 3, 32, 48, 5
+    sc, P, feats, proj, dv, sw, args = _setup(B, N, H, W, D, 3, 4)
+    ev = sw(*args, want_cost=True)
+    cost, rec, _ = _record_forward(sw, args, B, H, W, D)
+    torch.cuda.synchronize()
+    assert torch.equal(cost, ev["cost"])
+    # the last state slab = the eval sweep's final state (NHWC views)
+    L = _lib.lib()
+    slab = L.aarmvs_train_record_bytes(B, H, W, 1) // 4
+    st = rec["state"].view(torch.float32)[D * slab:(D + 1) * slab]
+    off = 0
+    for k, (hid, s) in enumerate(zip((16, 16, 16, 16, 8), (1, 2, 4, 2, 1))):
+        n = B * (H // s) * (W // s) * hid
+        for which in (0, 1):
+            got = st[off: off + n].view(B, H // s, W // s, hid).permute(0, 3, 1, 2)
+            want = sw.state(B, H, W, N - 1, D & 1, k, which)
+            assert torch.equal(got, want), (k, which)
+            off += -(-n // 64) * 64
+    # cell 0's gate pre-activations of plane 2 = conv3x3([x_2, h0 of plane 1]) in float64
+    d = 2
+    xs = rec["x"].view(torch.float32)[d * B * H * W * 32:(d + 1) * B * H * W * 32].view(B, H, W, 32)
+    st_d = rec["state"].view(torch.float32)[d * slab:(d + 1) * slab]
+    h0 = st_d[: B * H * W * 16].view(B, H, W, 16)
+    zsl = L.aarmvs_train_record_bytes(B, H, W, 2) // 4
+    z0 = rec["z"].view(torch.float32)[d * zsl: d * zsl + B * H * W * 64].view(B, H, W, 64)
+    inp = torch.cat([xs, h0], -1).permute(0, 3, 1, 2).double().cpu()
+    w = P["cost_regularization.cell_list.0.conv.weight"].double()
+    bb = P["cost_regularization.cell_list.0.conv.bias"].double()
+    zref = torch.nn.functional.conv2d(inp, w, bb, padding=1).permute(0, 2, 3, 1).numpy()
+    np.testing.assert_allclose(z0.cpu().numpy(), zref, atol=2e-5 * np.abs(zref).max(), rtol=0)
+
+
+def _oracle_grads(feats, proj, dv, P, R, dtype):
+    """float64/float32 autograd of the oracle's sweep (the reference's arithmetic) ->
+    (prob, d/dfeatures, {param: grad}, [dL/dx_d])."""
+    from oracle import sweep_oracle as orc
+    N, B, C, H, W = feats.shape
+    fc = feats.to(dtype).clone().requires_grad_(True)
+    Pp = {k: v.detach().to(dtype).clone().requires_grad_(True) for k, v in P.items()}
+    rels = [orc.relative_projection(proj[:, v], proj[:, 0]) for v in range(1, N)]
+    state = [(h.to(dtype), c.to(dtype)) for h, c in orc.init_state(B, H, W)]
+    costs, xs = [], []
+    for d in range(dv.shape[1]):
+        x = orc.cost_slice(fc[0], [fc[v] for v in range(1, N)], rels, dv[:, d], Pp, fast=True)
+        x.retain_grad()
+        xs.append(x)
+        cost, state = orc.unet_step(x, state, Pp)
+        costs.append(cost)
+    prob = torch.softmax(torch.stack(costs, 1).squeeze(2), dim=1)
+    (prob * R.to(dtype)).sum().backward()
+    return prob.detach(), fc.grad, {k: v.grad for k, v in Pp.items()}, [x.grad for x in xs]
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 32, 48, 6), (2, 4, 24, 40, 5), (1, 3, 16, 24, 18)])
+def test_backward_matches_float64_autograd(shape):
+    """Whole backward (regulariser + cost slice) vs float64 CPU autograd; shape 3 spans two
+    16-plane groups (the group boundary of the weight gradients and the cost-slice pass)."""
+    B, N, H, W, D = shape
+    sc, P, feats, proj, dv, sw, args = _setup(B, N, H, W, D, 11 + D, 6)
+    cost, rec, rel = _record_forward(sw, args, B, H, W, D)
+    R = torch.randn(B, D, H, W, generator=torch.Generator().manual_seed(5))
+    prob64, gf64, gp64, gx64 = _oracle_grads(feats, proj, dv, P, R, torch.float64)
+    prob = torch.softmax(cost, dim=1)
+    np.testing.assert_allclose(prob.cpu().numpy(), prob64.numpy(), atol=1e-5)
+    # dL/dcost of sum(R * softmax(cost))
+    Rd = R.to(DEV)
+    gcost = prob * (Rd - (Rd * prob).sum(dim=1, keepdim=True))
+    ref, srcs = args[0], args[1]
+    # regulariser only: dL/dx per plane and the cost_regularization.* gradients
+    _, _, gp_r, gx = sw.backward(ref, srcs, rel, dv, rec, gcost, regulariser_only=True, want_grad_x=True)
+    gx = gx.permute(0, 1, 4, 2, 3).cpu().numpy()   # [D,B,32,H,W]
+    errs = {"x": rel_l2(gx, np.stack([g.numpy() for g in gx64]))}
+    for k, g in gp_r.items():
+        if k.startswith("cost_regularization.") and k != "cost_regularization.conv_0.bias":
+            errs[k] = rel_l2(g.cpu().numpy(), gp64[k].numpy())
+        elif k.startswith("omega."):
+            assert float(g.abs().max()) == 0.0, k
+    # everything
+    g_ref, g_src, gp, _ = sw.backward(ref, srcs, rel, dv, rec, gcost)
+    gfeat = torch.stack([g_ref] + g_src).cpu().numpy()
+    errs["features"] = rel_l2(gfeat, gf64.numpy())
+    for k, g in gp.items():
+        if k != "cost_regularization.conv_0.bias":   # true gradient 0 (softmax over D)
+            errs["all:" + k] = rel_l2(g.cpu().numpy(), gp64[k].numpy())
+    print("\nrelative L2 vs float64:")
+    for k, e in errs.items():
+        print(f"  {k:52s} {e:.3e}")
+    bad = {k: e for k, e in errs.items() if not e <= 2e-5}
+    assert not bad, bad
+    assert abs(float(gp["cost_regularization.conv_0.bias"])) <= 1e-5 * float(gcost.abs().sum())
+
+
+def test_backward_is_deterministic_in_the_parameter_gradients():
+    """Parameter gradients are fixed-order fp64 sums: two backward calls agree bit for bit
+    (the feature gradients use fp32 atomics in the source scatter: equal to rounding)."""
+    B, N, H, W, D = 1, 3, 32, 48, 4
+    sc, P, feats, proj, dv, sw, args = _setup(B, N, H, W, D, 9, 2)
+    cost, rec, rel = _record_forward(sw, args, B, H, W, D)
+    g = torch.randn_like(cost)
+    a = sw.backward(args[0], args[1], rel, dv, rec, g)
+    b = sw.backward(args[0], args[1], rel, dv, rec, g)
+    for k in a[2]:
+        assert torch.equal(a[2][k], b[2][k]), k
+    assert torch.equal(a[0], b[0])
+    for x, y in zip(a[1], b[1]):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6 * float(x.abs().max()))

@@ -69,3 +69,38 @@ def test_sharded_eval_writes_every_sample_once(tmp_path, numdepth):
             np.testing.assert_array_equal(saved, out["depth"][0].cpu().numpy())
         conf = fusion.read_pfm(str(root / "out" / s["filename"].format("confidence_0", ".pfm")))[0]
         np.testing.assert_array_equal(conf, out["photometric_confidence"][0].cpu().numpy())
+
+
+def test_sharded_eval_two_rank_processes_share_one_gpu(tmp_path):
+    """``python -m aarmvs.eval_sharded`` as two rank processes (LOCAL_RANK 0 and 1) on the one
+    GPU (AARMVS_SHARED_GPU=1: rank 1 maps to cuda:0 through local_device_index, as in
+    train_ddp and bench.py): each writes its shard, together every sample once."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    root = _tree(tmp_path)
+    cmd = [sys.executable, "-m", "aarmvs.eval_sharded", "--testpath", str(root), "--testlist",
+           str(root / "list.txt"), "--outdir", str(root / "out"), "--max_h", "32", "--max_w", "48",
+           "--numdepth", "16", "--view_num", "3", "--interval_scale", "1.06"]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", AARMVS_SHARED_GPU="1",
+                   PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "aa-rmvsnet_amd"), ROOT,
+                                               os.environ.get("PYTHONPATH", "")]))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=150)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+        assert p.returncode == 0, out[-3000:]
+    assert "rank 0/2: 2 reference views written" in outs[0], outs[0][-2000:]
+    assert "rank 1/2: 2 reference views written" in outs[1], outs[1][-2000:]
+    pfms = sorted(p.name for p in (root / "out").rglob("*.pfm") if "depth_est_0" in str(p))
+    assert len(pfms) == 4

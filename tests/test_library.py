@@ -42,3 +42,30 @@ def test_host_only_queries():
     assert L.aarmvs_sweep_workspace_bytes(1, 128, 160, 2) > 0
     assert L.aarmvs_sweep_workspace_bytes(1, 130, 160, 2) == 0   # H % 4 != 0 rejected
     assert b"multiple" in L.aarmvs_last_error()
+
+
+def test_library_calls_run_under_their_tensors_device(monkeypatch):
+    """aarmvs.ops enters the device of its first device tensor (or DepthSweep) around every
+    library call, so the launch stream and the library's hipGetDevice() are that device's,
+    whatever device the caller left current (train/eval ranks on cuda:r)."""
+    import contextlib
+    import torch
+    from aarmvs import ops
+    entered = []
+
+    @contextlib.contextmanager
+    def fake_device(dev):
+        entered.append(dev)
+        yield
+
+    monkeypatch.setattr(torch.cuda, "device", fake_device)
+    sw = ops.DepthSweep.__new__(ops.DepthSweep)
+    sw.device = torch.device("cuda", 3)
+
+    @ops._on_tensor_device
+    def f(obj, x=None):
+        return "ran"
+
+    assert f(sw) == "ran" and entered == [torch.device("cuda", 3)]
+    assert f(torch.zeros(1)) == "ran" and len(entered) == 1          # CPU tensors: no guard
+    assert f(None, x=torch.device("cuda", 1)) == "ran" and entered[-1] == torch.device("cuda", 1)

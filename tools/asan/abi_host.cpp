@@ -93,6 +93,34 @@ int main() {
   CHECK(aarmvs_sweep(&a, nullptr) == AARMVS_ERR_INVALID);   // empty plane range
   a.d_begin = 0, a.nsrc = 2;
   CHECK(aarmvs_sweep(&a, nullptr) == AARMVS_ERR_INVALID);   // src_fea[1] null
+  // training record: sizes grow with the frame; a record with a null buffer is rejected
+  CHECK(aarmvs_train_record_bytes(1, 8, 8, 1) > 0 && aarmvs_train_record_bytes(1, 8, 8, 5) == 0);
+  CHECK(aarmvs_train_record_bytes(1, 8, 8, 2) < aarmvs_train_record_bytes(1, 16, 8, 2));
+  CHECK(aarmvs_train_record_bytes(1, 6, 8, 0) == 0 && has_error());
+  aarmvs_train_record rec;
+  std::memset(&rec, 0, sizeof(rec));
+  a.nsrc = 1, a.record = &rec;
+  CHECK(aarmvs_sweep(&a, nullptr) == AARMVS_ERR_INVALID && has_error());   // null record buffers
+  a.record = nullptr;
+  // backward: argument rejection before any launch
+  CHECK(aarmvs_backward_scratch_bytes(1, 64, 80, 2) > 0 && aarmvs_backward_scratch_bytes(1, 6, 8, 1) == 0);
+  CHECK(aarmvs_sweep_backward(nullptr, nullptr) == AARMVS_ERR_INVALID);
+  aarmvs_backward_args ba;
+  std::memset(&ba, 0, sizeof(ba));
+  ba.B = 1, ba.C = 32, ba.H = 8, ba.W = 8, ba.nsrc = 1, ba.D = 4;
+  CHECK(aarmvs_sweep_backward(&ba, nullptr) == AARMVS_ERR_INVALID);   // null pointers
+  ba.ref_fea = dummy, ba.src_fea[0] = dummy, ba.rel_proj = dummy, ba.depth_values = dummy;
+  ba.packed_params = dummy, ba.grad_cost = dummy, ba.workspace = dummy, ba.scratch = dummy;
+  ba.record = &rec;
+  CHECK(aarmvs_sweep_backward(&ba, nullptr) == AARMVS_ERR_INVALID);   // record buffers null
+  float* rb = dummy;
+  rec.x = rb, rec.state = rb, rec.z = rb, rec.u = rb, rec.stats = reinterpret_cast<double*>(rb);
+  CHECK(aarmvs_sweep_backward(&ba, nullptr) == AARMVS_ERR_INVALID);   // grad_ref required
+  ba.C = 16;
+  CHECK(aarmvs_sweep_backward(&ba, nullptr) == AARMVS_ERR_INVALID);   // C != 32
+  ba.C = 32, ba.H = 6;
+  CHECK(aarmvs_sweep_backward(&ba, nullptr) == AARMVS_ERR_INVALID);   // H % 4
+  a.nsrc = 2;
   CHECK(aarmvs_cost_slice(dummy, srcs, dummy, dummy, dummy, 1, 32, 8, 8, 2, dummy, dummy,
                           nullptr, nullptr) == AARMVS_ERR_INVALID);   // src_fea[1] null
   CHECK(aarmvs_cost_slice(dummy, srcs, dummy, dummy, dummy, 1, 8, 8, 8, 1, dummy, dummy,
