@@ -375,7 +375,7 @@ struct GnbArgs {
 };
 
 __global__ void __launch_bounds__(256) gnb_partial_kernel(GnbArgs a) {
-  __shared__ float red[36 * 4];
+  __shared__ double red[36 * 4];
   __shared__ float coef[2][16];   // a = rstd gamma, b = beta - mean a
   __shared__ float mr[2][2];
   const int b = blockIdx.y;
@@ -391,9 +391,9 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(GnbArgs a) {
     }
   }
   __syncthreads();
-  float s[36];
+  double s[36];   // fp64: cancelling sums
 #pragma unroll
-  for (int i = 0; i < 36; ++i) s[i] = 0.f;
+  for (int i = 0; i < 36; ++i) s[i] = 0.0;
   const float* grb = a.gr + (size_t)b * a.HW * 16;
   const float* ub = a.u + (size_t)b * a.HW * 16;
   for (int p = blockIdx.x * 256 + threadIdx.x; p < a.HW; p += gridDim.x * 256) {
@@ -416,7 +416,7 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(GnbArgs a) {
       }
     }
   }
-  block_sum<36>(s, red);
+  block_sum_d<36>(s, red);
   if (threadIdx.x == 0) {
     double* pp = a.part + ((size_t)b * gridDim.x + blockIdx.x) * 36;
 #pragma unroll

@@ -79,6 +79,31 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* red) {
   __syncthreads();
 }
 
+// block_sum in fp64 (parameter-gradient partials: long cancelling sums)
+template <int NV>
+__device__ __forceinline__ void block_sum_d(double (&v)[NV], double* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o, 64);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[i * nw + wid] = v[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      double s = 0.0;
+      for (int w = 0; w < nw; ++w) s += red[i * nw + w];
+      v[i] = s;
+    }
+  }
+  __syncthreads();
+}
+
 // Add (sum, sumsq) into the statistic's slot picked by the block id.
 __device__ __forceinline__ void stat_add(double* stat, double s, double ss) {
   double* slot = stat + 2 * (blockIdx.x % kSlots);

@@ -1229,7 +1229,7 @@ template <int STAGE>
 __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* __restrict__ P,
                                                         const float* __restrict__ Rel) {
   constexpr int NCOL = STAGE == 1 ? 15 : STAGE == 4 ? 4 : 30;
-  __shared__ float red[NCOL * 4];
+  __shared__ double red[NCOL * 4];
   __shared__ GnStat gs[3];
   __shared__ float gm[3][2];   // per statistic: mean(g_xhat), mean(g_xhat xhat)
   const PipeArgs& pa = a.p;
@@ -1246,9 +1246,9 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
   __syncthreads();
   OmegaP o;
   load_omega(pa, P, o);
-  float s[NCOL];
+  double s[NCOL];   // fp64: the parameter gradients are long cancelling sums
 #pragma unroll
-  for (int i = 0; i < NCOL; ++i) s[i] = 0.f;
+  for (int i = 0; i < NCOL; ++i) s[i] = 0.0;
   const float* m = Rel + 12 * (v * pa.B + b);
   const float dep = pa.dvals[b * pa.D + a.d0 + k];
   const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);
@@ -1364,7 +1364,7 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
     }
     a.gt1[kbv * HW + p] = make_float4(g_t1[0], g_t1[1], g_t1[2], g_t1[3]);
   }
-  block_sum<NCOL>(s, red);
+  block_sum_d<NCOL>(s, red);
   if (threadIdx.x == 0) {
     double* pp = a.part + (kbv * a.pblk + blockIdx.x) * 32;
 #pragma unroll

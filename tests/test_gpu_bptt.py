@@ -10,8 +10,9 @@
   autograd of the oracle through the same planes, per tensor in relative L2.
 
 Tolerances: the forward's cells and the backward's input-gradient convs run three-product
-split-fp16 MFMA (~2^-21 per product); per-tensor relative L2 <= 2e-5 against
-float64 (fp32 CPU autograd itself sits at ~1e-6 .. 1e-5 here).
+split-fp16 MFMA (~2^-21 per product); per tensor, the relative L2 error against
+float64 must be <= 2e-5 or <= twice float32 CPU autograd's own error (the reference's
+arithmetic; bias-like gradients are long cancelling sums where float32 itself is ~1e-4 off).
 """
 import os
 
@@ -64,8 +65,8 @@ def test_recorded_forward_matches_eval_sweep_and_holds_the_tensors():
     from aarmvs import _lib
     B, N, H, W, D = 1, 3, 32, 48, 5
     sc, P, feats, proj, dv, sw, args = _setup(B, N, H, W, D, 3, 4)
-    ev = sw(*args, want_cost=True)
     cost, rec, _ = _record_forward(sw, args, B, H, W, D)
+    ev = sw(*args, want_cost=True)   # (after: a sweep from plane 0 resets the workspace state)
     torch.cuda.synchronize()
     assert torch.equal(cost, ev["cost"])
     # the last state slab = the eval sweep's final state (NHWC views)
@@ -124,6 +125,7 @@ def test_backward_matches_float64_autograd(shape):
     cost, rec, rel = _record_forward(sw, args, B, H, W, D)
     R = torch.randn(B, D, H, W, generator=torch.Generator().manual_seed(5))
     prob64, gf64, gp64, gx64 = _oracle_grads(feats, proj, dv, P, R, torch.float64)
+    _, gf32, gp32, gx32 = _oracle_grads(feats, proj, dv, P, R, torch.float32)
     prob = torch.softmax(cost, dim=1)
     np.testing.assert_allclose(prob.cpu().numpy(), prob64.numpy(), atol=1e-5)
     # dL/dcost of sum(R * softmax(cost))
@@ -133,23 +135,27 @@ def test_backward_matches_float64_autograd(shape):
     # regulariser only: dL/dx per plane and the cost_regularization.* gradients
     _, _, gp_r, gx = sw.backward(ref, srcs, rel, dv, rec, gcost, regulariser_only=True, want_grad_x=True)
     gx = gx.permute(0, 1, 4, 2, 3).cpu().numpy()   # [D,B,32,H,W]
-    errs = {"x": rel_l2(gx, np.stack([g.numpy() for g in gx64]))}
+    # (GPU error, float32 CPU autograd's error), both against float64
+    errs = {"x": (rel_l2(gx, np.stack([g.numpy() for g in gx64])),
+                  rel_l2(np.stack([g.numpy() for g in gx32]), np.stack([g.numpy() for g in gx64])))}
     for k, g in gp_r.items():
         if k.startswith("cost_regularization.") and k != "cost_regularization.conv_0.bias":
-            errs[k] = rel_l2(g.cpu().numpy(), gp64[k].numpy())
+            errs[k] = (rel_l2(g.cpu().numpy(), gp64[k].numpy()), rel_l2(gp32[k].numpy(), gp64[k].numpy()))
         elif k.startswith("omega."):
             assert float(g.abs().max()) == 0.0, k
     # everything
     g_ref, g_src, gp, _ = sw.backward(ref, srcs, rel, dv, rec, gcost)
     gfeat = torch.stack([g_ref] + g_src).cpu().numpy()
-    errs["features"] = rel_l2(gfeat, gf64.numpy())
+    errs["features"] = (rel_l2(gfeat, gf64.numpy()), rel_l2(gf32.numpy(), gf64.numpy()))
     for k, g in gp.items():
         if k != "cost_regularization.conv_0.bias":   # true gradient 0 (softmax over D)
-            errs["all:" + k] = rel_l2(g.cpu().numpy(), gp64[k].numpy())
-    print("\nrelative L2 vs float64:")
-    for k, e in errs.items():
-        print(f"  {k:52s} {e:.3e}")
-    bad = {k: e for k, e in errs.items() if not e <= 2e-5}
+            errs["all:" + k] = (rel_l2(g.cpu().numpy(), gp64[k].numpy()),
+                                rel_l2(gp32[k].numpy(), gp64[k].numpy()))
+    print("\nrelative L2 vs float64 (gpu, cpu float32):")
+    for k, (e, c) in errs.items():
+        print(f"  {k:52s} {e:.3e} {c:.3e}")
+    # within 2e-5, or within twice the float32 CPU autograd's own error (cancelling sums)
+    bad = {k: e for k, e in errs.items() if not e[0] <= max(2e-5, 2.0 * e[1])}
     assert not bad, bad
     assert abs(float(gp["cost_regularization.conv_0.bias"])) <= 1e-5 * float(gcost.abs().sum())
 
