@@ -781,7 +781,7 @@ __global__ void __launch_bounds__(256) deconv_mfma_kernel(const float* __restric
                                                           const float* __restrict__ bias, int Hi,
                                                           int Wi, float* __restrict__ out,
                                                           double* __restrict__ gn_part) {
-  __shared__ float red[4 * 4];
+  __shared__ double red[4 * 4];
   const int b = blockIdx.z, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int x0 = blockIdx.x * kDpTW;
   const int n = lane & 31, hh = lane >> 5;   // B/D column (pixel), channel half
@@ -812,7 +812,7 @@ __global__ void __launch_bounds__(256) deconv_mfma_kernel(const float* __restric
       bl[j] = (_Float16)(t - (float)h);
     }
   };
-  float part[4] = {0.f, 0.f, 0.f, 0.f};
+  double part[4] = {0.0, 0.0, 0.0, 0.0};   // fp64 GroupNorm partials (E[x^2] - E[x]^2 cancels)
   typedef float fx16 __attribute__((ext_vector_type(16)));
 #pragma unroll 1
   for (int rr = 0; rr < 2; ++rr) {
@@ -855,8 +855,8 @@ __global__ void __launch_bounds__(256) deconv_mfma_kernel(const float* __restric
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             v4[u] = fmaf(A[4 * g + u], inv, bias[c0 + u]);
-            part[2 * grp] += v4[u];
-            part[2 * grp + 1] += v4[u] * v4[u];
+            part[2 * grp] += (double)v4[u];
+            part[2 * grp + 1] += (double)v4[u] * v4[u];
           }
           float4* d = reinterpret_cast<float4*>(ob + ((size_t)oy * Wo + ox) * 16 + c0);
           if (!(ABL & 1) || v4[0] == 1234.5f) *d = make_float4(v4[0], v4[1], v4[2], v4[3]);
@@ -864,7 +864,7 @@ __global__ void __launch_bounds__(256) deconv_mfma_kernel(const float* __restric
       }
     }
   }
-  block_sum<4>(part, red);
+  block_sum_d<4>(part, red);
   if (tid == 0) {
     double* pp = gn_part + 4 * (((size_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
 #pragma unroll

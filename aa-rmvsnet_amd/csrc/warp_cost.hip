@@ -646,7 +646,7 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   float* const box = smem;   // chunk c's source box, then (after the last chunk) Y
   float* const yimg = smem;
   __shared__ int red[kMThreads / 64][4];
-  __shared__ float wsum[kMThreads / 64][2];
+  __shared__ double wsum[kMThreads / 64][2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.z;
   const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
@@ -825,7 +825,8 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     }
   }
   __syncthreads();
-  float ps = 0.f, pss = 0.f;
+  // GroupNorm partials in fp64 from the first addition on (var = E[x^2] - E[x]^2 cancels)
+  double ps = 0.0, pss = 0.0;
   if (interior) {
     float g4[4] = {0.f, 0.f, 0.f, 0.f};
     if constexpr ((ABL & 32) != 0) {
@@ -853,11 +854,14 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     out.z = fmaf(g4[2], isc, o4[2]) + b0[2];
     out.w = fmaf(g4[3], isc, o4[3]) + b0[3];
     a.t1_next[kp * a.t1_kstride + ((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
-    ps = (out.x + out.y) + (out.z + out.w);
-    pss = (out.x * out.x + out.y * out.y) + (out.z * out.z + out.w * out.w);
+    ps = ((double)out.x + (double)out.y) + ((double)out.z + (double)out.w);
+    pss = ((double)out.x * out.x + (double)out.y * out.y) + ((double)out.z * out.z + (double)out.w * out.w);
   }
-  ps = wave_sum(ps);
-  pss = wave_sum(pss);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ps += __shfl_xor(ps, o, 64);
+    pss += __shfl_xor(pss, o, 64);
+  }
   if (lane == 0) {
     wsum[wave][0] = ps;
     wsum[wave][1] = pss;
@@ -877,7 +881,7 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
 template <int STAGE>
 __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
                                                           const float* __restrict__ P) {
-  __shared__ float red[2 * 4];
+  __shared__ double red[2 * 4];
   __shared__ GnStat gs[2];
   const int v = blockIdx.y, b = blockIdx.z / a.npl, kp = blockIdx.z - b * a.npl;
   const int HW = a.H * a.W;
@@ -888,7 +892,7 @@ __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
   OmegaP o;
   load_omega(a, P, o);
   const float4* t1 = a.t1_next + kp * a.t1_kstride + ((size_t)b * a.nsrc + v) * HW;
-  float part[2] = {0.f, 0.f};
+  double part[2] = {0.0, 0.0};   // fp64: var = E[x^2] - E[x]^2 cancels
   // four independent 16-B loads in flight per thread per iteration
   const int gstride = gridDim.x * blockDim.x;
   for (int p0 = blockIdx.x * blockDim.x + threadIdx.x; p0 < HW; p0 += 4 * gstride) {
@@ -915,11 +919,11 @@ __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
       gn_relu4(t2, gs[1], o.g1w, o.g1b, true, bb);
       conv1x1_4(bb, o.w2, o.b2, r);
     }
-    part[0] += (r[0] + r[1]) + (r[2] + r[3]);
-    part[1] += (r[0] * r[0] + r[1] * r[1]) + (r[2] * r[2] + r[3] * r[3]);
+    part[0] += ((double)r[0] + (double)r[1]) + ((double)r[2] + (double)r[3]);
+    part[1] += ((double)r[0] * r[0] + (double)r[1] * r[1]) + ((double)r[2] * r[2] + (double)r[3] * r[3]);
     }
   }
-  block_sum<2>(part, red);
+  block_sum_d<2>(part, red);
   if (threadIdx.x == 0) part_put(a, kp, b, v, blockIdx.x, part[0], part[1]);
 }
 
