@@ -47,7 +47,7 @@ const ParamLayout& param_layout() {
     l.owb_scale_off = pk;
     pk += 64;
     l.owm_off = pk;
-    pk += 4 * 2 * 64 * 8 / 2;   // halves -> floats
+    pk += 4 * 3 * 64 * 8 / 2;   // halves -> floats
     for (int k = 0; k < 2; ++k) {
       l.dct_off[k] = pk;
       pk += 16 * 9 * 16;
@@ -297,16 +297,23 @@ __global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __r
     const _Float16 xh = (_Float16)x;
     b[i] = g < 2 ? xh : (_Float16)(x - (float)xh);
   }
-  // omega_mfma's v_mfma_f32_32x32x16_f16 B fragments: per chunk c and kind k (0: [W_hi; W_hi]
-  // against A = [sq hi | sq lo], 1: [W_lo; 0]), lane l holds B[8 (l >> 5) + j][n = l & 31]
-  // with column n = 4 u + co (tap slot u: taps 0..3, 5..8)
+  // omega_mfma's v_mfma_f32_32x32x16_f16 B fragments: per chunk c and kind k against
+  // A = [sq hi | sq lo]: 0: [W_hi; W_hi], 1: [W_lo; 0], 2: [W_lo2; W_lo] with W = W_hi + W_lo +
+  // W_lo2 (three fp16 terms: the weights exact to ~2^-33, so the conv carries no systematic
+  // per-weight error; the dropped terms are sq_lo W_lo2 and sq_lo's own rounding, ~2^-22 random
+  // per product); lane l holds B[8 (l >> 5) + j][n = l & 31] with column n = 4 u + co (tap slot
+  // u: taps 0..3, 5..8)
   _Float16* bm = reinterpret_cast<_Float16*>(pk + L.owm_off);
-  for (int i = threadIdx.x; i < 4 * 2 * 64 * 8; i += blockDim.x) {
-    const int j = i & 7, lane = (i >> 3) & 63, k = (i >> 9) & 1, c = i >> 10;
+  for (int i = threadIdx.x; i < 4 * 3 * 64 * 8; i += blockDim.x) {
+    const int j = i & 7, lane = (i >> 3) & 63, k = (i >> 9) % 3, c = (i >> 9) / 3;
     const int n = lane & 31, u = n >> 2, tap = u < 4 ? u : u + 1, co = n & 3;
     const float x = w[(co * 32 + 8 * c + j) * 9 + tap] * sc;
     const _Float16 xh = (_Float16)x;
-    bm[i] = k == 0 ? xh : ((lane >> 5) == 0 ? (_Float16)(x - (float)xh) : (_Float16)0.0f);
+    const float r1 = x - (float)xh;
+    const _Float16 xl = (_Float16)r1;
+    const _Float16 xl2 = (_Float16)(r1 - (float)xl);
+    const bool top = (lane >> 5) == 0;   // K rows 0-7: against sq hi
+    bm[i] = k == 0 ? xh : k == 1 ? (top ? xl : (_Float16)0.0f) : (top ? xl2 : xl);
   }
 }
 

@@ -424,21 +424,34 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(GnbArgs a) {
   }
 }
 
-// per b: S1, S2 of both groups -> gnb_sum[b][j]; the affine sums (all b, fixed order) -> gacc
-__global__ void gnb_reduce_kernel(const double* __restrict__ part, int nblk, int B, int j,
-                                  double* __restrict__ gnb_sum, double* __restrict__ gacc_gamma,
-                                  double* __restrict__ gacc_beta) {
-  const int i = threadIdx.x;
-  if (i >= 36) return;
+// per b: S1, S2 of both groups -> gnb_sum[b][j]; the affine sums (all b, fixed order) -> gacc.
+// One block per column: strided per-thread sums and a fixed tree per b.
+__global__ void __launch_bounds__(256) gnb_reduce_kernel(const double* __restrict__ part, int nblk,
+                                                         int B, int j, double* __restrict__ gnb_sum,
+                                                         double* __restrict__ gacc_gamma,
+                                                         double* __restrict__ gacc_beta) {
+  __shared__ double red[256];
+  const int i = blockIdx.x, t = threadIdx.x;
   double tot = 0.0;
   for (int b = 0; b < B; ++b) {
     double s = 0.0;
-    for (int k = 0; k < nblk; ++k) s += part[((size_t)b * nblk + k) * 36 + i];
-    if (i < 4) gnb_sum[(b * 2 + j) * 4 + i] = s;
-    tot += s;
+    for (int k = t; k < nblk; k += 256) s += part[((size_t)b * nblk + k) * 36 + i];
+    red[t] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (t < o) red[t] += red[t + o];
+      __syncthreads();
+    }
+    if (t == 0) {
+      if (i < 4) gnb_sum[(b * 2 + j) * 4 + i] = red[0];
+      tot += red[0];
+    }
+    __syncthreads();
   }
-  if (i >= 4 && i < 20) gacc_gamma[i - 4] += tot;
-  if (i >= 20) gacc_beta[i - 20] += tot;
+  if (t == 0) {
+    if (i >= 4 && i < 20) gacc_gamma[i - 4] += tot;
+    if (i >= 20) gacc_beta[i - 20] += tot;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1055,7 +1068,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     const int nblk = std::max(1, std::min(L.gnb_nblk, (int)((hwo + 1023) / 1024)));
     hipLaunchKernelGGL(gnb_partial_kernel, dim3(nblk, B), dim3(256), 0, s, g);
     CK(hipGetLastError());
-    hipLaunchKernelGGL(gnb_reduce_kernel, dim3(1), dim3(64), 0, s, L.gnb_part, nblk, B, j, L.gnb_sum,
+    hipLaunchKernelGGL(gnb_reduce_kernel, dim3(36), dim3(256), 0, s, L.gnb_part, nblk, B, j, L.gnb_sum,
                        L.gacc + PL.raw_off[j ? P_D1GW : P_D0GW], L.gacc + PL.raw_off[j ? P_D1GB : P_D0GB]);
     CK(hipGetLastError());
     DcbArgs a{};

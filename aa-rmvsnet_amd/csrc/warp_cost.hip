@@ -606,8 +606,9 @@ __device__ __forceinline__ void dma_wait() {
 // v_permlane32_swap per dword pair turns the 64 lanes' (hi, lo) into the A operands of
 // two v_mfma_f32_32x32x16_f16 row groups (rows = the 32 pixels of a haloed row; K =
 // [8 ch hi | 8 ch lo]), and
-//   Y[px][u, co] += A x [W_hi ; W_hi]   +   A x [W_lo ; 0]        (u: 8 off-centre taps)
-// gives hi W_hi + lo W_hi + hi W_lo (the split-fp16 product) over
+//   Y[px][u, co] += A x [W_hi ; W_hi]  +  A x [W_lo ; 0]  +  A x [W_lo2 ; W_lo]   (u: 8 off-centre taps)
+// gives hi W_hi + lo W_hi + hi W_lo + hi W_lo2 + lo W_lo (the split-fp16 product with the weights
+// in three fp16 terms, DESIGN.md §Precision: no systematic per-weight error) over
 // the 32 N columns (tap slot u, output channel co).  The centre tap stays an fp32 VALU
 // chain on the lane's own sq.  After the 4 chunks Y goes to LDS (pixel stride 36 floats:
 // conflict-free float4 reads) and each interior pixel sums its 8 neighbours' Y[., u, co].
@@ -790,19 +791,23 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     }
     const half8 A0 = __builtin_bit_cast(half8, u32x4{hw[0], hw[1], hw[2], hw[3]});
     const half8 A1 = __builtin_bit_cast(half8, u32x4{lw[0], lw[1], lw[2], lw[3]});
-    half8 Bd, Bl;
+    half8 Bd, Bl, Bl2;
     if constexpr ((ABL & 128) != 0) {
       Bd = A1;
       Bl = A0;
+      Bl2 = A1;
     } else {
-      Bd = owm[(c * 2 + 0) * 64 + lane];
-      Bl = owm[(c * 2 + 1) * 64 + lane];
+      Bd = owm[(c * 3 + 0) * 64 + lane];
+      Bl = owm[(c * 3 + 1) * 64 + lane];
+      Bl2 = owm[(c * 3 + 2) * 64 + lane];
     }
     if (!(ABL & 1)) {
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, acc1, 0, 0, 0);
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl2, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl2, acc1, 0, 0, 0);
     } else {
       acc0[0] += (float)A0[0] + (float)Bd[1];
       acc1[0] += (float)A1[0] + (float)Bl[1];
@@ -1387,7 +1392,7 @@ __global__ void cbw_gsum_kernel(const double* __restrict__ part, int pblk, doubl
   gsum[kbv * 6 + 2 * st + c] = s;
 }
 
-// parameter columns -> gacc (fixed order: 8 strided row sets per column, then in order)
+// parameter columns -> gacc: one block per column, strided per-thread sums then a fixed tree
 struct CbwCols {
   int c0, ncol;
   int off[30];   // gacc index of column c0 + j
@@ -1395,17 +1400,16 @@ struct CbwCols {
 __global__ void __launch_bounds__(256) cbw_param_kernel(const double* __restrict__ part, int nrow,
                                                         CbwCols cols, double* __restrict__ gacc) {
   __shared__ double red[256];
-  const int t = threadIdx.x, j = t >> 3, r0 = t & 7;
+  const int t = threadIdx.x, j = blockIdx.x;
   double s = 0.0;
-  if (j < cols.ncol)
-    for (int r = r0; r < nrow; r += 8) s += part[(size_t)r * 32 + cols.c0 + j];
+  for (int r = t; r < nrow; r += 256) s += part[(size_t)r * 32 + cols.c0 + j];
   red[t] = s;
   __syncthreads();
-  if (r0 == 0 && j < cols.ncol) {
-    double tot = 0.0;
-    for (int i = 0; i < 8; ++i) tot += red[t + i];
-    gacc[cols.off[j]] += tot;
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
   }
+  if (t == 0) gacc[cols.off[j]] += red[0];
 }
 
 // dL/dsq, the feature gradients and the conv3x3 weight gradient.  Block: a 16 x 16 tile of
@@ -1643,7 +1647,8 @@ static CostBwdLayout cost_bwd_layout(void* base, int B, int H, int W, int nsrc) 
   };
   const size_t HW = (size_t)H * W;
   const int G = kPlaneGroup;
-  L.pblk = std::max(1, std::min((int)((HW + 1023) / 1024), 8 * cu_count() / std::max(1, B * nsrc) + 1));
+  // blocks per (plane, b, view) of the chain kernels: a group launch has G x B x nsrc x pblk
+  L.pblk = std::max(1, std::min((int)((HW + 4095) / 4096), 64));
   L.ntiles16 = ((W + kFbT - 1) / kFbT) * ((H + kFbT - 1) / kFbT);
   L.go = reinterpret_cast<float*>(take((size_t)G * B * nsrc * HW * 4));
   L.gt1 = reinterpret_cast<float4*>(take((size_t)G * B * nsrc * HW * 16));
@@ -1717,28 +1722,36 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   hipLaunchKernelGGL(cbw_chain_kernel<1>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(cbw_gsum_kernel, dim3(nkbv), dim3(64), 0, s, L.part, L.pblk, L.gsum, 2);
-  hipLaunchKernelGGL(cbw_param_kernel, dim3(1), dim3(256), 0, s, L.part, nrow,
-                     cols(2, {{P_OWO, 4}, {P_OBO, 1}, {P_OG2W, 4}, {P_OG2B, 4}}), c.gacc);
+  {
+    const CbwCols cc = cols(2, {{P_OWO, 4}, {P_OBO, 1}, {P_OG2W, 4}, {P_OG2B, 4}});
+    hipLaunchKernelGGL(cbw_param_kernel, dim3(cc.ncol), dim3(256), 0, s, L.part, nrow, cc, c.gacc);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // stage 2: GN2 sums; W2, b2, gamma2, beta2
   hipLaunchKernelGGL(cbw_chain_kernel<2>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(cbw_gsum_kernel, dim3(nkbv), dim3(64), 0, s, L.part, L.pblk, L.gsum, 1);
-  hipLaunchKernelGGL(cbw_param_kernel, dim3(1), dim3(256), 0, s, L.part, nrow,
-                     cols(2, {{P_OW2, 16}, {P_OB2, 4}, {P_OG1W, 4}, {P_OG1B, 4}}), c.gacc);
+  {
+    const CbwCols cc = cols(2, {{P_OW2, 16}, {P_OB2, 4}, {P_OG1W, 4}, {P_OG1B, 4}});
+    hipLaunchKernelGGL(cbw_param_kernel, dim3(cc.ncol), dim3(256), 0, s, L.part, nrow, cc, c.gacc);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // stage 3: GN1 sums; W1, b1, gamma1, beta1
   hipLaunchKernelGGL(cbw_chain_kernel<3>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(cbw_gsum_kernel, dim3(nkbv), dim3(64), 0, s, L.part, L.pblk, L.gsum, 0);
-  hipLaunchKernelGGL(cbw_param_kernel, dim3(1), dim3(256), 0, s, L.part, nrow,
-                     cols(2, {{P_OW1, 16}, {P_OB1, 4}, {P_OG0W, 4}, {P_OG0B, 4}}), c.gacc);
+  {
+    const CbwCols cc = cols(2, {{P_OW1, 16}, {P_OB1, 4}, {P_OG0W, 4}, {P_OG0B, 4}});
+    hipLaunchKernelGGL(cbw_param_kernel, dim3(cc.ncol), dim3(256), 0, s, L.part, nrow, cc, c.gacc);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // stage 4: dL/dt1; b0
   hipLaunchKernelGGL(cbw_chain_kernel<4>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(cbw_param_kernel, dim3(1), dim3(256), 0, s, L.part, nrow, cols(0, {{P_OB0, 4}}),
-                     c.gacc);
+  {
+    const CbwCols cc = cols(0, {{P_OB0, 4}});
+    hipLaunchKernelGGL(cbw_param_kernel, dim3(cc.ncol), dim3(256), 0, s, L.part, nrow, cc, c.gacc);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // dL/dsq -> features, conv3x3 weights
   CbfArgs fa{};
