@@ -11,7 +11,8 @@ import os
 
 MAX_SRC = 16
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libaarmvs.so")
+# AARMVS_LIB: an alternative build of the library (A/B diagnostics; tools/), else the in-tree one
+LIB_PATH = os.environ.get("AARMVS_LIB") or os.path.join(_HERE, "libaarmvs.so")
 
 c_int, c_size_t, c_void_p, c_char_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
 
