@@ -1182,6 +1182,15 @@ hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t
 namespace aarmvs {
 
 // omega chain of one (pixel, view) with its intermediates (omega_weight's operations)
+// DPP within a 16-lane row: the value of lane x - 1 (row_shr:1) / x + 1 (row_shl:1); 0 at the
+// row's edge
+__device__ __forceinline__ int dpp_row_from_left(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int dpp_row_from_right(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xF, 0xF, false);
+}
+
 struct OmegaChain {
   float t[4], v1[4], aa[4], t2[4], v2[4], bb[4], t3[4], g3[4], s3[4], w;
 };
@@ -1412,39 +1421,44 @@ __global__ void __launch_bounds__(256) cbw_param_kernel(const double* __restrict
   if (t == 0) gacc[cols.off[j]] += red[0];
 }
 
-// dL/dsq, the feature gradients and the conv3x3 weight gradient.  Block: a 16 x 16 tile of
-// one sample, all views and all planes of the group, one 8-channel chunk at a time; thread =
-// pixel.  dL/dref accumulates in registers over views and planes (one writer per pixel);
-// dL/dsrc goes to an LDS box per (view, chunk) covering the tile's bilinear taps over the
-// group's planes (corner positions bound them: the plane homography and the position along
-// a depth ray are monotone while z > 0), flushed with global atomics; taps outside the box,
-// or views whose box does not fit, use global atomics directly.  The conv3x3 weight gradient
-// gW0[co][c][tap] = sum_q dL/dt1[q - off(tap)][co] sq[q][c]: thread t < 216 owns (channel, tap)
-// pair t % 72 of the chunk and a third of the tile's pixels, summed in order at the end.
-constexpr int kFbT = 16, kFbBoxPx = 768;
+// dL/dsq, the feature gradients and the conv3x3 weight gradient.  Block: a 16 x 16 tile of one
+// sample, one source view and one 8-channel chunk, all planes of the group; thread = pixel.
+//   dL/dsq = -(1 + w)/nsrc dL/dx + conv3x3^T(dL/dt1)   (this chunk's 8 channels)
+//   dL/dwarp = 2 (warp - ref) dL/dsq;  dL/dref -= dL/dwarp (per view, summed in view order by
+//   cost_bwd_end: one writer per (view, pixel, channel));
+//   dL/dsrc: bilinear scatter of dL/dwarp into an LDS box covering the tile's taps over the
+//   group's planes (corner positions bound them: the plane homography and the position along a
+//   depth ray are monotone while z > 0), flushed once with global atomics; taps outside the
+//   box (or a box that does not fit) use global atomics directly;
+//   gW0[co][c][tap] = sum_q dL/dt1[q - off(tap)][co] sq[q][c]: thread t < 216 owns (channel,
+//   tap) pair t % 72 of the chunk and a third of the tile's pixels, summed in order at the end.
+constexpr int kFbT = 16, kFbBoxPx = 1024;
 struct CbfArgs {
   PipeArgs p;
   const float* gx;          // [n][B][HW][32]
   const float4* gt1;        // [n][B][nsrc][HW]
   float* gsrc8;             // [nsrc][B][4][HW][8] dL/dsrc (c8 layout) accumulated
-  float* gref;              // [B][32][HW] dL/dref (NCHW) accumulated
-  float* wpart;             // [blocks][1152] conv3x3 weight-gradient partials [co][c][tap]
+  float* grefv;             // [nsrc][B][32][HW] dL/dref per view (NCHW) accumulated
+  float* wpart;             // [4 chunks][nsrc][B][tiles][288] conv3x3 weight-gradient partials
   int d0, n;
 };
 
-__global__ void __launch_bounds__(256) cbw_feat_kernel(CbfArgs a, const float* __restrict__ P,
+#ifndef AARMVS_CBF_MINB
+#define AARMVS_CBF_MINB 2
+#endif
+__global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs a, const float* __restrict__ P,
                                                        const float* __restrict__ Rel) {
-  extern __shared__ __attribute__((aligned(16))) char lds_fb[];
-  float* w0s = reinterpret_cast<float*>(lds_fb);                          // [4][32][9]
-  float4* gts = reinterpret_cast<float4*>(lds_fb + 4608);                 // [18][18]
-  float* sqs = reinterpret_cast<float*>(lds_fb + 4608 + 5184);            // [256][8]
-  float* box = sqs + 256 * 8;                                             // [kFbBoxPx][8]
-  float* wsum = box + kFbBoxPx * 8;                                       // [4][72][3][4]
-  __shared__ GnStat gs[3];
+  __shared__ float4 w0q[9][8];                    // this chunk's conv3x3 weights [tap][c] (co in .xyzw)
+  __shared__ float4 gts[18 * 18];                 // dL/dt1 of the haloed tile (one plane)
+  __shared__ float sqs[256][9];                   // the tile's sq (8 channels, padded)
+  __shared__ __attribute__((aligned(16))) float box[kFbBoxPx * 8];
+  __shared__ float wsum[72][3][4];
+  __shared__ GnStat gsk[kPlaneGroup][3];
   __shared__ int bred[4][4];
   __shared__ int bad;
   const PipeArgs& pa = a.p;
-  const int tid = threadIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, b = blockIdx.z;
+  const int v = blockIdx.y >> 2, c = blockIdx.y & 3;
   const int H = pa.H, W = pa.W, HW = H * W, nsrc = pa.nsrc;
   const int tiles_x = (W + kFbT - 1) / kFbT;
   const int tx0 = (blockIdx.x % tiles_x) * kFbT, ty0 = (blockIdx.x / tiles_x) * kFbT;
@@ -1452,166 +1466,256 @@ __global__ void __launch_bounds__(256) cbw_feat_kernel(CbfArgs a, const float* _
   const int x = tx0 + lx, y = ty0 + ly;
   const bool in = x < W && y < H;
   const int p = in ? y * W + x : 0;
-  for (int i = tid; i < 4 * 32 * 9; i += 256) w0s[i] = P[pa.off_ow0 + i];   // raw [co][c][tap]
+  if (tid < 72) {   // raw [co][32][tap]
+    const int tap = tid % 9, j = tid / 9;
+    const float* w = P + pa.off_ow0 + (8 * c + j) * 9 + tap;
+    w0q[tap][j] = make_float4(w[0], w[288], w[576], w[864]);
+  }
+  if (tid < 3 * a.n) {
+    const int k = tid / 3, st = tid % 3;
+    gsk[k][st] = stat_read(pa.st_prev + k * pa.st_kstride + st_index(b, v, st, nsrc), 4.0 * HW);
+  }
+  if (tid == 0) bad = 0;
   OmegaP o;
   load_omega(pa, P, o);
   const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);
   const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(pa.ref + (size_t)b * kC * HW, fbytes);
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(pa.src[v] + (size_t)b * kC * HW, fbytes);
+  const float* m = Rel + 12 * (v * pa.B + b);
   const int pair = tid % 72, sub = tid / 72;   // weight-gradient role (tid < 216)
   const int pch = pair / 9, ptap = pair % 9;
   const int q0 = sub * 86, q1 = min(256, q0 + 86);
-#pragma unroll 1
-  for (int c = 0; c < 4; ++c) {
-    float gref[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float wacc[4] = {0.f, 0.f, 0.f, 0.f};
-    const float4 rf0 = in ? ld_c8(rref, (uint32_t)p, 2 * c, HW) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 rf1 = in ? ld_c8(rref, (uint32_t)p, 2 * c + 1, HW) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 1
-    for (int v = 0; v < nsrc; ++v) {
-      const float* m = Rel + 12 * (v * pa.B + b);
-      const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(pa.src[v] + (size_t)b * kC * HW, fbytes);
-      // this view's source box over the group's planes: tile corners x planes
-      int bx0 = INT_MAX, by0 = INT_MAX, bx1 = -1, by1 = -1;
-      if (tid == 0) bad = 0;
-      __syncthreads();
-      if (tid < 4 * a.n) {
-        const int cx = (tid & 1) ? min(tx0 + kFbT - 1, W - 1) : tx0;
-        const int cy = (tid & 2) ? min(ty0 + kFbT - 1, H - 1) : ty0;
-        const float dep = pa.dvals[b * pa.D + a.d0 + (tid >> 2)];
-        const float zc = (m[8] * (float)cx + m[9] * (float)cy + m[10]) * dep + m[11];
-        const TapF tf = tap_f(m, dep, cx, cy, H, W);
-        if (!(zc > 0.f) || !(tf.xf == tf.xf) || !(tf.yf == tf.yf) || fabsf(tf.xf) > 1e6f ||
-            fabsf(tf.yf) > 1e6f) {
-          bad = 1;
-        } else {
-          bx0 = max(0, (int)tf.xf);
-          by0 = max(0, (int)tf.yf);
-          bx1 = min(W - 1, (int)tf.xf + 1);
-          by1 = min(H - 1, (int)tf.yf + 1);
-        }
-      }
-      const Box bxr = box_reduce<4>(bx0, by0, bx1, by1, bred);
-      const bool use_box = !bad && bxr.nx > 0 && bxr.ny > 0 && bxr.nx * bxr.ny <= kFbBoxPx;
-      if (use_box)
-        for (int i = tid; i < bxr.nx * bxr.ny * 8; i += 256) box[i] = 0.f;
-#pragma unroll 1
-      for (int k = 0; k < a.n; ++k) {
-        __syncthreads();   // box zeroed / previous plane's LDS reads done
-        const size_t kbv = ((size_t)k * pa.B + b) * nsrc + v;
-        for (int i = tid; i < 18 * 18; i += 256) {
-          const int hy = i / 18, hx = i % 18, gy = ty0 - 1 + hy, gxx = tx0 - 1 + hx;
-          gts[i] = (gy >= 0 && gy < H && gxx >= 0 && gxx < W) ? a.gt1[kbv * HW + gy * W + gxx]
-                                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        if (tid < 3)
-          gs[tid] = stat_read(pa.st_prev + k * pa.st_kstride + st_index(b, v, tid, nsrc), 4.0 * HW);
-        __syncthreads();
-        float sqv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (in) {
-          const float dep = pa.dvals[b * pa.D + a.d0 + k];
-          const TapF tf = tap_f(m, dep, x, y, H, W);
-          const Box none{0, 0, 0, 0};
-          const TapP t = tap_p(tf, true, H, W, false, none, fbytes / 32u);
-          const float4 g0 = bil4(ld_c8(rsrc, t.pix[0], 2 * c, HW), ld_c8(rsrc, t.pix[1], 2 * c, HW),
-                                 ld_c8(rsrc, t.pix[2], 2 * c, HW), ld_c8(rsrc, t.pix[3], 2 * c, HW), t);
-          const float4 g1 = bil4(ld_c8(rsrc, t.pix[0], 2 * c + 1, HW), ld_c8(rsrc, t.pix[1], 2 * c + 1, HW),
-                                 ld_c8(rsrc, t.pix[2], 2 * c + 1, HW), ld_c8(rsrc, t.pix[3], 2 * c + 1, HW), t);
-          const float4 s0 = sqdiff4(g0, rf0), s1 = sqdiff4(g1, rf1);
-          const float wv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-          const float rv[8] = {rf0.x, rf0.y, rf0.z, rf0.w, rf1.x, rf1.y, rf1.z, rf1.w};
-          sqv[0] = s0.x; sqv[1] = s0.y; sqv[2] = s0.z; sqv[3] = s0.w;
-          sqv[4] = s1.x; sqv[5] = s1.y; sqv[6] = s1.z; sqv[7] = s1.w;
-          OmegaChain ch;
-          omega_chain(pa.t1_prev[k * pa.t1_kstride + ((size_t)b * nsrc + v) * HW + p], gs, o, ch);
-          const float* gxp = a.gx + (((size_t)k * pa.B + b) * HW + p) * kC + 8 * c;
-          const float dsc = -(ch.w + 1.0f) / (float)nsrc;
-          float gw[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float gsq = dsc * gxp[j];
-            const int cc = 8 * c + j;
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap) {
-              const float4 gt = gts[(ly + 2 - tap / 3) * 18 + lx + 2 - tap % 3];
-              gsq = fmaf(w0s[(0 * 32 + cc) * 9 + tap], gt.x, gsq);
-              gsq = fmaf(w0s[(1 * 32 + cc) * 9 + tap], gt.y, gsq);
-              gsq = fmaf(w0s[(2 * 32 + cc) * 9 + tap], gt.z, gsq);
-              gsq = fmaf(w0s[(3 * 32 + cc) * 9 + tap], gt.w, gsq);
-            }
-            gw[j] = 2.0f * (wv[j] - rv[j]) * gsq;
-            gref[j] -= gw[j];
-          }
-          // bilinear scatter of dL/dwarp into the source view (grid_sample backward)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float xf = tf.xf + (float)(q & 1), yf = tf.yf + (float)(q >> 1);
-            const bool ok = (xf > -1.0f) && (xf < (float)W) && (yf > -1.0f) && (yf < (float)H);
-            if (!ok) continue;
-            const int xi = (int)xf, yi = (int)yf;
-            const float wt = tf.wt[q];
-            if (use_box && xi >= bxr.x0 && xi < bxr.x0 + bxr.nx && yi >= bxr.y0 && yi < bxr.y0 + bxr.ny) {
-              float* bp = box + ((yi - bxr.y0) * bxr.nx + (xi - bxr.x0)) * 8;
-#pragma unroll
-              for (int j = 0; j < 8; ++j) atomicAdd(bp + j, wt * gw[j]);
-            } else {
-              float* gp = a.gsrc8 + ((((size_t)v * pa.B + b) * 4 + c) * HW + (size_t)yi * W + xi) * 8;
-#pragma unroll
-              for (int j = 0; j < 8; ++j) atomicAdd(gp + j, wt * gw[j]);
-            }
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sqs[tid * 8 + j] = sqv[j];
-        __syncthreads();
-        if (tid < 216) {
-          const int dy = ptap / 3, dx = ptap % 3;
-          for (int qq = q0; qq < q1; ++qq) {
-            const float sv = sqs[qq * 8 + pch];
-            const float4 gt = gts[((qq >> 4) + 2 - dy) * 18 + (qq & 15) + 2 - dx];
-            wacc[0] = fmaf(gt.x, sv, wacc[0]);
-            wacc[1] = fmaf(gt.y, sv, wacc[1]);
-            wacc[2] = fmaf(gt.z, sv, wacc[2]);
-            wacc[3] = fmaf(gt.w, sv, wacc[3]);
-          }
-        }
-      }
-      __syncthreads();
-      if (use_box) {   // flush the box: 8 contiguous channels per source pixel
-        float* gb = a.gsrc8 + (((size_t)v * pa.B + b) * 4 + c) * HW * 8;
-        for (int i = tid; i < bxr.nx * bxr.ny * 8; i += 256) {
-          const int px = i >> 3, j = i & 7, ry = px / bxr.nx, rx = px % bxr.nx;
-          const float val = box[i];
-          if (val != 0.f) atomicAdd(gb + ((size_t)(bxr.y0 + ry) * W + bxr.x0 + rx) * 8 + j, val);
-        }
-      }
-    }
-    if (in) {
-      float* gr = a.gref + (size_t)b * kC * HW + p;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) gr[(size_t)(8 * c + j) * HW] += gref[j];
-    }
-    if (tid < 216) {
-#pragma unroll
-      for (int co = 0; co < 4; ++co) wsum[((c * 72 + pair) * 3 + sub) * 4 + co] = wacc[co];
+  float gref[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float wacc[4] = {0.f, 0.f, 0.f, 0.f};
+  const float4 rf0 = in ? ld_c8(rref, (uint32_t)p, 2 * c, HW) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 rf1 = in ? ld_c8(rref, (uint32_t)p, 2 * c + 1, HW) : make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  // the source box over the group's planes: tile corners x planes
+  int bx0 = INT_MAX, by0 = INT_MAX, bx1 = -1, by1 = -1;
+  if (tid < 4 * a.n) {
+    const int cx = (tid & 1) ? min(tx0 + kFbT - 1, W - 1) : tx0;
+    const int cy = (tid & 2) ? min(ty0 + kFbT - 1, H - 1) : ty0;
+    const float dep = pa.dvals[b * pa.D + a.d0 + (tid >> 2)];
+    const float zc = (m[8] * (float)cx + m[9] * (float)cy + m[10]) * dep + m[11];
+    const TapF tf = tap_f(m, dep, cx, cy, H, W);
+    if (!(zc > 0.f) || !(tf.xf == tf.xf) || !(tf.yf == tf.yf) || fabsf(tf.xf) > 1e6f ||
+        fabsf(tf.yf) > 1e6f) {
+      bad = 1;
+    } else {
+      bx0 = max(0, (int)tf.xf);
+      by0 = max(0, (int)tf.yf);
+      bx1 = min(W - 1, (int)tf.xf + 1);
+      by1 = min(H - 1, (int)tf.yf + 1);
     }
   }
+  const Box bxr = box_reduce<4>(bx0, by0, bx1, by1, bred);
+  const bool use_box = !bad && bxr.nx > 0 && bxr.ny > 0 && bxr.nx * bxr.ny <= kFbBoxPx;
+  if (use_box)
+    for (int i = tid; i < bxr.nx * bxr.ny * 8; i += 256) box[(i & 7) * kFbBoxPx + (i >> 3)] = 0.f;
+  const float* gxb = a.gx + 8 * c;
+  // software pipeline: the global operands of plane k + 1 (dL/dt1 halo, t1, dL/dx, the source
+  // gathers) are loaded while plane k is computed
+  const int hi0 = tid, hi1 = tid + 256;
+  auto halo = [&](int i, size_t kbv) {
+    const int hy = i / 18, hx = i % 18, gy = ty0 - 1 + hy, gxx = tx0 - 1 + hx;
+    return (i < 18 * 18 && gy >= 0 && gy < H && gxx >= 0 && gxx < W) ? a.gt1[kbv * HW + gy * W + gxx]
+                                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  float4 nh0, nh1, nt1, ngx0, ngx1, ns[4][2];
+  TapF ntf;
+  auto fetch = [&](int k) {
+    const size_t kbv = ((size_t)k * pa.B + b) * nsrc + v;
+    nh0 = halo(hi0, kbv);
+    nh1 = halo(hi1, kbv);
+    if (in) {
+      nt1 = pa.t1_prev[k * pa.t1_kstride + ((size_t)b * nsrc + v) * HW + p];
+      const float* gxp = gxb + (((size_t)k * pa.B + b) * HW + p) * kC;
+      ngx0 = *reinterpret_cast<const float4*>(gxp);
+      ngx1 = *reinterpret_cast<const float4*>(gxp + 4);
+      ntf = tap_f(m, pa.dvals[b * pa.D + a.d0 + k], x, y, H, W);
+      const Box none{0, 0, 0, 0};
+      const TapP t = tap_p(ntf, true, H, W, false, none, fbytes / 32u);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ns[q][0] = ld_c8(rsrc, t.pix[q], 2 * c, HW);
+        ns[q][1] = ld_c8(rsrc, t.pix[q], 2 * c + 1, HW);
+      }
+    }
+  };
+  fetch(0);
+#pragma unroll 1
+  for (int k = 0; k < a.n; ++k) {
+    __syncthreads();   // box zeroed / previous plane's LDS reads done
+    gts[hi0] = nh0;
+    if (hi1 < 18 * 18) gts[hi1] = nh1;
+    __syncthreads();
+    const float4 t1v = nt1, gx0 = ngx0, gx1 = ngx1;
+    const TapF tf = ntf;
+    float4 sv4[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      sv4[q][0] = ns[q][0];
+      sv4[q][1] = ns[q][1];
+    }
+    if (k + 1 < a.n) fetch(k + 1);
+    float sqv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float gw[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (in) {
+      const Box none{0, 0, 0, 0};
+      const TapP t = tap_p(tf, true, H, W, false, none, fbytes / 32u);
+      const float4 g0 = bil4(sv4[0][0], sv4[1][0], sv4[2][0], sv4[3][0], t);
+      const float4 g1 = bil4(sv4[0][1], sv4[1][1], sv4[2][1], sv4[3][1], t);
+      const float4 s0 = sqdiff4(g0, rf0), s1 = sqdiff4(g1, rf1);
+      const float wv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float rv[8] = {rf0.x, rf0.y, rf0.z, rf0.w, rf1.x, rf1.y, rf1.z, rf1.w};
+      sqv[0] = s0.x; sqv[1] = s0.y; sqv[2] = s0.z; sqv[3] = s0.w;
+      sqv[4] = s1.x; sqv[5] = s1.y; sqv[6] = s1.z; sqv[7] = s1.w;
+      OmegaChain ch;
+      omega_chain(t1v, gsk[k], o, ch);
+      const float gxv[8] = {gx0.x, gx0.y, gx0.z, gx0.w, gx1.x, gx1.y, gx1.z, gx1.w};
+      const float dsc = -(ch.w + 1.0f) / (float)nsrc;
+      float gsq[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gsq[j] = dsc * gxv[j];
+#pragma unroll 3
+      for (int tap = 0; tap < 9; ++tap) {
+        const float4 gt = gts[(ly + 2 - tap / 3) * 18 + lx + 2 - tap % 3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float4 w = w0q[tap][j];
+          gsq[j] = fmaf(w.x, gt.x, gsq[j]);
+          gsq[j] = fmaf(w.y, gt.y, gsq[j]);
+          gsq[j] = fmaf(w.z, gt.z, gsq[j]);
+          gsq[j] = fmaf(w.w, gt.w, gsq[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        gw[j] = 2.0f * (wv[j] - rv[j]) * gsq[j];
+        gref[j] -= gw[j];
+      }
+    }
+    // bilinear scatter of dL/dwarp into the source view (grid_sample backward).  Pairs along a
+    // tile row whose taps are horizontally adjacent (corner 1, 3 of pixel x = corner 0, 2 of
+    // pixel x + 1: the usual case) are merged first (DPP within the 16-lane row): one atomic
+    // per shared source pixel instead of two.
+    {
+      const bool fin = in && tf.xf == tf.xf && tf.yf == tf.yf;
+      const int kx = fin ? (int)fminf(fmaxf(tf.xf, -8.f), (float)W + 8.f) : -100;
+      const int ky = fin ? (int)fminf(fmaxf(tf.yf, -8.f), (float)H + 8.f) : -100;
+      const int lkx = dpp_row_from_left(kx), lky = dpp_row_from_left(ky);
+      const int rkx = dpp_row_from_right(kx), rky = dpp_row_from_right(ky);
+      const bool take = lx > 0 && lkx + 1 == kx && lky == ky;
+      const bool give = lx < 15 && rkx == kx + 1 && rky == ky;
+      float c0[8], c2[8], c1[8], c3[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float r1 = __int_as_float(dpp_row_from_left(__float_as_int(tf.wt[1] * gw[j])));
+        const float r3 = __int_as_float(dpp_row_from_left(__float_as_int(tf.wt[3] * gw[j])));
+        c0[j] = take ? tf.wt[0] * gw[j] + r1 : tf.wt[0] * gw[j];
+        c2[j] = take ? tf.wt[2] * gw[j] + r3 : tf.wt[2] * gw[j];
+        c1[j] = tf.wt[1] * gw[j];
+        c3[j] = tf.wt[3] * gw[j];
+      }
+      if (in) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if ((q & 1) && give) continue;   // handed to the right neighbour
+          const float xf = tf.xf + (float)(q & 1), yf = tf.yf + (float)(q >> 1);
+          const bool ok = (xf > -1.0f) && (xf < (float)W) && (yf > -1.0f) && (yf < (float)H);
+          if (!ok) continue;
+          const int xi = (int)xf, yi = (int)yf;
+          float cv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cv[j] = q == 0 ? c0[j] : q == 1 ? c1[j] : q == 2 ? c2[j] : c3[j];
+          if (use_box && xi >= bxr.x0 && xi < bxr.x0 + bxr.nx && yi >= bxr.y0 && yi < bxr.y0 + bxr.ny) {
+            float* bp = box + (yi - bxr.y0) * bxr.nx + (xi - bxr.x0);   // channel planes
+#pragma unroll
+            for (int j = 0; j < 8; ++j) atomicAdd(bp + j * kFbBoxPx, cv[j]);
+          } else {
+            float* gp = a.gsrc8 + ((((size_t)v * pa.B + b) * 4 + c) * HW + (size_t)yi * W + xi) * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) atomicAdd(gp + j, cv[j]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sqs[tid][j] = sqv[j];
+    __syncthreads();
+    if (tid < 216) {
+      const int dy = ptap / 3, dx = ptap % 3;
+#pragma unroll 6
+      for (int qq = q0; qq < q1; ++qq) {
+        const float sv = sqs[qq][pch];
+        const float4 gt = gts[((qq >> 4) + 2 - dy) * 18 + (qq & 15) + 2 - dx];
+        wacc[0] = fmaf(gt.x, sv, wacc[0]);
+        wacc[1] = fmaf(gt.y, sv, wacc[1]);
+        wacc[2] = fmaf(gt.z, sv, wacc[2]);
+        wacc[3] = fmaf(gt.w, sv, wacc[3]);
+      }
+    }
+  }
+  if (in) {
+    float* gr = a.grefv + ((size_t)v * pa.B + b) * kC * HW + p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gr[(size_t)(8 * c + j) * HW] += gref[j];
+  }
+  if (tid < 216) {
+#pragma unroll
+    for (int co = 0; co < 4; ++co) wsum[pair][sub][co] = wacc[co];
+  }
   __syncthreads();
-  float* wp = a.wpart + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 1152;
-  for (int i = tid; i < 1152; i += 256) {   // i = (co * 32 + cc) * 9 + tap
-    const int tap = i % 9, cc = (i / 9) % 32, co = i / 288;
-    const int c = cc >> 3, pr = (cc & 7) * 9 + tap;
-    const float* ws3 = wsum + ((c * 72 + pr) * 3) * 4 + co;
+  if (use_box) {   // flush the box: 8 contiguous channels per source pixel
+    float* gb = a.gsrc8 + (((size_t)v * pa.B + b) * 4 + c) * HW * 8;
+    for (int i = tid; i < bxr.nx * bxr.ny * 8; i += 256) {
+      const int px = i >> 3, j = i & 7, ry = px / bxr.nx, rx = px % bxr.nx;
+      const float val = box[j * kFbBoxPx + px];
+      if (val != 0.f) atomicAdd(gb + ((size_t)(bxr.y0 + ry) * W + bxr.x0 + rx) * 8 + j, val);
+    }
+  }
+  const size_t blk = (((size_t)c * nsrc + v) * pa.B + b) * gridDim.x + blockIdx.x;
+  float* wp = a.wpart + blk * 288;
+  for (int i = tid; i < 288; i += 256) {   // i = (co * 8 + j) * 9 + tap
+    const int tap = i % 9, j = (i / 9) % 8, co = i / 72;
+    const float* ws3 = &wsum[j * 9 + tap][0][co];
     wp[i] = (ws3[0] + ws3[4]) + ws3[8];
   }
 }
 
-__global__ void __launch_bounds__(256) cbw_w0_reduce_kernel(const float* __restrict__ wpart, int nblk,
+// per chunk c: sum the (view, b, tile) partials in a fixed order -> gW0[co][8c + j][tap], in
+// two passes: 64 contiguous segments of the partials (blockIdx.y), then the segments in order.
+constexpr int kW0Seg = 64;
+__global__ void __launch_bounds__(256) cbw_w0_seg_kernel(const float* __restrict__ wpart, int nblk,
+                                                         double* __restrict__ wseg) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 1152) return;
+  const int tap = i % 9, cc = (i / 9) % 32, co = i / 288;
+  const int c = cc >> 3, j = cc & 7;
+  const float* src = wpart + (size_t)c * nblk * 288 + (co * 8 + j) * 9 + tap;
+  const int k0 = (int)((long)blockIdx.y * nblk / kW0Seg), k1 = (int)((long)(blockIdx.y + 1) * nblk / kW0Seg);
+  double s = 0.0;
+  for (int k = k0; k < k1; ++k) s += src[(size_t)k * 288];
+  wseg[(size_t)blockIdx.y * 1152 + i] = s;
+}
+
+__global__ void __launch_bounds__(256) cbw_w0_reduce_kernel(const double* __restrict__ wseg,
                                                             double* __restrict__ gw) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= 1152) return;
   double s = 0.0;
-  for (int k = 0; k < nblk; ++k) s += wpart[(size_t)k * 1152 + i];
+  for (int k = 0; k < kW0Seg; ++k) s += wseg[(size_t)k * 1152 + i];
   gw[i] += s;
+}
+
+// dL/dref = sum over views (in view order) of the per-view accumulators
+__global__ void __launch_bounds__(256) cbw_ref_sum_kernel(const float* __restrict__ grefv, int nsrc,
+                                                          size_t n, float* __restrict__ gref) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    float s = grefv[i];
+    for (int v = 1; v < nsrc; ++v) s += grefv[(size_t)v * n + i];
+    gref[i] = s;
+  }
 }
 
 // c8 [B][4][HW][8] -> NCHW [B][32][HW]
@@ -1631,7 +1735,9 @@ struct CostBwdLayout {
   double* gsum;
   double* part;
   float* wpart;
+  double* wseg;
   float* gsrc8;
+  float* grefv;
   size_t bytes;
   int pblk, ntiles16;
 };
@@ -1654,8 +1760,10 @@ static CostBwdLayout cost_bwd_layout(void* base, int B, int H, int W, int nsrc) 
   L.gt1 = reinterpret_cast<float4*>(take((size_t)G * B * nsrc * HW * 16));
   L.gsum = reinterpret_cast<double*>(take((size_t)G * B * nsrc * 6 * 8));
   L.part = reinterpret_cast<double*>(take((size_t)G * B * nsrc * L.pblk * 32 * 8));
-  L.wpart = reinterpret_cast<float*>(take((size_t)L.ntiles16 * B * 1152 * 4));
+  L.wpart = reinterpret_cast<float*>(take((size_t)4 * nsrc * B * L.ntiles16 * 288 * 4));
+  L.wseg = reinterpret_cast<double*>(take((size_t)kW0Seg * 1152 * 8));
   L.gsrc8 = reinterpret_cast<float*>(take((size_t)nsrc * B * 32 * HW * 4));
+  L.grefv = reinterpret_cast<float*>(take((size_t)nsrc * B * 32 * HW * 4));
   L.bytes = off;
   return L;
 }
@@ -1680,9 +1788,7 @@ hipError_t cost_bwd_begin(CostBwdCtx& c, hipStream_t s) {
   hipError_t e;
   const size_t HW = (size_t)a->H * a->W;
   if ((e = hipMemsetAsync(L.gsrc8, 0, (size_t)a->nsrc * a->B * 32 * HW * 4, s)) != hipSuccess) return e;
-  if (a->grad_ref && (e = hipMemsetAsync(a->grad_ref, 0, (size_t)a->B * 32 * HW * 4, s)) != hipSuccess)
-    return e;
-  return hipSuccess;
+  return hipMemsetAsync(L.grefv, 0, (size_t)a->nsrc * a->B * 32 * HW * 4, s);
 }
 
 hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t s) {
@@ -1759,22 +1865,17 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   fa.gx = gx;
   fa.gt1 = L.gt1;
   fa.gsrc8 = L.gsrc8;
-  fa.gref = a->grad_ref;
+  fa.grefv = L.grefv;
   fa.wpart = L.wpart;
   fa.d0 = g0;
   fa.n = n;
-  constexpr size_t lds = 4608 + 5184 + 256 * 8 * 4 + kFbBoxPx * 8 * 4 + 4 * 72 * 3 * 4 * 4;
-  static bool attr = false;
-  if (!attr) {
-    if ((e = hipFuncSetAttribute((const void*)cbw_feat_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)lds)) != hipSuccess)
-      return e;
-    attr = true;
-  }
-  hipLaunchKernelGGL(cbw_feat_kernel, dim3(L.ntiles16, a->B), dim3(256), lds, s, fa, ba.p.params, ba.p.rel);
+  hipLaunchKernelGGL(cbw_feat_kernel, dim3(L.ntiles16, 4 * a->nsrc, a->B), dim3(256), 0, s, fa,
+                     ba.p.params, ba.p.rel);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(cbw_w0_reduce_kernel, dim3(5), dim3(256), 0, s, L.wpart, L.ntiles16 * a->B,
-                     c.gacc + PL.raw_off[P_OW0]);
+  hipLaunchKernelGGL(cbw_w0_seg_kernel, dim3(5, kW0Seg), dim3(256), 0, s, L.wpart,
+                     a->nsrc * a->B * L.ntiles16, L.wseg);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(cbw_w0_reduce_kernel, dim3(5), dim3(256), 0, s, L.wseg, c.gacc + PL.raw_off[P_OW0]);
   return hipGetLastError();
 }
 
@@ -1782,6 +1883,13 @@ hipError_t cost_bwd_end(CostBwdCtx& c, hipStream_t s) {
   const aarmvs_backward_args* a = c.a;
   CostBwdLayout L = cost_bwd_layout(c.scratch, a->B, a->H, a->W, a->nsrc);
   const int HW = a->H * a->W;
+  {
+    const size_t n = (size_t)a->B * 32 * HW;
+    hipLaunchKernelGGL(cbw_ref_sum_kernel, dim3((unsigned)std::min<size_t>(4096, (n + 255) / 256)), dim3(256),
+                       0, s, L.grefv, a->nsrc, n, a->grad_ref);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   for (int v = 0; v < a->nsrc; ++v) {
     if (!a->grad_src[v]) continue;
     hipLaunchKernelGGL(c8_to_nchw_kernel, dim3(std::min(4096, (32 * HW + 255) / 256), a->B), dim3(256), 0, s,
