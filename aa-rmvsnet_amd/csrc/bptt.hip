@@ -82,11 +82,13 @@ struct BpttLayout {
   double* gnb_sum;     // [B][2 deconvs][2 groups][2]: (sum g xhat-grad, sum g xhat-grad xhat)
   double* gacc;        // [raw param count] fp64 parameter-gradient accumulators
   float* wpart;        // [kWgBlocks][kWgPartMax] wgrad partials
+  double* rseg;        // [kRedSeg][kWgPartMax] segment sums of the partials
   size_t bytes;
   size_t cell_px[5];
   int gnb_nblk;
 };
 constexpr size_t kWgPartMax = 64 * 64 * 9 + 64;
+constexpr int kRedSeg = 64;      // segments of the two-pass partial reduction
 
 static inline size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 
@@ -121,6 +123,7 @@ BpttLayout bptt_layout(void* base, int B, int H, int W) {
   L.gnb_sum = reinterpret_cast<double*>(take((size_t)B * 8 * 8));
   L.gacc = reinterpret_cast<double*>(take(param_layout().raw_total * 8));
   L.wpart = reinterpret_cast<float*>(take((size_t)kWgBlocks * kWgPartMax * 4));
+  L.rseg = reinterpret_cast<double*>(take((size_t)kRedSeg * kWgPartMax * 8));
   L.bytes = off;
   return L;
 }
@@ -561,11 +564,9 @@ __global__ void __launch_bounds__(256) deconv_bwd_kernel(DcbArgs a) {
 // Cell weight gradient over a group of planes: gW[cz][ci][tap] = sum_{d,p} gz_d[p][cz] in_d[p +
 // off(tap)][ci], gb[cz] = sum gz.  v_mfma_f32_16x16x32_f16 with K = the 32 pixels of a tile
 // row: A = gz^T (16 gate channels x 32 px, from a channel-major LDS image), B = the cell input
-// at the tap's offset (32 px x 16 input channels, from one of three column-shifted LDS copies
-// of the haloed input tile, so every fragment read is a 16-B aligned row).  Four split-fp16
-// products per MFMA step (hi hi, hi lo, lo hi, lo lo: ~fp32 products).  blockIdx.y = 16-channel
-// input chunk; the blocks stride over the group's (plane, tile) items and write one partial
-// each; wave w owns gate m-tile w % (CZ/16) and every (4 / (CZ/16))-th tap.
+// at the tap's offset (32 px x 16 input channels).  Four split-fp16 products per MFMA step
+// (hi hi, hi lo, lo hi, lo lo: ~fp32 products).  Blocks stride over the group's (plane, tile)
+// items and write one partial each, reduced in a fixed order (reduce_partials).
 // ---------------------------------------------------------------------------
 enum WgMode : int { WG_PLAIN = 0, WG_POOL = 1, WG_GNRELU = 2 };
 struct WgPart {
@@ -580,248 +581,398 @@ struct WgPart {
   float scale;          // staging scale (power of two)
   const unsigned* bound;// if set: scale = 2^-e with *bound 2^-e in [2^14, 2^15) (the cost slice x)
 };
+struct WgChunk {         // one 16-channel input chunk (wgrad2), resolved on the host
+  const float* ptr;     // plane 0's tensor at the chunk's first channel; plane d at + d * dstride
+  size_t dstride;
+  int nch, mode;        // the part's channel count (pixel stride), mode
+  int nv;               // valid channels of the chunk (16 or 8)
+  int j;                // GNRELU: deconv index
+  const double* stats;  // GNRELU: plane 0's reg stats (+ d * sstride)
+  size_t sstride;
+  const float* gamma;   // GNRELU: at the chunk's first channel
+  const float* beta;
+  int gn0;              // GNRELU: GroupNorm group of the chunk's first channel
+  float scale;
+  const unsigned* bound;
+};
 struct WgradArgs {
   const float* gz;        // [G][P][CZ]
   const unsigned* zmax;   // [G] per-plane scales of gz
   WgPart part[3];
+  WgChunk chunk[3];
+  int gn_chunk;           // wgrad2: the GNRELU chunk (its statistics tabled in LDS), or -1
+  double* rseg;           // reduction segments (BpttLayout::rseg)
   int nparts, cin;        // input channels (valid)
   int nplanes, d0;        // group planes: record plane d0 + k  <->  gz slot k
   int B, H, W;            // cell resolution
   float* wpart;           // [gridDim.x][kWgPartMax]: [CZ][cin_pad][9] then bias [CZ]
 };
 
-constexpr int kWgTH = 4, kWgTW = 32;
+// ---------------------------------------------------------------------------
+// wgrad2: all input chunks in one block: each (plane, 4 x 32 tile) item is staged once for
+// every input chunk, and the next item's global operands are loaded into registers while the
+// current item's MFMAs run.  The input is staged once per channel, column c of a row at half 8 + c; a
+// lane's B fragment for tap column dx is its aligned 8 columns shifted by dx - 1, assembled
+// from the aligned 16 B and one neighbouring dword with v_alignbit (no shifted copies).
+// LDS rows are padded so that the 16 lanes of a fragment read hit 16 different bank groups.
+// 512 threads: wave w owns gate m-tile w % (CZ/16) and a share of the (chunk, tap row) combos.
+// ---------------------------------------------------------------------------
+constexpr int kW2TH = 4;                          // tile rows (x 32 columns)
+constexpr int kW2ZS = kW2TH * 32 + 8;             // halves per gate channel
+constexpr int kW2RL = 48;                         // halves per input row (columns -2 .. 33 at 6 .. 41)
+constexpr int kW2IS = (kW2TH + 2) * kW2RL + 8;    // halves per input channel
 
-template <int CZ>
-__global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
-  constexpr int MTZ = CZ / 16, TS = 4 / MTZ;        // m-tiles; tap stride per wave
-  constexpr int NTAP = (9 + TS - 1) / TS;
-  // LDS (dynamic): gz^T [2 hi/lo][CZ][kWgTH][32]; input [2][3 dx][16 ci][kWgTH + 2][32];
-  // bias partials [256 threads][8]
-  extern __shared__ __attribute__((aligned(16))) char lds_wg[];
-  typedef _Float16 ZT[CZ][kWgTH][kWgTW];
-  typedef _Float16 IT[3][16][kWgTH + 2][kWgTW];
-  ZT* zt = reinterpret_cast<ZT*>(lds_wg);
-  IT* it = reinterpret_cast<IT*>(lds_wg + 2 * sizeof(ZT));
-  float (*bred)[8] = reinterpret_cast<float (*)[8]>(lds_wg + 2 * sizeof(ZT) + 2 * sizeof(IT));
+template <int CZ, int NCH>
+constexpr size_t wgrad2_lds() {
+  return (size_t)2 * CZ * kW2ZS * 2 + (size_t)2 * NCH * 16 * kW2IS * 2;
+}
+
+__device__ __forceinline__ unsigned pack_h2(_Float16 a, _Float16 b) {
+  return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
+}
+
+template <int CZ, int NCH>
+__global__ void __launch_bounds__(512) wgrad2_kernel(WgradArgs a) {
+  constexpr int MT = CZ / 16, NS = 8 / MT;
+  constexpr int NCOMBO = NCH * 3, CPW = (NCOMBO + NS - 1) / NS;
+  constexpr int CIN = NCH * 16, NG = CZ / 8;
+  constexpr int NU = (kW2TH + 2) * 18 * NCH;               // input staging units (2 px x 16 ch)
+  static_assert(NU <= 512, "one input unit per thread");
+  extern __shared__ __attribute__((aligned(16))) char lds_w2[];
+  _Float16* zt = reinterpret_cast<_Float16*>(lds_w2);       // [2][CZ][kW2ZS]
+  _Float16* it = zt + 2 * CZ * kW2ZS;                         // [2][CIN][kW2IS]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int mt = wave % MTZ, t0 = wave / MTZ;
-  const int chunk = blockIdx.y;
-  const int tiles_x = (a.W + kWgTW - 1) / kWgTW, tiles_y = (a.H + kWgTH - 1) / kWgTH;
+  const int tiles_x = (a.W + 31) / 32, tiles_y = (a.H + kW2TH - 1) / kW2TH;
   const int ntile = a.B * tiles_x * tiles_y;
   const int nitem = ntile * a.nplanes;
-  bfloatx4 acc[NTAP];
-#pragma unroll
-  for (int t = 0; t < NTAP; ++t) acc[t] = bfloatx4{0.f, 0.f, 0.f, 0.f};
-  // this chunk's input part
-  int pi = 0, lc0 = 16 * chunk;
-  while (pi + 1 < a.nparts && lc0 >= a.part[pi].nch) {
-    lc0 -= a.part[pi].nch;
-    ++pi;
-  }
-  WgPart pt = a.part[pi];
-  if (pt.bound) pt.scale = ldexpf(1.0f, -scale_exp(*pt.bound));
-  const int nv = min(16, pt.nch - lc0);   // valid channels of the chunk (8 or 16)
+  // staging scale of a chunk
+  auto chunk_scale = [&](const WgChunk& ch) {
+    return ch.bound ? ldexpf(1.0f, -scale_exp(*ch.bound)) : ch.scale;
+  };
+  auto item_pos = [&](int item, int& k, int& b, int& y0, int& x0) {
+    k = item / ntile;
+    const int tile = item % ntile;
+    b = tile / (tiles_x * tiles_y);
+    const int rem = tile % (tiles_x * tiles_y);
+    y0 = (rem / tiles_x) * kW2TH;
+    x0 = (rem % tiles_x) * 32;
+  };
+  // staging roles
+  const bool zrole = tid < 64 * NG;
+  const int zpp = tid / NG, zcg = tid % NG;                  // pixel pair (row zpp / 16), channel group
+  const int zr = zpp >> 4, zx = 2 * (zpp & 15);
+  struct Pre {
+    float4 z[4];
+    float4 in[2][2][2];   // [8-channel half][pixel][float4]
+  };
   float bacc[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) bacc[i] = 0.f;
-#pragma unroll 1
-  for (int item = blockIdx.x; item < nitem; item += gridDim.x) {
-    const int k = item / ntile, tile = item % ntile;
-    const int b = tile / (tiles_x * tiles_y), rem = tile % (tiles_x * tiles_y);
-    const int y0 = (rem / tiles_x) * kWgTH, x0 = (rem % tiles_x) * kWgTW;
-    const float zs = ldexpf(1.0f, -scale_exp(a.zmax[k]));
-    __syncthreads();   // previous item's fragment reads done
-    // gz tile -> zt[cz][row][px] (channel-major), scaled; thread: one pixel, 8 channels
-    {
+  // input unit of this thread: chunk uc, tile row rr - 1, columns 2 ucp - 2, 2 ucp - 1
+  const bool irole = tid < NU;
+  const int uc = tid % NCH, ucp = (tid / NCH) % 18, urr = tid / (NCH * 18);
+  const WgChunk uch = a.chunk[uc];            // this thread's chunk, for every item
+  // GroupNorm statistics of the GNRELU chunk for the group's planes: [k][b][group]
+  float2* gst = reinterpret_cast<float2*>(it + 2 * CIN * kW2IS);
+  if (a.gn_chunk >= 0) {
+    const WgChunk& gc = a.chunk[a.gn_chunk];
+    for (int e = tid; e < a.nplanes * a.B * 2; e += 512) {
+      const int kk = e / (2 * a.B), bb = (e >> 1) % a.B, g = e & 1;
+      const GnStat st = stat_read(gc.stats + (size_t)(a.d0 + kk) * gc.sstride + reg_stat_index(bb, gc.j, g),
+                                  8.0 * a.H * a.W);
+      gst[e] = make_float2(st.mean, st.rstd);
+    }
+  }
+  const float usc = chunk_scale(uch);
+  const float zs = ldexpf(1.0f, -scale_exp(a.zmax[0]));   // the group's slots share one exponent
+  auto fetch = [&](int item) {
+    Pre pf;
+    float4(&zq)[4] = pf.z;
+    int k, b, y0, x0;
+    item_pos(item, k, b, y0, x0);
+    if (zrole) {
       const float* gzp = a.gz + (size_t)k * a.B * a.H * a.W * CZ;
-      constexpr int NG = CZ / 8;
-      for (int e = tid; e < kWgTH * kWgTW * NG; e += 256) {
-        const int cg = e % NG, px = e / NG, r = px / kWgTW, xx = px % kWgTW;
-        const int gy = y0 + r, gx = x0 + xx;
-        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (gy < a.H && gx < a.W) {
-          const float4* s = reinterpret_cast<const float4*>(gzp + (((size_t)b * a.H + gy) * a.W + gx) * CZ + 8 * cg);
-          const float4 q0 = s[0], q1 = s[1];
-          v[0] = q0.x; v[1] = q0.y; v[2] = q0.z; v[3] = q0.w;
-          v[4] = q1.x; v[5] = q1.y; v[6] = q1.z; v[7] = q1.w;
-        }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (chunk == 0) bacc[i] += v[i];
-          _Float16 hi, lo;
-          split16(v[i] * zs, hi, lo);
-          zt[0][8 * cg + i][r][xx] = hi;
-          zt[1][8 * cg + i][r][xx] = lo;
+      for (int h = 0; h < 2; ++h) {
+        const int gy = y0 + zr, gx = x0 + zx + h;
+        if (gy < a.H && gx < a.W) {
+          const float4* s4 = reinterpret_cast<const float4*>(gzp + (((size_t)b * a.H + gy) * a.W + gx) * CZ + 8 * zcg);
+          zq[2 * h] = s4[0];
+          zq[2 * h + 1] = s4[1];
+        } else {
+          zq[2 * h] = zq[2 * h + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
     }
-    // input chunk tile (rows y0-1 .. y0+TH, cols x0-1 .. x0+32) -> three column-shifted copies
-    {
-      const float* base = pt.ptr + (size_t)(a.d0 + k) * pt.dstride;
-      const int Hs = pt.mode == WG_POOL ? 2 * a.H : a.H, Ws = pt.mode == WG_POOL ? 2 * a.W : a.W;
-      const float* bb = base + (size_t)b * Hs * Ws * pt.nch;
-      float gsc[16], gsh[16];
-      if (pt.mode == WG_GNRELU) {
-        const double* st = pt.stats + (size_t)(a.d0 + k) * pt.sstride;
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          const GnStat s = stat_read(st + reg_stat_index(b, pt.j, g), 8.0 * a.H * a.W);
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) pf.in[hh][h][0] = pf.in[hh][h][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (irole) {
+      const int gy = y0 - 1 + urr;
+      if (uch.mode != WG_POOL && gy >= 0 && gy < a.H) {
+        const float* bb = uch.ptr + (size_t)(a.d0 + k) * uch.dstride + (size_t)b * a.H * a.W * uch.nch;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          if (8 * hh >= uch.nv) continue;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int gx = x0 + 2 * ucp - 2 + h;
+            if (gx >= 0 && gx < a.W) {
+              const float4* s4 = reinterpret_cast<const float4*>(bb + ((size_t)gy * a.W + gx) * uch.nch + 8 * hh);
+              pf.in[hh][h][0] = s4[0];
+              pf.in[hh][h][1] = s4[1];
+            }
+          }
+        }
+      }
+    }
+    return pf;
+  };
+  // D accumulators: combo i (chunk c = q / 3, tap row dy = q % 3, q = s + NS i) x tap column dx
+  const int mt = wave % MT, sgrp = wave / MT;
+  bfloatx4 acc[CPW][3];
+#pragma unroll
+  for (int i = 0; i < CPW; ++i)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) acc[i][dx] = bfloatx4{0.f, 0.f, 0.f, 0.f};
+  const int item0 = blockIdx.x;
+  Pre pre;
+  if (item0 < nitem) pre = fetch(item0);
+#pragma unroll 1
+  for (int item = item0; item < nitem; item += gridDim.x) {
+    int k, b, y0, x0;
+    item_pos(item, k, b, y0, x0);
+    __syncthreads();   // the previous item's fragment reads are done
+    const float4(&zq)[4] = pre.z;
+    if (zrole) {
+      const float v0[8] = {zq[0].x, zq[0].y, zq[0].z, zq[0].w, zq[1].x, zq[1].y, zq[1].z, zq[1].w};
+      const float v1[8] = {zq[2].x, zq[2].y, zq[2].z, zq[2].w, zq[3].x, zq[3].y, zq[3].z, zq[3].w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        bacc[i] += v0[i] + v1[i];
+        _Float16 h0, l0, h1, l1;
+        split16(v0[i] * zs, h0, l0);
+        split16(v1[i] * zs, h1, l1);
+        const int o = (8 * zcg + i) * kW2ZS + zr * 32 + zx;
+        *reinterpret_cast<unsigned*>(zt + o) = pack_h2(h0, h1);
+        *reinterpret_cast<unsigned*>(zt + CZ * kW2ZS + o) = pack_h2(l0, l1);
+      }
+    }
+    if (irole) {
+      const int c = uc, cp = ucp, rr = urr;
+      const int gy = y0 - 1 + rr;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const bool valid = 8 * hh < uch.nv;
+        float v[2][8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4* q = pre.in[hh][h];
+          v[h][0] = q[0].x; v[h][1] = q[0].y; v[h][2] = q[0].z; v[h][3] = q[0].w;
+          v[h][4] = q[1].x; v[h][5] = q[1].y; v[h][6] = q[1].z; v[h][7] = q[1].w;
+        }
+        if (uch.mode == WG_POOL && valid) {
+          // 2x2 max-pool of the finer state, loaded here (cells 1 and 2)
+          const int Ws = 2 * a.W;
+          const float* bb = uch.ptr + (size_t)(a.d0 + k) * uch.dstride + (size_t)b * 4 * a.H * a.W * uch.nch;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int gx = x0 + 2 * cp - 2 + h;
+            if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+              const float* s0 = bb + ((size_t)(2 * gy) * Ws + 2 * gx) * uch.nch + 8 * hh;
+#pragma unroll 1
+              for (int w = 0; w < 4; ++w) {
+                const float4* s4 = reinterpret_cast<const float4*>(s0 + ((w >> 1) * Ws + (w & 1)) * uch.nch);
+                const float4 a0 = s4[0], a1 = s4[1];
+                const float qq[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[h][i] = w == 0 ? qq[i] : fmaxf(v[h][i], qq[i]);
+              }
+            }
+          }
+        } else if (uch.mode == WG_GNRELU && valid) {
+          const float2 ms = gst[(k * a.B + b) * 2 + uch.gn0 + hh];
+          const GnStat gs{ms.x, ms.y};
+          const bool in0 = gy >= 0 && gy < a.H && x0 + 2 * cp - 2 >= 0 && x0 + 2 * cp - 2 < a.W;
+          const bool in1 = gy >= 0 && gy < a.H && x0 + 2 * cp - 1 >= 0 && x0 + 2 * cp - 1 < a.W;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            const int c = 8 * g + i;
-            gsc[c] = s.rstd * pt.gamma[c];
-            gsh[c] = pt.beta[c] - s.mean * gsc[c];
-          }
-        }
-      }
-      for (int e = tid; e < (kWgTH + 2) * (kWgTW + 2) * 2; e += 256) {
-        const int hh = e & 1, pxl = e >> 1;
-        const int r = pxl / (kWgTW + 2), cc = pxl % (kWgTW + 2);
-        const int gy = y0 - 1 + r, gx = x0 - 1 + cc;
-        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W && 8 * hh < nv) {
-          const int ch = lc0 + 8 * hh;
-          if (pt.mode == WG_POOL) {
-            const float* s0 = bb + ((size_t)(2 * gy) * Ws + 2 * gx) * pt.nch + ch;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-              const float4* s = reinterpret_cast<const float4*>(s0 + ((w >> 1) * Ws + (w & 1)) * pt.nch);
-              const float4 q0 = s[0], q1 = s[1];
-              const float qq[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-#pragma unroll
-              for (int i = 0; i < 8; ++i) v[i] = w == 0 ? qq[i] : fmaxf(v[i], qq[i]);
-            }
-          } else {
-            const float4* s = reinterpret_cast<const float4*>(bb + ((size_t)gy * Ws + gx) * pt.nch + ch);
-            const float4 q0 = s[0], q1 = s[1];
-            v[0] = q0.x; v[1] = q0.y; v[2] = q0.z; v[3] = q0.w;
-            v[4] = q1.x; v[5] = q1.y; v[6] = q1.z; v[7] = q1.w;
-            if (pt.mode == WG_GNRELU) {
-#pragma unroll
-              for (int i = 0; i < 8; ++i) v[i] = fmaxf(fmaf(v[i], gsc[8 * hh + i], gsh[8 * hh + i]), 0.0f);
-            }
+            const float gsc = gs.rstd * uch.gamma[8 * hh + i];
+            const float gsh = uch.beta[8 * hh + i] - gs.mean * gsc;
+            v[0][i] = in0 ? fmaxf(fmaf(v[0][i], gsc, gsh), 0.0f) : 0.0f;
+            v[1][i] = in1 ? fmaxf(fmaf(v[1][i], gsc, gsh), 0.0f) : 0.0f;
           }
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          _Float16 hi, lo;
-          split16(v[i] * pt.scale, hi, lo);
+          _Float16 h0, l0, h1, l1;
+          split16(v[0][i] * usc, h0, l0);
+          split16(v[1][i] * usc, h1, l1);
+          const int o = (16 * c + 8 * hh + i) * kW2IS + rr * kW2RL + 6 + 2 * cp;
+          *reinterpret_cast<unsigned*>(it + o) = pack_h2(h0, h1);
+          *reinterpret_cast<unsigned*>(it + CIN * kW2IS + o) = pack_h2(l0, l1);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one half's values live at a time
+      }
+    }
+    __syncthreads();
+    if (item + (int)gridDim.x < nitem) pre = fetch(item + gridDim.x);   // in flight during the MFMAs
+    const int ar = lane & 15, g = lane >> 4;
+#pragma unroll 1
+    for (int r = 0; r < kW2TH; ++r) {
+      const int ao = (16 * mt + ar) * kW2ZS + r * 32 + 8 * g;
+      const bhalf8 zh = *reinterpret_cast<const bhalf8*>(zt + ao);
+      const bhalf8 zl = *reinterpret_cast<const bhalf8*>(zt + CZ * kW2ZS + ao);
+#pragma unroll
+      for (int i = 0; i < CPW; ++i) {
+        const int q = sgrp + NS * i;
+        if (q < NCOMBO) {
+          const int c = q / 3, dy = q % 3;
+          const int bo = (16 * c + ar) * kW2IS + (r + dy) * kW2RL + 8 + 8 * g;
+          bhalf8 bf[2][3];
+#pragma unroll
+          for (int hl = 0; hl < 2; ++hl) {
+            const _Float16* src = it + hl * CIN * kW2IS + bo;
+            const uint4 U = *reinterpret_cast<const uint4*>(src);
+            const unsigned pv = *reinterpret_cast<const unsigned*>(src - 2);
+            const unsigned nx = *reinterpret_cast<const unsigned*>(src + 8);
+            const unsigned s0 = __builtin_amdgcn_alignbit(U.x, pv, 16);
+            const unsigned s1 = __builtin_amdgcn_alignbit(U.y, U.x, 16);
+            const unsigned s2 = __builtin_amdgcn_alignbit(U.z, U.y, 16);
+            const unsigned s3 = __builtin_amdgcn_alignbit(U.w, U.z, 16);
+            const unsigned s4 = __builtin_amdgcn_alignbit(nx, U.w, 16);
+            bf[hl][0] = __builtin_bit_cast(bhalf8, make_uint4(s0, s1, s2, s3));
+            bf[hl][1] = __builtin_bit_cast(bhalf8, U);
+            bf[hl][2] = __builtin_bit_cast(bhalf8, make_uint4(s1, s2, s3, s4));
+          }
 #pragma unroll
           for (int dx = 0; dx < 3; ++dx) {
-            const int xc = cc - dx;   // copy dx holds image column x0 + xc + dx - 1 at xc
-            if (xc >= 0 && xc < kWgTW) {
-              it[0][dx][8 * hh + i][r][xc] = hi;
-              it[1][dx][8 * hh + i][r][xc] = lo;
-            }
+            acc[i][dx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zh, bf[0][dx], acc[i][dx], 0, 0, 0);
+            acc[i][dx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zh, bf[1][dx], acc[i][dx], 0, 0, 0);
+            acc[i][dx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zl, bf[0][dx], acc[i][dx], 0, 0, 0);
+            acc[i][dx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zl, bf[1][dx], acc[i][dx], 0, 0, 0);
           }
         }
-      }
-    }
-    __syncthreads();
-    // MFMAs: per tile row, A = zt[16 mt + (l & 15)][r][8 (l >> 4) ..], B = it[dx][l & 15][r + dy][8 (l >> 4) ..]
-    const int ar = lane & 15, ak = 8 * (lane >> 4);
-#pragma unroll 1
-    for (int r = 0; r < kWgTH; ++r) {
-      const bhalf8 zh = *reinterpret_cast<const bhalf8*>(&zt[0][16 * mt + ar][r][ak]);
-      const bhalf8 zl = *reinterpret_cast<const bhalf8*>(&zt[1][16 * mt + ar][r][ak]);
-#pragma unroll
-      for (int ti = 0; ti < NTAP; ++ti) {
-        const int tap = t0 + ti * TS;
-        if (tap < 9) {
-          const int dy = tap / 3, dx = tap % 3;
-          const bhalf8 ih = *reinterpret_cast<const bhalf8*>(&it[0][dx][ar][r + dy][ak]);
-          const bhalf8 il = *reinterpret_cast<const bhalf8*>(&it[1][dx][ar][r + dy][ak]);
-          acc[ti] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zh, ih, acc[ti], 0, 0, 0);
-          acc[ti] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zh, il, acc[ti], 0, 0, 0);
-          acc[ti] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zl, ih, acc[ti], 0, 0, 0);
-          acc[ti] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zl, il, acc[ti], 0, 0, 0);
-        }
+        __builtin_amdgcn_sched_barrier(0);   // one combo's fragments live at a time
       }
     }
   }
-  // the per-plane gz scale was applied before the sums: the gz planes of a group share one
-  // scale only if their maxima share an exponent, so undo it per item -- done by requiring a
-  // common scale: see launch_wgrad (the group's zmax slots are equalised first)
-  const float inv = ldexpf(1.0f, scale_exp(a.zmax[0])) / pt.scale;
+  // the group's zmax slots share one exponent (zmax_group_kernel)
+  const float zinv = ldexpf(1.0f, scale_exp(a.zmax[0]));
   float* wp = a.wpart + (size_t)blockIdx.x * kWgPartMax;
   const int cinp = 16 * ((a.cin + 15) / 16);
-  // D: col = ci (lane & 15), row = 4 (lane >> 4) + reg -> cz = 16 mt + row
 #pragma unroll
-  for (int ti = 0; ti < NTAP; ++ti) {
-    const int tap = t0 + ti * TS;
-    if (tap < 9) {
+  for (int i = 0; i < CPW; ++i) {
+    const int q = sgrp + NS * i;
+    if (q < NCOMBO) {
+      const int c = q / 3, dy = q % 3;
+      const float inv = zinv / chunk_scale(a.chunk[c]);
+      const int ci = 16 * c + (lane & 15);
 #pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int cz = 16 * mt + 4 * (lane >> 4) + rg, ci = 16 * chunk + (lane & 15);
-        wp[((size_t)cz * cinp + ci) * 9 + tap] = acc[ti][rg] * inv;
-      }
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const int cz = 16 * mt + 4 * (lane >> 4) + rg;
+          wp[((size_t)cz * cinp + ci) * 9 + 3 * dy + dx] = acc[i][dx][rg] * inv;
+        }
     }
   }
-  if (chunk == 0) {
-    // thread tid staged channel group tid % NG in every item (256 % NG == 0): fixed-order sum
-    constexpr int NG = CZ / 8;
-    __syncthreads();
+  // bias: thread tid staged channel group tid % NG of pixel pair tid / NG in every item
+  __syncthreads();
+  float* bred = reinterpret_cast<float*>(lds_w2);   // [64 NG][8]
+  if (zrole) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) bred[tid][i] = bacc[i];
-    __syncthreads();
-    if (tid < CZ) {
-      float sb = 0.f;
-      for (int t = tid / 8; t < 256; t += NG) sb += bred[t][tid % 8];
-      wp[(size_t)CZ * cinp * 9 + tid] = sb;
-    }
+    for (int i = 0; i < 8; ++i) bred[tid * 8 + i] = bacc[i];
+  }
+  __syncthreads();
+  if (tid < CZ) {
+    const int cg = tid / 8, i = tid % 8;
+    float sb = 0.f;
+    for (int t = cg; t < 64 * NG; t += NG) sb += bred[t * 8 + i];
+    wp[(size_t)CZ * cinp * 9 + tid] = sb;
   }
 }
 
-// partials of nblk blocks -> gacc (raw layout [cz][cin][3][3] then bias [cz]), fixed order
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ wpart, int nblk,
-                                                           int cz, int cin, double* __restrict__ gw,
-                                                           double* __restrict__ gb) {
-  const int cinp = 16 * ((cin + 15) / 16);
-  const int n = cz * cin * 9 + cz;
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
-    size_t src;
+// Partials -> fp64 accumulators, deterministic, in two passes: pass 1 sums each entry over
+// kRedSeg contiguous segments of the nblk partials (blockIdx.y = segment), pass 2 sums the
+// segments in order into the destination (wgrad: raw layout [cz][cin][3][3] then bias [cz],
+// from the partials' [cz][cin_pad][9] + bias; identity: entries < nw to gw, the rest to gb).
+__global__ void __launch_bounds__(256) seg_reduce_kernel(const float* __restrict__ part, int nblk,
+                                                         int stride, int n, double* __restrict__ seg) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  const int k0 = (int)((long)blockIdx.y * nblk / kRedSeg), k1 = (int)((long)(blockIdx.y + 1) * nblk / kRedSeg);
+  double s = 0.0;
+  for (int k = k0; k < k1; ++k) s += part[(size_t)k * stride + e];
+  seg[(size_t)blockIdx.y * n + e] = s;
+}
+
+__global__ void __launch_bounds__(256) seg_final_kernel(const double* __restrict__ seg, int n_src, int cz,
+                                                        int cin, int n, int nw, double* __restrict__ gw,
+                                                        double* __restrict__ gb) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  int src = e;
+  if (cz > 0) {   // wgrad layout
+    const int cinp = 16 * ((cin + 15) / 16);
     if (e < cz * cin * 9) {
       const int tap = e % 9, ci = (e / 9) % cin, z = e / (9 * cin);
-      src = ((size_t)z * cinp + ci) * 9 + tap;
+      src = (z * cinp + ci) * 9 + tap;
     } else {
-      src = (size_t)cz * cinp * 9 + (e - cz * cin * 9);
+      src = cz * cinp * 9 + (e - cz * cin * 9);
     }
-    double s = 0.0;
-    for (int k = 0; k < nblk; ++k) s += wpart[(size_t)k * kWgPartMax + src];
-    if (e < cz * cin * 9)
-      gw[e] += s;
-    else
-      gb[e - cz * cin * 9] += s;
   }
+  double s = 0.0;
+  for (int k = 0; k < kRedSeg; ++k) s += seg[(size_t)k * n_src + src];
+  if (e < nw)
+    gw[e] += s;
+  else
+    gb[e - nw] += s;
+}
+
+static hipError_t reduce_partials(const float* part, int nblk, int stride, int n_src, int cz, int cin, int n,
+                                  int nw, double* rseg, double* gw, double* gb, hipStream_t s) {
+  hipLaunchKernelGGL(seg_reduce_kernel, dim3((n_src + 255) / 256, kRedSeg), dim3(256), 0, s, part, nblk,
+                     stride, n_src, rseg);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(seg_final_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rseg, n_src, cz, cin, n, nw,
+                     gw, gb);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 // deconv_j weight / bias gradient over a group: gW[ci][co][ky][kx] = sum_{d, iy, ix}
-// h[iy][ix][ci] gu[2iy-1+ky][2ix-1+kx][co], gb[co] = sum gu.  Thread t owns 9 of the 2304
-// (ci, co, tap) entries; blocks stride over 64-pixel runs of the coarse image (per plane), with
-// the run's h and its gu rows staged in LDS; one partial per block (2304 + 16 floats).
+// h[iy][ix][ci] gu[2iy-1+ky][2ix-1+kx][co], gb[co] = sum gu.  Per tap a 16 x 16 GEMM over the
+// pixels on v_mfma_f32_16x16x4_f32 (fp32 operands: the products are exact as in the
+// reference's fp32 conv): A = h^T (16 ci x 4 px), B = gu at the tap (4 px x 16 co).  Blocks
+// stride over 64-pixel runs of the coarse image (per plane), with the run's h and its gu rows
+// staged in LDS; wave w owns taps w, w + 4, w + 8; one partial per block (2304 + 16 floats).
 // ---------------------------------------------------------------------------
+constexpr int kDcwBlocks = 1024, kDcwPart = 2320;
 struct DcwArgs {
   const float* h;       // coarse input plane 0 (record state slab of d0 + 1: h' of the
   size_t hstride;       //   deconv's source cell), + k * hstride
   const float* gu;      // [G][B][Ho][Wo][16]
   int nplanes, B, Hi, Wi;
-  float* wpart;
+  float* wpart;         // [gridDim.x][kDcwPart]
 };
 
 __global__ void __launch_bounds__(256) deconv_wgrad_kernel(DcwArgs a) {
   __shared__ float hs[64][17];
   __shared__ float gs[3][130][17];   // fine rows 2y-1 .. 2y+1, cols 2x0-1 .. 2x0+128
-  const int tid = threadIdx.x;
+  __shared__ float bred[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Ho = 2 * a.Hi, Wo = 2 * a.Wi;
   const int runs_x = (a.Wi + 63) / 64;
   const int nrun = a.nplanes * a.B * a.Hi * runs_x;
-  float acc[9];
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 acc[3];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) acc[i] = 0.f;
+  for (int i = 0; i < 3; ++i) acc[i] = f4{0.f, 0.f, 0.f, 0.f};
   float bacc = 0.f;
-  // entry e = tid + 256 i: (ci, co, tap) = (e / 144, (e / 9) % 16, e % 9)
+  const int m = lane & 15, kq = lane >> 4;
 #pragma unroll 1
   for (int run = blockIdx.x; run < nrun; run += gridDim.x) {
     int t = run;
@@ -844,40 +995,39 @@ __global__ void __launch_bounds__(256) deconv_wgrad_kernel(DcwArgs a) {
       gs[rr][cc][c] = (oy >= 0 && oy < Ho && ox >= 0 && ox < Wo) ? gp[((size_t)oy * Wo + ox) * 16 + c] : 0.f;
     }
     __syncthreads();
-    const int npx = min(64, a.Wi - x0);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int e = tid + 256 * i;
-      const int ci = e / 144, co = (e / 9) % 16, tap = e % 9, dy = tap / 3, dx = tap % 3;
-      float s = acc[i];
-      for (int px = 0; px < npx; ++px) s = fmaf(hs[px][ci], gs[dy][2 * px + dx][co], s);
-      acc[i] = s;
+    for (int i = 0; i < 3; ++i) {
+      const int tap = wave + 4 * i;
+      if (tap < 9) {
+        const int dy = tap / 3, dx = tap % 3;
+#pragma unroll 4
+        for (int p0 = 0; p0 < 64; p0 += 4) {
+          const int px = p0 + kq;
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(hs[px][m], gs[dy][2 * px + dx][m], acc[i], 0, 0, 0);
+        }
+      }
     }
-    if (tid < 16) {   // bias: each fine pixel of the run's owned quads once
+    if (tid < 64) {   // bias: each fine pixel of the run's owned quads once; lane phase tid >> 4
+      const int co = tid & 15, ph = tid >> 4;
+      const int npx = min(64, a.Wi - x0);
       float s = 0.f;
-      for (int px = 0; px < npx; ++px)
-        s += gs[1][2 * px + 1][tid] + gs[1][2 * px + 2][tid] + gs[2][2 * px + 1][tid] + gs[2][2 * px + 2][tid];
+      for (int px = ph; px < npx; px += 4)
+        s += gs[1][2 * px + 1][co] + gs[1][2 * px + 2][co] + gs[2][2 * px + 1][co] + gs[2][2 * px + 2][co];
       bacc += s;
     }
   }
-  float* wp = a.wpart + (size_t)blockIdx.x * kWgPartMax;
+  float* wp = a.wpart + (size_t)blockIdx.x * kDcwPart;
+  // D: row = ci = 4 (lane >> 4) + r, col = co = lane & 15; entry (ci * 16 + co) * 9 + tap
 #pragma unroll
-  for (int i = 0; i < 9; ++i) wp[tid + 256 * i] = acc[i];
-  if (tid < 16) wp[2304 + tid] = bacc;
-}
-
-// partials -> gacc: raw ConvTranspose2d layout [ci][co][3][3] (entry order e = (ci*16+co)*9+tap)
-__global__ void __launch_bounds__(256) small_reduce_kernel(const float* __restrict__ wpart, int nblk,
-                                                           int n, int nw, double* __restrict__ gw,
-                                                           double* __restrict__ gb) {
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
-    double s = 0.0;
-    for (int k = 0; k < nblk; ++k) s += wpart[(size_t)k * kWgPartMax + e];
-    if (e < nw)
-      gw[e] += s;
-    else
-      gb[e - nw] += s;
+  for (int i = 0; i < 3; ++i) {
+    const int tap = wave + 4 * i;
+    if (tap < 9)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) wp[((4 * kq + r) * 16 + m) * 9 + tap] = acc[i][r];
   }
+  if (tid < 64) bred[tid] = bacc;
+  __syncthreads();
+  if (tid < 16) wp[2304 + tid] = (bred[tid] + bred[16 + tid]) + (bred[32 + tid] + bred[48 + tid]);
 }
 
 // conv_0 (head) weight / bias gradient over a group: gW[ci][tap] = sum gcost[p] h4[p + off][ci],
@@ -963,24 +1113,50 @@ static hipError_t run_dgrad(const DgradArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int CZ>
-static hipError_t run_wgrad(const WgradArgs& a, double* gw, double* gb, hipStream_t s) {
-  const int chunks = (a.cin + 15) / 16;
-  constexpr size_t lds = 2 * (size_t)CZ * kWgTH * kWgTW * 2 + 2 * 3 * 16 * (kWgTH + 2) * kWgTW * 2 +
-                         256 * 8 * 4;
+// the 16-channel input chunks of a cell conv's parts
+static void fill_chunks(WgradArgs& a) {
+  int c = 0;
+  for (int pi = 0; pi < a.nparts; ++pi) {
+    const WgPart& p = a.part[pi];
+    for (int lc = 0; lc < p.nch && c < 3; lc += 16, ++c) {
+      WgChunk& ch = a.chunk[c];
+      ch.ptr = p.ptr + lc;
+      ch.dstride = p.dstride;
+      ch.nch = p.nch;
+      ch.mode = p.mode;
+      ch.nv = std::min(16, p.nch - lc);
+      ch.j = p.j;
+      ch.stats = p.stats;
+      ch.sstride = p.sstride;
+      ch.gamma = p.gamma ? p.gamma + lc : nullptr;
+      ch.beta = p.beta ? p.beta + lc : nullptr;
+      ch.gn0 = lc / 8;
+      ch.scale = p.scale;
+      ch.bound = p.bound;
+    }
+  }
+}
+
+template <int CZ, int NCH>
+static hipError_t run_wgrad(WgradArgs a, double* gw, double* gb, hipStream_t s) {
+  fill_chunks(a);
+  a.gn_chunk = -1;
+  for (int c = 0; c < NCH; ++c)
+    if (a.chunk[c].mode == WG_GNRELU) a.gn_chunk = c;
+  const size_t lds = wgrad2_lds<CZ, NCH>() + (size_t)kPlaneGroup * a.B * 2 * sizeof(float2);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)wgrad_kernel<CZ>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)wgrad2_kernel<CZ, NCH>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(wgrad_kernel<CZ>, dim3(kWgBlocks, chunks), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((wgrad2_kernel<CZ, NCH>), dim3(kWgBlocks), dim3(512), lds, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // the chunks write disjoint entries of the same per-block partials
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(64), dim3(256), 0, s, a.wpart, kWgBlocks, CZ, a.cin, gw, gb);
-  return hipGetLastError();
+  return reduce_partials(a.wpart, kWgBlocks, (int)kWgPartMax, CZ * 16 * NCH * 9 + CZ, CZ, a.cin,
+                         CZ * a.cin * 9 + CZ, CZ * a.cin * 9, a.rseg, gw, gb, s);
 }
 
 }  // namespace aarmvs
@@ -1142,6 +1318,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       a.H = H / res_div[k];
       a.W = W / res_div[k];
       a.wpart = L.wpart;
+      a.rseg = L.rseg;
       const size_t S = T.state_slab;
       switch (k) {
         case 0:
@@ -1175,7 +1352,11 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       }
       double* gw = L.gacc + PL.raw_off[P_C0W + 2 * k];
       double* gb = L.gacc + PL.raw_off[P_C0B + 2 * k];
-      CK(kCellHid[k] == 16 ? run_wgrad<64>(a, gw, gb, s) : run_wgrad<32>(a, gw, gb, s));
+      const int nch = (a.cin + 15) / 16;
+      const hipError_t we = kCellHid[k] == 8 ? run_wgrad<32, 3>(a, gw, gb, s)
+                            : nch == 3     ? run_wgrad<64, 3>(a, gw, gb, s)
+                                           : run_wgrad<64, 2>(a, gw, gb, s);
+      CK(we);
     }
     for (int j = 0; j < 2; ++j) {
       DcwArgs a{};
@@ -1187,11 +1368,10 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       a.Hi = j ? H / 2 : H / 4;
       a.Wi = j ? W / 2 : W / 4;
       a.wpart = L.wpart;
-      hipLaunchKernelGGL(deconv_wgrad_kernel, dim3(kWgBlocks), dim3(256), 0, s, a);
+      hipLaunchKernelGGL(deconv_wgrad_kernel, dim3(kDcwBlocks), dim3(256), 0, s, a);
       CK(hipGetLastError());
-      hipLaunchKernelGGL(small_reduce_kernel, dim3(10), dim3(256), 0, s, L.wpart, kWgBlocks, 2320, 2304,
-                         L.gacc + PL.raw_off[j ? P_D1W : P_D0W], L.gacc + PL.raw_off[j ? P_D1B : P_D0B]);
-      CK(hipGetLastError());
+      CK(reduce_partials(L.wpart, kDcwBlocks, kDcwPart, 2320, 0, 0, 2320, 2304, L.rseg,
+                         L.gacc + PL.raw_off[j ? P_D1W : P_D0W], L.gacc + PL.raw_off[j ? P_D1B : P_D0B], s));
     }
     {
       HwArgs a{};
@@ -1207,9 +1387,8 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       a.wpart = L.wpart;
       hipLaunchKernelGGL(head_wgrad_kernel, dim3(kWgBlocks), dim3(256), 0, s, a);
       CK(hipGetLastError());
-      hipLaunchKernelGGL(small_reduce_kernel, dim3(1), dim3(256), 0, s, L.wpart, kWgBlocks, 73, 72,
-                         L.gacc + PL.raw_off[P_HW], L.gacc + PL.raw_off[P_HB]);
-      CK(hipGetLastError());
+      CK(reduce_partials(L.wpart, kWgBlocks, (int)kWgPartMax, 73, 0, 0, 73, 72, L.rseg,
+                         L.gacc + PL.raw_off[P_HW], L.gacc + PL.raw_off[P_HB], s));
     }
     if (r.grad_x)
       CK(hipMemcpyAsync(r.grad_x + (size_t)g0 * xs, L.gx, (size_t)n * xs * 4, hipMemcpyDeviceToDevice, s));

@@ -117,10 +117,20 @@ struct GnStat {
   float mean, rstd;
 };
 __device__ __forceinline__ GnStat stat_read(const double* stat, double n) {
+  // slots summed in index order; the loads are issued 16 slots at a time (two round trips)
+  static_assert(kSlots % 16 == 0, "slot batches");
+  const double2* p = reinterpret_cast<const double2*>(stat);
   double s = 0.0, ss = 0.0;
-  for (int i = 0; i < kSlots; ++i) {
-    s += stat[2 * i];
-    ss += stat[2 * i + 1];
+#pragma unroll
+  for (int h = 0; h < kSlots; h += 16) {
+    double2 v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = p[h + i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s += v[i].x;
+      ss += v[i].y;
+    }
   }
   const double mean = s / n;
   double var = ss / n - mean * mean;
