@@ -1182,15 +1182,6 @@ hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t
 namespace aarmvs {
 
 // omega chain of one (pixel, view) with its intermediates (omega_weight's operations)
-// DPP within a 16-lane row: the value of lane x - 1 (row_shr:1) / x + 1 (row_shl:1); 0 at the
-// row's edge
-__device__ __forceinline__ int dpp_row_from_left(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
-}
-__device__ __forceinline__ int dpp_row_from_right(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xF, 0xF, false);
-}
-
 struct OmegaChain {
   float t[4], v1[4], aa[4], t2[4], v2[4], bb[4], t3[4], g3[4], s3[4], w;
 };
@@ -1426,13 +1417,20 @@ __global__ void __launch_bounds__(256) cbw_param_kernel(const double* __restrict
 //   dL/dsq = -(1 + w)/nsrc dL/dx + conv3x3^T(dL/dt1)   (this chunk's 8 channels)
 //   dL/dwarp = 2 (warp - ref) dL/dsq;  dL/dref -= dL/dwarp (per view, summed in view order by
 //   cost_bwd_end: one writer per (view, pixel, channel));
-//   dL/dsrc: bilinear scatter of dL/dwarp into an LDS box covering the tile's taps over the
-//   group's planes (corner positions bound them: the plane homography and the position along a
-//   depth ray are monotone while z > 0), flushed once with global atomics; taps outside the
-//   box (or a box that does not fit) use global atomics directly;
+//   dL/dsrc: grid_sample's bilinear scatter of dL/dwarp, done as a gather.  The source box (the
+//   bounding box of the tile's taps over the group's planes: corner positions bound them, the
+//   plane homography and the position along a depth ray being monotone while z > 0) is owned
+//   pixel by pixel by the block's threads, which accumulate in registers over the planes.  Per
+//   plane every reference pixel files its index under the box cell of its top-left tap (one
+//   integer LDS atomic for the slot); each owned source pixel then reads the cells of its four
+//   possible top-left taps and adds wt[corner] * dL/dwarp of the pixels filed there.  After the
+//   group the owned pixels are flushed with global atomics (neighbouring tiles' boxes overlap).
+//   A cell with more than kFbSlots pixels, a tap outside the box, or a box that does not fit
+//   (kFbOwn pixels per thread) uses global atomics directly.  (The LDS box of float atomics this
+//   replaces took half of the kernel: 32 ds_add_f32 per pixel and plane.)
 //   gW0[co][c][tap] = sum_q dL/dt1[q - off(tap)][co] sq[q][c]: thread t < 216 owns (channel,
 //   tap) pair t % 72 of the chunk and a third of the tile's pixels, summed in order at the end.
-constexpr int kFbT = 16, kFbBoxPx = 1024;
+constexpr int kFbT = 16, kFbOwn = 3, kFbBoxPx = kFbOwn * 256, kFbCells = 1280, kFbSlots = 2;
 struct CbfArgs {
   PipeArgs p;
   const float* gx;          // [n][B][HW][32]
@@ -1446,12 +1444,20 @@ struct CbfArgs {
 #ifndef AARMVS_CBF_MINB
 #define AARMVS_CBF_MINB 2
 #endif
+// diagnostic builds only (tools/cbf_ab.sh): 1 no weight-gradient loop, 2 no scatter, 4 no source
+// gathers, 8 no box flush, 16 no conv3x3^T; the library is built with 0
+#ifndef AARMVS_CBF_ABL
+#define AARMVS_CBF_ABL 0
+#endif
 __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs a, const float* __restrict__ P,
                                                        const float* __restrict__ Rel) {
   __shared__ float4 w0q[9][8];                    // this chunk's conv3x3 weights [tap][c] (co in .xyzw)
   __shared__ float4 gts[18 * 18];                 // dL/dt1 of the haloed tile (one plane)
   __shared__ float sqs[256][9];                   // the tile's sq (8 channels, padded)
-  __shared__ __attribute__((aligned(16))) float box[kFbBoxPx * 8];
+  __shared__ int cnt[kFbCells];                   // pixels filed per top-left-tap cell (one plane)
+  __shared__ unsigned short lst[kFbCells][kFbSlots];   // their tile indices
+  __shared__ float4 gwim[256][2];                 // dL/dwarp of the tile's pixels (8 channels)
+  __shared__ float4 wtim[256];                    // their bilinear weights
   __shared__ float wsum[72][3][4];
   __shared__ GnStat gsk[kPlaneGroup][3];
   __shared__ int bred[4][4];
@@ -1509,9 +1515,28 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
     }
   }
   const Box bxr = box_reduce<4>(bx0, by0, bx1, by1, bred);
-  const bool use_box = !bad && bxr.nx > 0 && bxr.ny > 0 && bxr.nx * bxr.ny <= kFbBoxPx;
+  // cells: top-left tap positions x0 - 1 .. x0 + nx - 1 (and likewise in y), row stride cw
+  const int cw = bxr.nx + 1;
+  const bool use_box = !bad && bxr.nx > 0 && bxr.ny > 0 && bxr.nx * bxr.ny <= kFbBoxPx &&
+                       cw * (bxr.ny + 1) <= kFbCells;
   if (use_box)
-    for (int i = tid; i < bxr.nx * bxr.ny * 8; i += 256) box[(i & 7) * kFbBoxPx + (i >> 3)] = 0.f;
+    for (int i = tid; i < cw * (bxr.ny + 1); i += 256) cnt[i] = 0;
+  float own[kFbOwn][8];   // owned source-box pixels tid + 256 j: dL/dsrc over the group's planes
+#pragma unroll
+  for (int j = 0; j < kFbOwn; ++j)
+#pragma unroll
+    for (int ch = 0; ch < 8; ++ch) own[j][ch] = 0.f;
+  int mycell = -1;        // the cell this thread's pixel was filed under (reset next plane)
+  int obase[kFbOwn];      // cell of owned pixel j's own position (its corner-0 cell), or -1
+#pragma unroll
+  for (int j = 0; j < kFbOwn; ++j) {
+    const int i = tid + 256 * j;
+    obase[j] = -1;
+    if (use_box && i < bxr.nx * bxr.ny) {
+      const int ry = i / bxr.nx, rx = i - ry * bxr.nx;
+      obase[j] = (ry + 1) * cw + rx + 1;
+    }
+  }
   const float* gxb = a.gx + 8 * c;
   // software pipeline: the global operands of plane k + 1 (dL/dt1 halo, t1, dL/dx, the source
   // gathers) are loaded while plane k is computed
@@ -1537,6 +1562,10 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
       const TapP t = tap_p(ntf, true, H, W, false, none, fbytes / 32u);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        if (AARMVS_CBF_ABL & 4) {
+          ns[q][0] = ns[q][1] = make_float4(ntf.wt[0], ntf.wt[1], (float)t.pix[q], 0.f);
+          continue;
+        }
         ns[q][0] = ld_c8(rsrc, t.pix[q], 2 * c, HW);
         ns[q][1] = ld_c8(rsrc, t.pix[q], 2 * c + 1, HW);
       }
@@ -1545,9 +1574,11 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
   fetch(0);
 #pragma unroll 1
   for (int k = 0; k < a.n; ++k) {
-    __syncthreads();   // box zeroed / previous plane's LDS reads done
+    __syncthreads();   // cells zeroed / previous plane's LDS reads done
     gts[hi0] = nh0;
     if (hi1 < 18 * 18) gts[hi1] = nh1;
+    if (mycell >= 0) cnt[mycell] = 0;
+    mycell = -1;
     __syncthreads();
     const float4 t1v = nt1, gx0 = ngx0, gx1 = ngx1;
     const TapF tf = ntf;
@@ -1578,7 +1609,7 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
 #pragma unroll
       for (int j = 0; j < 8; ++j) gsq[j] = dsc * gxv[j];
 #pragma unroll 3
-      for (int tap = 0; tap < 9; ++tap) {
+      for (int tap = 0; tap < ((AARMVS_CBF_ABL & 16) ? 1 : 9); ++tap) {
         const float4 gt = gts[(ly + 2 - tap / 3) * 18 + lx + 2 - tap % 3];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -1595,55 +1626,41 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
         gref[j] -= gw[j];
       }
     }
-    // bilinear scatter of dL/dwarp into the source view (grid_sample backward).  Pairs along a
-    // tile row whose taps are horizontally adjacent (corner 1, 3 of pixel x = corner 0, 2 of
-    // pixel x + 1: the usual case) are merged first (DPP within the 16-lane row): one atomic
-    // per shared source pixel instead of two.
-    {
-      const bool fin = in && tf.xf == tf.xf && tf.yf == tf.yf;
-      const int kx = fin ? (int)fminf(fmaxf(tf.xf, -8.f), (float)W + 8.f) : -100;
-      const int ky = fin ? (int)fminf(fmaxf(tf.yf, -8.f), (float)H + 8.f) : -100;
-      const int lkx = dpp_row_from_left(kx), lky = dpp_row_from_left(ky);
-      const int rkx = dpp_row_from_right(kx), rky = dpp_row_from_right(ky);
-      const bool take = lx > 0 && lkx + 1 == kx && lky == ky;
-      const bool give = lx < 15 && rkx == kx + 1 && rky == ky;
-      float c0[8], c2[8], c1[8], c3[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float r1 = __int_as_float(dpp_row_from_left(__float_as_int(tf.wt[1] * gw[j])));
-        const float r3 = __int_as_float(dpp_row_from_left(__float_as_int(tf.wt[3] * gw[j])));
-        c0[j] = take ? tf.wt[0] * gw[j] + r1 : tf.wt[0] * gw[j];
-        c2[j] = take ? tf.wt[2] * gw[j] + r3 : tf.wt[2] * gw[j];
-        c1[j] = tf.wt[1] * gw[j];
-        c3[j] = tf.wt[3] * gw[j];
-      }
-      if (in) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if ((q & 1) && give) continue;   // handed to the right neighbour
-          const float xf = tf.xf + (float)(q & 1), yf = tf.yf + (float)(q >> 1);
-          const bool ok = (xf > -1.0f) && (xf < (float)W) && (yf > -1.0f) && (yf < (float)H);
-          if (!ok) continue;
-          const int xi = (int)xf, yi = (int)yf;
-          float cv[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) cv[j] = q == 0 ? c0[j] : q == 1 ? c1[j] : q == 2 ? c2[j] : c3[j];
-          if (use_box && xi >= bxr.x0 && xi < bxr.x0 + bxr.nx && yi >= bxr.y0 && yi < bxr.y0 + bxr.ny) {
-            float* bp = box + (yi - bxr.y0) * bxr.nx + (xi - bxr.x0);   // channel planes
-#pragma unroll
-            for (int j = 0; j < 8; ++j) atomicAdd(bp + j * kFbBoxPx, cv[j]);
-          } else {
-            float* gp = a.gsrc8 + ((((size_t)v * pa.B + b) * 4 + c) * HW + (size_t)yi * W + xi) * 8;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) atomicAdd(gp + j, cv[j]);
-          }
+    // grid_sample backward: file the pixel under its top-left tap's cell for the gather below;
+    // taps that are not gathered (in-image corners outside the box, every corner of a pixel not
+    // filed) are scattered with global atomics here
+    if (in && !(AARMVS_CBF_ABL & 2) && tf.xf == tf.xf && tf.yf == tf.yf) {
+      const int kx = (int)fminf(fmaxf(tf.xf, -8.f), (float)W + 8.f);
+      const int ky = (int)fminf(fmaxf(tf.yf, -8.f), (float)H + 8.f);
+      const int cx = kx - bxr.x0 + 1, cy = ky - bxr.y0 + 1;
+      bool filed = false;
+      if (use_box && cx >= 0 && cx < cw && cy >= 0 && cy <= bxr.ny) {
+        const int cell = cy * cw + cx;
+        const int slot = atomicAdd(&cnt[cell], 1);
+        mycell = cell;
+        if (slot < kFbSlots) {
+          lst[cell][slot] = (unsigned short)tid;
+          gwim[tid][0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
+          gwim[tid][1] = make_float4(gw[4], gw[5], gw[6], gw[7]);
+          wtim[tid] = make_float4(tf.wt[0], tf.wt[1], tf.wt[2], tf.wt[3]);
+          filed = true;
         }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int xi = kx + (q & 1), yi = ky + (q >> 1);
+        if (xi < 0 || xi >= W || yi < 0 || yi >= H) continue;   // zero padding
+        const bool inbox = xi >= bxr.x0 && xi < bxr.x0 + bxr.nx && yi >= bxr.y0 && yi < bxr.y0 + bxr.ny;
+        if (filed && inbox) continue;
+        float* gp = a.gsrc8 + ((((size_t)v * pa.B + b) * 4 + c) * HW + (size_t)yi * W + xi) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomicAdd(gp + j, tf.wt[q] * gw[j]);
       }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) sqs[tid][j] = sqv[j];
     __syncthreads();
-    if (tid < 216) {
+    if (tid < 216 && !(AARMVS_CBF_ABL & 1)) {
       const int dy = ptap / 3, dx = ptap % 3;
 #pragma unroll 6
       for (int qq = q0; qq < q1; ++qq) {
@@ -1653,6 +1670,32 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
         wacc[1] = fmaf(gt.y, sv, wacc[1]);
         wacc[2] = fmaf(gt.z, sv, wacc[2]);
         wacc[3] = fmaf(gt.w, sv, wacc[3]);
+      }
+    }
+    // the gather: owned source pixel s takes corner q of the pixels filed under cell s - q
+    if (use_box && !(AARMVS_CBF_ABL & 2)) {
+#pragma unroll
+      for (int j = 0; j < kFbOwn; ++j) {
+        if (obase[j] < 0) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cell = obase[j] - (q >> 1) * cw - (q & 1);
+          const int n = min(cnt[cell], kFbSlots);
+          for (int sl = 0; sl < n; ++sl) {
+            const int pp = lst[cell][sl];
+            const float4 wq = wtim[pp];
+            const float w = q == 0 ? wq.x : q == 1 ? wq.y : q == 2 ? wq.z : wq.w;
+            const float4 g0 = gwim[pp][0], g1 = gwim[pp][1];
+            own[j][0] += w * g0.x;
+            own[j][1] += w * g0.y;
+            own[j][2] += w * g0.z;
+            own[j][3] += w * g0.w;
+            own[j][4] += w * g1.x;
+            own[j][5] += w * g1.y;
+            own[j][6] += w * g1.z;
+            own[j][7] += w * g1.w;
+          }
+        }
       }
     }
   }
@@ -1666,12 +1709,16 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
     for (int co = 0; co < 4; ++co) wsum[pair][sub][co] = wacc[co];
   }
   __syncthreads();
-  if (use_box) {   // flush the box: 8 contiguous channels per source pixel
+  if (use_box && !(AARMVS_CBF_ABL & 8)) {   // flush the owned box pixels (8 channels each)
     float* gb = a.gsrc8 + (((size_t)v * pa.B + b) * 4 + c) * HW * 8;
-    for (int i = tid; i < bxr.nx * bxr.ny * 8; i += 256) {
-      const int px = i >> 3, j = i & 7, ry = px / bxr.nx, rx = px % bxr.nx;
-      const float val = box[j * kFbBoxPx + px];
-      if (val != 0.f) atomicAdd(gb + ((size_t)(bxr.y0 + ry) * W + bxr.x0 + rx) * 8 + j, val);
+#pragma unroll
+    for (int j = 0; j < kFbOwn; ++j) {
+      if (obase[j] < 0) continue;
+      const int i = tid + 256 * j, ry = i / bxr.nx, rx = i - ry * bxr.nx;
+      float* gp = gb + ((size_t)(bxr.y0 + ry) * W + bxr.x0 + rx) * 8;
+#pragma unroll
+      for (int ch = 0; ch < 8; ++ch)
+        if (own[j][ch] != 0.f) atomicAdd(gp + ch, own[j][ch]);
     }
   }
   const size_t blk = (((size_t)c * nsrc + v) * pa.B + b) * gridDim.x + blockIdx.x;
