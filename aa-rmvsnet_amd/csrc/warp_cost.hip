@@ -1428,9 +1428,17 @@ __global__ void __launch_bounds__(256) cbw_param_kernel(const double* __restrict
 //   A cell with more than kFbSlots pixels, a tap outside the box, or a box that does not fit
 //   (kFbOwn pixels per thread) uses global atomics directly.  (The LDS box of float atomics this
 //   replaces took half of the kernel: 32 ds_add_f32 per pixel and plane.)
-//   gW0[co][c][tap] = sum_q dL/dt1[q - off(tap)][co] sq[q][c]: thread t < 216 owns (channel,
-//   tap) pair t % 72 of the chunk and a third of the tile's pixels, summed in order at the end.
+//   gW0[co][c][tap] = sum_q dL/dt1[q - off(tap)][co] sq[q][c]: thread t < 252 owns (half of the
+//   chunk's channels, tap) pair t % 18 for all four co (16 sums: one float4 read of sq and one of
+//   dL/dt1 per 16 FMAs) over the tile pixels q = t / 18 + 14 i; the 14 pixel subsets are summed in
+//   order at the end.
 constexpr int kFbT = 16, kFbOwn = 3, kFbBoxPx = kFbOwn * 256, kFbCells = 1280, kFbSlots = 2;
+constexpr int kWgPairs = 18, kWgSubs = 14;
+// LDS scratch of the plane loop (gather cells, filed dL/dwarp and weights), reused after the
+// loop for the weight-gradient subset sums
+constexpr int kFbGwOff = 0, kFbWtOff = 256 * 32, kFbCntOff = kFbWtOff + 256 * 16,
+              kFbLstOff = kFbCntOff + kFbCells * 4, kFbScratch = kFbLstOff + kFbCells * kFbSlots * 2;
+static_assert(kFbScratch >= kWgPairs * kWgSubs * 16 * 4, "subset sums fit the scratch");
 struct CbfArgs {
   PipeArgs p;
   const float* gx;          // [n][B][HW][32]
@@ -1453,12 +1461,14 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
                                                        const float* __restrict__ Rel) {
   __shared__ float4 w0q[9][8];                    // this chunk's conv3x3 weights [tap][c] (co in .xyzw)
   __shared__ float4 gts[18 * 18];                 // dL/dt1 of the haloed tile (one plane)
-  __shared__ float sqs[256][9];                   // the tile's sq (8 channels, padded)
-  __shared__ int cnt[kFbCells];                   // pixels filed per top-left-tap cell (one plane)
-  __shared__ unsigned short lst[kFbCells][kFbSlots];   // their tile indices
-  __shared__ float4 gwim[256][2];                 // dL/dwarp of the tile's pixels (8 channels)
-  __shared__ float4 wtim[256];                    // their bilinear weights
-  __shared__ float wsum[72][3][4];
+  __shared__ float4 sq4[256][2];                  // the tile's sq (8 channels)
+  __shared__ __attribute__((aligned(16))) char fbs[kFbScratch];
+  float4 (*const gwim)[2] = reinterpret_cast<float4 (*)[2]>(fbs + kFbGwOff);   // dL/dwarp (8 ch)
+  float4* const wtim = reinterpret_cast<float4*>(fbs + kFbWtOff);              // bilinear weights
+  int* const cnt = reinterpret_cast<int*>(fbs + kFbCntOff);   // pixels filed per top-left-tap cell
+  unsigned short (*const lst)[kFbSlots] =
+      reinterpret_cast<unsigned short (*)[kFbSlots]>(fbs + kFbLstOff);         // their tile indices
+  float (*const wsum)[kWgSubs][16] = reinterpret_cast<float (*)[kWgSubs][16]>(fbs);   // after the loop
   __shared__ GnStat gsk[kPlaneGroup][3];
   __shared__ int bred[4][4];
   __shared__ int bad;
@@ -1488,11 +1498,12 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
   const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(pa.ref + (size_t)b * kC * HW, fbytes);
   const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(pa.src[v] + (size_t)b * kC * HW, fbytes);
   const float* m = Rel + 12 * (v * pa.B + b);
-  const int pair = tid % 72, sub = tid / 72;   // weight-gradient role (tid < 216)
-  const int pch = pair / 9, ptap = pair % 9;
-  const int q0 = sub * 86, q1 = min(256, q0 + 86);
+  const int pair = tid % kWgPairs, sub = tid / kWgPairs;   // weight-gradient role (tid < 252)
+  const int pcg = pair / 9, ptap = pair % 9;
   float gref[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float wacc[4] = {0.f, 0.f, 0.f, 0.f};
+  float wacc[16];   // [co][4 channels of half pcg]
+#pragma unroll
+  for (int i = 0; i < 16; ++i) wacc[i] = 0.f;
   const float4 rf0 = in ? ld_c8(rref, (uint32_t)p, 2 * c, HW) : make_float4(0.f, 0.f, 0.f, 0.f);
   const float4 rf1 = in ? ld_c8(rref, (uint32_t)p, 2 * c + 1, HW) : make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
@@ -1657,19 +1668,20 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
         for (int j = 0; j < 8; ++j) atomicAdd(gp + j, tf.wt[q] * gw[j]);
       }
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sqs[tid][j] = sqv[j];
+    sq4[tid][0] = make_float4(sqv[0], sqv[1], sqv[2], sqv[3]);
+    sq4[tid][1] = make_float4(sqv[4], sqv[5], sqv[6], sqv[7]);
     __syncthreads();
-    if (tid < 216 && !(AARMVS_CBF_ABL & 1)) {
+    if (tid < kWgPairs * kWgSubs && !(AARMVS_CBF_ABL & 1)) {
       const int dy = ptap / 3, dx = ptap % 3;
-#pragma unroll 6
-      for (int qq = q0; qq < q1; ++qq) {
-        const float sv = sqs[qq][pch];
+#pragma unroll 4
+      for (int qq = sub; qq < 256; qq += kWgSubs) {
+        const float4 sv = sq4[qq][pcg];
         const float4 gt = gts[((qq >> 4) + 2 - dy) * 18 + (qq & 15) + 2 - dx];
-        wacc[0] = fmaf(gt.x, sv, wacc[0]);
-        wacc[1] = fmaf(gt.y, sv, wacc[1]);
-        wacc[2] = fmaf(gt.z, sv, wacc[2]);
-        wacc[3] = fmaf(gt.w, sv, wacc[3]);
+        const float g4[4] = {gt.x, gt.y, gt.z, gt.w}, s4[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+        for (int co = 0; co < 4; ++co)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) wacc[co * 4 + j] = fmaf(g4[co], s4[j], wacc[co * 4 + j]);
       }
     }
     // the gather: owned source pixel s takes corner q of the pixels filed under cell s - q
@@ -1704,9 +1716,10 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
 #pragma unroll
     for (int j = 0; j < 8; ++j) gr[(size_t)(8 * c + j) * HW] += gref[j];
   }
-  if (tid < 216) {
+  __syncthreads();   // every gather of the last plane done: the scratch becomes the subset sums
+  if (tid < kWgPairs * kWgSubs) {
 #pragma unroll
-    for (int co = 0; co < 4; ++co) wsum[pair][sub][co] = wacc[co];
+    for (int i = 0; i < 16; ++i) wsum[pair][sub][i] = wacc[i];
   }
   __syncthreads();
   if (use_box && !(AARMVS_CBF_ABL & 8)) {   // flush the owned box pixels (8 channels each)
@@ -1725,8 +1738,11 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
   float* wp = a.wpart + blk * 288;
   for (int i = tid; i < 288; i += 256) {   // i = (co * 8 + j) * 9 + tap
     const int tap = i % 9, j = (i / 9) % 8, co = i / 72;
-    const float* ws3 = &wsum[j * 9 + tap][0][co];
-    wp[i] = (ws3[0] + ws3[4]) + ws3[8];
+    const int pr = (j >> 2) * 9 + tap, col = co * 4 + (j & 3);
+    float sum = wsum[pr][0][col];
+#pragma unroll
+    for (int k = 1; k < kWgSubs; ++k) sum += wsum[pr][k][col];
+    wp[i] = sum;
   }
 }
 
