@@ -269,10 +269,14 @@ constexpr int kDgTH = 8, kDgTW = 32, kDgW2 = kDgTW + 2, kDgNPIX = (kDgTH + 2) * 
 
 __device__ __forceinline__ int dg_pix(int p, int h) { return p * 32 + ((h ^ ((p >> 3) & 1)) << 4); }
 
+// Persistent: a block keeps its m-tile's fragments in LDS and walks the tiles (stride gridDim.x);
+// the next chunk's gz (this tile's, or the next tile's first) is loaded into registers while the
+// current chunk's MFMAs run.
 template <int CZ>
 __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
   constexpr int NCHK = CZ / 16;
   constexpr int AH = NCHK * 9 * 2 * 512;   // halves of this m-tile's fragments (hi and lo)
+  constexpr int NI = (2 * kDgNPIX + 511) / 512;   // staging items per thread
   extern __shared__ __attribute__((aligned(16))) char lds_dg[];
   char* wl = lds_dg;                        // [chunk][tap][hi, lo][64 lanes][8]
   char* in_hi = wl + AH * 2;
@@ -280,9 +284,9 @@ __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mt = blockIdx.y;
   const int tiles_x = (a.W + kDgTW - 1) / kDgTW, tiles_y = (a.H + kDgTH - 1) / kDgTH;
-  const int tile = blockIdx.x;
-  const int b = tile / (tiles_x * tiles_y), rem = tile % (tiles_x * tiles_y);
-  const int y0 = (rem / tiles_x) * kDgTH, x0 = (rem % tiles_x) * kDgTW;
+  const int ntiles = a.B * tiles_x * tiles_y;
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;   // whole block
   {
     const float4* s = reinterpret_cast<const float4*>(a.wfrag + (size_t)mt * (AH / 2));
     float4* d = reinterpret_cast<float4*>(wl);
@@ -291,71 +295,105 @@ __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
   const int ez = scale_exp(*a.zmax);
   const float zs = ldexpf(1.0f, -ez);
   const float inv = *a.wscale * ldexpf(1.0f, ez);
-  const float* gzb = a.gz + (size_t)b * a.H * a.W * CZ;
-  bfloatx16 acc;
+  auto coords = [&](int t, int& b, int& y0, int& x0) {
+    b = t / (tiles_x * tiles_y);
+    const int rem = t % (tiles_x * tiles_y);
+    y0 = (rem / tiles_x) * kDgTH;
+    x0 = (rem % tiles_x) * kDgTW;
+  };
+  float4 pv[NI][2];   // the prefetched chunk: item j = (half hh, haloed pixel p) of e = tid + 512 j
+  auto load = [&](int t, int c) {
+    int b, y0, x0;
+    coords(t, b, y0, x0);
+    const float* gzb = a.gz + (size_t)b * a.H * a.W * CZ;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-  const int col = lane & 31, h = lane >> 5;
-#pragma unroll 1
-  for (int c = 0; c < NCHK; ++c) {
-    __syncthreads();   // previous chunk's fragment reads done (fragments visible the first time)
-    for (int e = tid; e < 2 * kDgNPIX; e += 512) {
+    for (int j = 0; j < NI; ++j) {
+      const int e = tid + 512 * j;
       const int hh = e >= kDgNPIX ? 1 : 0, p = e - hh * kDgNPIX;
       const int row = p / kDgW2, cc = p - row * kDgW2;
       const int gy = y0 - 1 + row, gx = x0 - 1 + cc;
-      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+      pv[j][0] = pv[j][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < 2 * kDgNPIX && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
         const float4* s = reinterpret_cast<const float4*>(gzb + ((size_t)gy * a.W + gx) * CZ + 16 * c + 8 * hh);
-        const float4 q0 = s[0], q1 = s[1];
-        v[0] = q0.x; v[1] = q0.y; v[2] = q0.z; v[3] = q0.w;
-        v[4] = q1.x; v[5] = q1.y; v[6] = q1.z; v[7] = q1.w;
+        pv[j][0] = s[0];
+        pv[j][1] = s[1];
       }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int e = tid + 512 * j;
+      if (e >= 2 * kDgNPIX) continue;
+      const int hh = e >= kDgNPIX ? 1 : 0, p = e - hh * kDgNPIX;
+      const float v[8] = {pv[j][0].x, pv[j][0].y, pv[j][0].z, pv[j][0].w,
+                          pv[j][1].x, pv[j][1].y, pv[j][1].z, pv[j][1].w};
       bhalf8 hv, lv;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int k = 0; k < 8; ++k) {
         _Float16 hi, lo;
-        split16(v[j] * zs, hi, lo);
-        hv[j] = hi;
-        lv[j] = lo;
+        split16(v[k] * zs, hi, lo);
+        hv[k] = hi;
+        lv[k] = lo;
       }
       *reinterpret_cast<bhalf8*>(in_hi + dg_pix(p, hh)) = hv;
       *reinterpret_cast<bhalf8*>(in_lo + dg_pix(p, hh)) = lv;
     }
-    __syncthreads();
+  };
+  const int col = lane & 31, h = lane >> 5;
+  load(tile, 0);
+  for (; tile < ntiles; tile += gridDim.x) {
+    int b, y0, x0;
+    coords(tile, b, y0, x0);
+    const int next = tile + (int)gridDim.x;
+    bfloatx16 acc;
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int p = (wave + tap / 3) * kDgW2 + col + tap % 3;
-      const bhalf8 bh = *reinterpret_cast<const bhalf8*>(in_hi + dg_pix(p, h));
-      const bhalf8 bl = *reinterpret_cast<const bhalf8*>(in_lo + dg_pix(p, h));
-      const char* af = wl + (size_t)(((c * 9 + tap) * 2) * 512 + lane * 8) * 2;
-      const bhalf8 ah = *reinterpret_cast<const bhalf8*>(af);
-      const bhalf8 alo = *reinterpret_cast<const bhalf8*>(af + 512 * 2);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bh, acc, 0, 0, 0);
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll 1
+    for (int c = 0; c < NCHK; ++c) {
+      __syncthreads();   // previous chunk's fragment reads done (fragments visible the first time)
+      store();
+      __syncthreads();
+      if (c + 1 < NCHK)
+        load(tile, c + 1);
+      else if (next < ntiles)
+        load(next, 0);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int p = (wave + tap / 3) * kDgW2 + col + tap % 3;
+        const bhalf8 bh = *reinterpret_cast<const bhalf8*>(in_hi + dg_pix(p, h));
+        const bhalf8 bl = *reinterpret_cast<const bhalf8*>(in_lo + dg_pix(p, h));
+        const char* af = wl + (size_t)(((c * 9 + tap) * 2) * 512 + lane * 8) * 2;
+        const bhalf8 ah = *reinterpret_cast<const bhalf8*>(af);
+        const bhalf8 alo = *reinterpret_cast<const bhalf8*>(af + 512 * 2);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bh, acc, 0, 0, 0);
+      }
     }
-  }
-  const int y = y0 + wave, x = x0 + col;
-  if (y >= a.H || x >= a.W) return;
-  const size_t p = ((size_t)b * a.H + y) * a.W + x;
-  // D row m = 8 (j >> 2) + 4 h + (j & 3) -> output channel 32 mt + m
+    const int y = y0 + wave, x = x0 + col;
+    if (y < a.H && x < a.W) {
+      const size_t p = ((size_t)b * a.H + y) * a.W + x;
+      // D row m = 8 (j >> 2) + 4 h + (j & 3) -> output channel 32 mt + m
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int co = 32 * mt + 8 * g + 4 * h;
-    if (co >= a.cout) continue;
+      for (int g = 0; g < 4; ++g) {
+        const int co = 32 * mt + 8 * g + 4 * h;
+        if (co >= a.cout) continue;
 #pragma unroll
-    for (int pi = 0; pi < 3; ++pi) {
-      if (pi >= a.nparts) break;
-      const DgPart& pt = a.part[pi];
-      if (co >= pt.c0 && co < pt.c0 + pt.nch) {
-        float4* d = reinterpret_cast<float4*>(pt.dst + p * pt.nch + (co - pt.c0));
-        float4 v = make_float4(acc[4 * g] * inv, acc[4 * g + 1] * inv, acc[4 * g + 2] * inv,
-                               acc[4 * g + 3] * inv);
-        if (pt.add) {
-          const float4 o = *d;
-          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        for (int pi = 0; pi < 3; ++pi) {
+          if (pi >= a.nparts) break;
+          const DgPart& pt = a.part[pi];
+          if (co >= pt.c0 && co < pt.c0 + pt.nch) {
+            float4* d = reinterpret_cast<float4*>(pt.dst + p * pt.nch + (co - pt.c0));
+            float4 v = make_float4(acc[4 * g] * inv, acc[4 * g + 1] * inv, acc[4 * g + 2] * inv,
+                                   acc[4 * g + 3] * inv);
+            if (pt.add) {
+              const float4 o = *d;
+              v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+            }
+            *d = v;
+          }
         }
-        *d = v;
       }
     }
   }
@@ -1109,7 +1147,11 @@ static hipError_t run_dgrad(const DgradArgs& a, hipStream_t s) {
   }
   const int tiles = a.B * ((a.W + kDgTW - 1) / kDgTW) * ((a.H + kDgTH - 1) / kDgTH);
   const int mtn = (a.cout + 31) / 32;
-  hipLaunchKernelGGL(dgrad_kernel<CZ>, dim3(tiles, mtn), dim3(512), lds, s, a);
+  // persistent blocks: as many as the CUs hold (LDS-bound), split over the m-tiles
+  const int cu = cu_count();
+  const int per_cu = std::max(1, (int)((160 * 1024) / lds));
+  const int grid = std::max(1, std::min(tiles, std::max(1, cu * per_cu / mtn)));
+  hipLaunchKernelGGL(dgrad_kernel<CZ>, dim3(grid, mtn), dim3(512), lds, s, a);
   return hipGetLastError();
 }
 
