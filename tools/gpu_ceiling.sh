@@ -1,0 +1,20 @@
+#!/bin/bash
+# Ceiling analysis of the cost-slice kernels (rocprofv3 PMC passes, one counter set per run,
+# within the gfx950 per-block limits of MI355X_MICROARCH.md): one 16-plane group of the
+# headline sweep (tools/pmc_sweep.py).  Summary: python tools/ceiling_summary.py gpurun_out/ceil
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/ceil
+run() {  # run NAME counters...
+  local name=$1; shift
+  rm -rf gpurun_out/ceil/$name
+  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/ceil/$name -o p -- \
+    python3 tools/pmc_sweep.py --planes 16 > gpurun_out/ceil/$name.log 2>&1 || { echo "pass $name failed"; tail -3 gpurun_out/ceil/$name.log; exit 1; }
+  echo "pass $name ok"
+}
+run sq_time SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE
+run sq_mix SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
+run tex TA_BUSY_avr TA_TOTAL_WAVEFRONTS_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum GRBM_GUI_ACTIVE
+run l2 TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum TCC_EA0_RDREQ_sum
+run fetch FETCH_SIZE
+run write WRITE_SIZE
