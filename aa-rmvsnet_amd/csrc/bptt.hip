@@ -78,8 +78,7 @@ struct BpttLayout {
   float* gpool[2];     // dL/d maxpool(h0'), maxpool(h1') [B][H/2^(j+1)][.][16]
   float* gu[2];        // [G][B][Hu][Wu][16] dL/du_j (deconv outputs) of the group's planes
   float* gx;           // [G][B][H][W][32] dL/dx of the group's planes
-  double* gnb_part;    // [B][nblk][36] GroupNorm-backward partial sums
-  double* gnb_sum;     // [B][2 deconvs][2 groups][2]: (sum g xhat-grad, sum g xhat-grad xhat)
+  double* gnb_part[2]; // per deconv [G][B][nblk][36] GroupNorm-backward partial sums of the group's planes
   double* gacc;        // [raw param count] fp64 parameter-gradient accumulators
   float* wpart;        // [kWgBlocks][kWgPartMax] wgrad partials
   double* rseg;        // [kRedSeg][kWgPartMax] segment sums of the partials
@@ -119,8 +118,8 @@ BpttLayout bptt_layout(void* base, int B, int H, int W) {
   L.gu[1] = reinterpret_cast<float*>(take((size_t)G * B * HW * 16 * 4));
   L.gx = reinterpret_cast<float*>(take((size_t)G * B * HW * kC * 4));
   L.gnb_nblk = (int)std::min<size_t>(512, (HW + 1023) / 1024);
-  L.gnb_part = reinterpret_cast<double*>(take((size_t)B * L.gnb_nblk * 36 * 8));
-  L.gnb_sum = reinterpret_cast<double*>(take((size_t)B * 8 * 8));
+  for (int j = 0; j < 2; ++j)
+    L.gnb_part[j] = reinterpret_cast<double*>(take((size_t)G * B * L.gnb_nblk * 36 * 8));
   L.gacc = reinterpret_cast<double*>(take(param_layout().raw_total * 8));
   L.wpart = reinterpret_cast<float*>(take((size_t)kWgBlocks * kWgPartMax * 4));
   L.rseg = reinterpret_cast<double*>(take((size_t)kRedSeg * kWgPartMax * 8));
@@ -465,33 +464,32 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(GnbArgs a) {
   }
 }
 
-// per b: S1, S2 of both groups -> gnb_sum[b][j]; the affine sums (all b, fixed order) -> gacc.
-// One block per column: strided per-thread sums and a fixed tree per b.
-__global__ void __launch_bounds__(256) gnb_reduce_kernel(const double* __restrict__ part, int nblk,
-                                                         int B, int j, double* __restrict__ gnb_sum,
-                                                         double* __restrict__ gacc_gamma,
+// The affine sums of a group's planes -> gacc, once per group (one block per column 4 .. 35):
+// plane by plane in the backward's order (last first), per plane the samples in order, per
+// sample strided per-thread sums and a fixed tree -- the order a per-plane reduce would use.
+__global__ void __launch_bounds__(256) gnb_affine_kernel(const double* __restrict__ part, int n, int nblk,
+                                                         int B, double* __restrict__ gacc_gamma,
                                                          double* __restrict__ gacc_beta) {
   __shared__ double red[256];
-  const int i = blockIdx.x, t = threadIdx.x;
-  double tot = 0.0;
-  for (int b = 0; b < B; ++b) {
-    double s = 0.0;
-    for (int k = t; k < nblk; k += 256) s += part[((size_t)b * nblk + k) * 36 + i];
-    red[t] = s;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (t < o) red[t] += red[t + o];
+  const int i = 4 + blockIdx.x, t = threadIdx.x;
+  for (int k = n - 1; k >= 0; --k) {
+    double tot = 0.0;
+    for (int b = 0; b < B; ++b) {
+      double s = 0.0;
+      for (int m = t; m < nblk; m += 256) s += part[(((size_t)k * B + b) * nblk + m) * 36 + i];
+      red[t] = s;
+      __syncthreads();
+      for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) red[t] += red[t + o];
+        __syncthreads();
+      }
+      if (t == 0) tot += red[0];
       __syncthreads();
     }
     if (t == 0) {
-      if (i < 4) gnb_sum[(b * 2 + j) * 4 + i] = red[0];
-      tot += red[0];
+      if (i < 20) gacc_gamma[i - 4] += tot;
+      else gacc_beta[i - 20] += tot;
     }
-    __syncthreads();
-  }
-  if (t == 0) {
-    if (i >= 4 && i < 20) gacc_gamma[i - 4] += tot;
-    if (i >= 20) gacc_beta[i - 20] += tot;
   }
 }
 
@@ -506,7 +504,8 @@ struct DcbArgs {
   const float* gr;       // [B][Ho][Wo][16]
   const float* u;        // [B][Ho][Wo][16]
   const double* stats;   // plane's reg stats
-  const double* gnb_sum; // [B][2][4]
+  const double* part;    // the plane's GroupNorm-backward partials [B][nblk][36]
+  int nblk;
   const float* gamma;
   const float* beta;
   const float* w;        // raw ConvTranspose2d weight [ci][co][3][3]
@@ -519,7 +518,24 @@ __global__ void __launch_bounds__(256) deconv_bwd_kernel(DcbArgs a) {
   __shared__ float4 wsh[9 * 16 * 4];   // [tap][co][ci / 4]
   __shared__ float coef[4][16];        // y = u a + b; xhat = (u - mean) rstd
   __shared__ float gco[2][2];          // per group: S1 / n, S2 / n
+  __shared__ double gred[4][256];
   const int b = blockIdx.y, tid = threadIdx.x;
+  // S1, S2 of both groups from the partials: strided per-thread sums and a fixed tree (every
+  // block computes the same values)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    double sum = 0.0;
+    for (int m = tid; m < a.nblk; m += 256) sum += a.part[((size_t)b * a.nblk + m) * 36 + i];
+    gred[i][tid] = sum;
+  }
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gred[i][tid] += gred[i][tid + o];
+    }
+    __syncthreads();
+  }
   const int Ho = 2 * a.Hi, Wo = 2 * a.Wi;
   for (int i = tid; i < 9 * 16 * 16; i += 256) {
     const int ci = i & 15, co = (i >> 4) & 15, tap = i >> 8;
@@ -535,8 +551,8 @@ __global__ void __launch_bounds__(256) deconv_bwd_kernel(DcbArgs a) {
     coef[3][c] = st.rstd;
     if ((c & 7) == 0) {
       const double n = 8.0 * Ho * Wo;
-      gco[g][0] = (float)(a.gnb_sum[(b * 2 + a.j) * 4 + 2 * g] / n);
-      gco[g][1] = (float)(a.gnb_sum[(b * 2 + a.j) * 4 + 2 * g + 1] / n);
+      gco[g][0] = (float)(gred[2 * g][0] / n);
+      gco[g][1] = (float)(gred[2 * g + 1][0] / n);
     }
   }
   __syncthreads();
@@ -1271,6 +1287,11 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     a.W = W / res_div[k];
     return kCellHid[k] == 16 ? run_dgrad<64>(a, s) : run_dgrad<32>(a, s);
   };
+  // GroupNorm-backward partial blocks per (plane, sample) of deconv j's output
+  auto gnb_nblk = [&](int j) {
+    const size_t hwo = (size_t)(j ? H : H / 2) * (j ? W : W / 2);
+    return std::max(1, std::min(L.gnb_nblk, (int)((hwo + 1023) / 1024)));
+  };
   auto deconv_bwd = [&](int j, int slot, const UnetIO& io) {
     const int Ho = j ? H : H / 2, Wo = j ? W : W / 2;
     const size_t hwo = (size_t)Ho * Wo;
@@ -1280,20 +1301,18 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     g.stats = io.reg_stats;
     g.gamma = pk + PL.pk_off[j ? P_D1GW : P_D0GW];
     g.beta = pk + PL.pk_off[j ? P_D1GB : P_D0GB];
-    g.part = L.gnb_part;
+    const int nblk = gnb_nblk(j);
+    g.part = L.gnb_part[j] + (size_t)slot * B * nblk * 36;
     g.j = j;
     g.HW = (int)hwo;
-    const int nblk = std::max(1, std::min(L.gnb_nblk, (int)((hwo + 1023) / 1024)));
     hipLaunchKernelGGL(gnb_partial_kernel, dim3(nblk, B), dim3(256), 0, s, g);
-    CK(hipGetLastError());
-    hipLaunchKernelGGL(gnb_reduce_kernel, dim3(36), dim3(256), 0, s, L.gnb_part, nblk, B, j, L.gnb_sum,
-                       L.gacc + PL.raw_off[j ? P_D1GW : P_D0GW], L.gacc + PL.raw_off[j ? P_D1GB : P_D0GB]);
     CK(hipGetLastError());
     DcbArgs a{};
     a.gr = L.gr[j];
     a.u = g.u;
     a.stats = io.reg_stats;
-    a.gnb_sum = L.gnb_sum;
+    a.part = g.part;
+    a.nblk = nblk;
     a.gamma = g.gamma;
     a.beta = g.beta;
     a.w = pk + PL.pk_off[j ? P_D1W : P_D0W];
@@ -1399,6 +1418,11 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
                             : nch == 3     ? run_wgrad<64, 3>(a, gw, gb, s)
                                            : run_wgrad<64, 2>(a, gw, gb, s);
       CK(we);
+    }
+    for (int j = 0; j < 2; ++j) {   // the deconvs' GroupNorm affine gradients of the group
+      hipLaunchKernelGGL(gnb_affine_kernel, dim3(32), dim3(256), 0, s, L.gnb_part[j], n, gnb_nblk(j), B,
+                         L.gacc + PL.raw_off[j ? P_D1GW : P_D0GW], L.gacc + PL.raw_off[j ? P_D1GB : P_D0GB]);
+      CK(hipGetLastError());
     }
     for (int j = 0; j < 2; ++j) {
       DcwArgs a{};
