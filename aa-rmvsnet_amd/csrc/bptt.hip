@@ -137,7 +137,7 @@ BpttLayout bptt_layout(void* base, int B, int H, int W) {
 // One thread per (pixel, 4 hidden channels).
 // ---------------------------------------------------------------------------
 struct GateBwdArgs {
-  const float* z;        // [P][4 hid] pre-activations (i, f, o, g)
+  const float* z;        // pre-activations (i, f, o, g), the record's [B][hid/4][4][H*W][4]
   const float* c_prev;   // [P][hid]
   const float* c_new;    // [P][hid]
   const float* gh;       // [P][hid] dL/dh'
@@ -203,11 +203,13 @@ __global__ void __launch_bounds__(256) gate_bwd_kernel(GateBwdArgs a) {
         }
       }
     }
-    const float* zp = a.z + p * (4 * hid) + c0;
+    // the record's planar gate layout [B][hid/4 quads][4 gates][H*W][4] (CellArgs::z_out)
+    const size_t HWc = (size_t)a.H * a.W;
+    const float* zp = a.z + (size_t)b * 4 * hid * HWc + ((size_t)(c0 >> 2) * 4 * HWc + (p - (size_t)b * HWc)) * 4;
     const float4 zi = *reinterpret_cast<const float4*>(zp);
-    const float4 zf = *reinterpret_cast<const float4*>(zp + hid);
-    const float4 zo = *reinterpret_cast<const float4*>(zp + 2 * hid);
-    const float4 zg = *reinterpret_cast<const float4*>(zp + 3 * hid);
+    const float4 zf = *reinterpret_cast<const float4*>(zp + HWc * 4);
+    const float4 zo = *reinterpret_cast<const float4*>(zp + 2 * HWc * 4);
+    const float4 zg = *reinterpret_cast<const float4*>(zp + 3 * HWc * 4);
     const float4 cp = *reinterpret_cast<const float4*>(a.c_prev + p * hid + c0);
     const float4 cn = *reinterpret_cast<const float4*>(a.c_new + p * hid + c0);
     const float4 gc4 = *reinterpret_cast<const float4*>(a.gc + p * hid + c0);

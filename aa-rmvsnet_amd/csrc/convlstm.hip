@@ -44,7 +44,8 @@ struct CellArgs {
   float* h_new;
   float* c;             // c' out ([B][H][W][HID]); the eval sweep updates c in place (c_in == c)
   const float* c_in;    // c of the previous plane
-  float* z_out;         // training record: the gate pre-activations (conv + bias) [B][H][W][4 HID], or null
+  float* z_out;         // training record: the gate pre-activations (conv + bias), or null: planar,
+                        // [B][HID/4 channel quads][gates i, f, o, g][H*W][4]
   const float* wpk;     // packed A operands [K/2][MT][64]
   const float* bias;    // [4*hid]
   const unsigned* xbound;   // cell 0: float bits of a bound on |x| (fp16 range guard), or null
@@ -384,7 +385,10 @@ __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 
         *reinterpret_cast<float4*>(a.c + o) = make_float4(cn[0], cn[1], cn[2], cn[3]);
         *reinterpret_cast<float4*>(a.h_new + o) = make_float4(hn[0], hn[1], hn[2], hn[3]);
         if (a.z_out) {   // gates i, f, o, g of channels m*8 + 4 hi .. +3 (module.py:83)
-          float* zo = a.z_out + pix * (4 * HID) + m * 8 + 4 * hi;
+          // planar record layout [B][HID/4 channel quads][4 gates][H*W][4]: a wave's stores of
+          // one gate are contiguous (512 B per half-wave)
+          const size_t P = (size_t)a.H * a.W;
+          float* zo = a.z_out + (size_t)b * 4 * HID * P + ((size_t)(m * 2 + hi) * 4 * P + (size_t)y * a.W + x) * 4;
 #pragma unroll
           for (int gt = 0; gt < 4; ++gt) {
             float zz[4];
@@ -393,7 +397,7 @@ __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 
               const int ch = m * 8 + 4 * hi + q;
               zz[q] = fmaf(acc[m][r][4 * gt + q], inv_scale, a.bias[gt * HID + ch]);
             }
-            *reinterpret_cast<float4*>(zo + gt * HID) = make_float4(zz[0], zz[1], zz[2], zz[3]);
+            *reinterpret_cast<float4*>(zo + gt * P * 4) = make_float4(zz[0], zz[1], zz[2], zz[3]);
           }
         }
       }

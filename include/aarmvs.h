@@ -91,7 +91,8 @@ int aarmvs_homo_warp_backward(const float* grad_out, const float* rel_proj, cons
  *   0 x      [B,H,W,32] cost slice of the plane (NHWC);                 D slabs
  *   1 state  h, c of the five cells (NHWC); slab 0 is the zero initial state
  *            (drmvsnet.py:133-134), slab d+1 the state after plane d;  D+1 slabs
- *   2 z      the five cells' gate pre-activations (conv + bias; i,f,o,g); D slabs
+ *   2 z      the five cells' gate pre-activations (conv + bias), per cell planar
+ *            [B][hid/4 channel quads][gates i,f,o,g][H*W][4];           D slabs
  *   3 u      the two deconvs' outputs before GroupNorm;                  D slabs
  *   4 stats  the two deconvs' GroupNorm statistics (fp64);               D slabs
  * ~1 KB per pixel and plane at B = 1 (63 GB for 640x512, D = 192). */

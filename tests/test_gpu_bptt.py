@@ -87,7 +87,9 @@ def test_recorded_forward_matches_eval_sweep_and_holds_the_tensors():
     st_d = rec["state"].view(torch.float32)[d * slab:(d + 1) * slab]
     h0 = st_d[: B * H * W * 16].view(B, H, W, 16)
     zsl = L.aarmvs_train_record_bytes(B, H, W, 2) // 4
-    z0 = rec["z"].view(torch.float32)[d * zsl: d * zsl + B * H * W * 64].view(B, H, W, 64)
+    # planar record layout [B][4 channel quads][4 gates][H*W][4] -> [B,H,W,(gate, channel)]
+    z0 = (rec["z"].view(torch.float32)[d * zsl: d * zsl + B * H * W * 64].view(B, 4, 4, H * W, 4)
+          .permute(0, 3, 2, 1, 4).reshape(B, H, W, 64))
     inp = torch.cat([xs, h0], -1).permute(0, 3, 1, 2).double().cpu()
     w = P["cost_regularization.cell_list.0.conv.weight"].double()
     bb = P["cost_regularization.cell_list.0.conv.bias"].double()
