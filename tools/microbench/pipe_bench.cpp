@@ -209,6 +209,32 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
       CK(hipEventElapsedTime(&ms, e0, e1));
       printf("cost_x npl=8 4-row tiles (256 threads) %8.3f ms/plane\n", ms / 10 / npl);
+      // co-running: omega_mfma (the library's 16x16 tiles) on one stream and cost_x (4-row
+      // tiles) on another, independent buffers -- do the two kernels' limits (latency / L1
+      // gathers) overlap on shared CUs?
+      PipeArgs ao = a0;
+      ao.npl = 8; ao.t1_kstride = t1k; ao.st_kstride = stk; ao.d_next = 1; ao.t1_next = t1b; ao.st_next = stb;
+      const int nt16 = OmegaTile<16>::tiles(H, W);
+      ao.part_n = nt16;
+      hipStream_t s1, s2;
+      CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+      CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+      auto om16 = [&](hipStream_t st) { hipLaunchKernelGGL((omega_mfma_kernel<0, 16>), dim3(nt16 * nsrc * 8, 1, B), dim3(OmegaTile<16>::NT), 0, st, ao, dpar, drel, ws.xbound); };
+      auto cx4 = [&](hipStream_t st) { hipLaunchKernelGGL((cost_x_kernel<2, 4>), dim3(tiles_x * ((H + 3) / 4) * npl, B), dim3(2 * 4 * kTileW), 0, st, c, dpar, drel); };
+      auto timed = [&](const char* name, auto body) {
+        body(); CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < 5; ++i) body();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+        float mm; CK(hipEventElapsedTime(&mm, e0, e1));
+        printf("corun %-40s %8.3f ms per (8-plane) launch pair\n", name, mm / 5);
+      };
+      timed("omega alone", [&] { om16(s1); });
+      timed("cost_x alone", [&] { cx4(s2); });
+      timed("omega then cost_x (one stream)", [&] { om16(s1); cx4(s1); });
+      timed("omega || cost_x (two streams)", [&] { om16(s1); cx4(s2); });
+      CK(hipStreamDestroy(s1)); CK(hipStreamDestroy(s2));
     }
   }
   {
