@@ -702,8 +702,15 @@ __global__ void __launch_bounds__(512) wgrad2_kernel(WgradArgs a) {
   const int ntile = a.B * tiles_x * tiles_y;
   const int nitem = ntile * a.nplanes;
   // staging scale of a chunk
+  // GroupNorm+ReLU chunks: the nominal 16 lowered so that bound 16 2^-e <= 2^15 (the forward
+  // cells' range guard, gn_relu_bound)
   auto chunk_scale = [&](const WgChunk& ch) {
-    return ch.bound ? ldexpf(1.0f, -scale_exp(*ch.bound)) : ch.scale;
+    if (ch.bound) return ldexpf(1.0f, -scale_exp(*ch.bound));
+    if (ch.mode == WG_GNRELU) {
+      const float b16 = gn_relu_bound(ch.gamma - 8 * ch.gn0, ch.beta - 8 * ch.gn0, 8.0 * a.H * a.W) * ch.scale;
+      if (b16 > 32768.0f) return ch.scale * ldexpf(1.0f, -(ilogbf(b16) >= 134 ? 120 : ilogbf(b16) - 14));
+    }
+    return ch.scale;
   };
   auto item_pos = [&](int item, int& k, int& b, int& y0, int& x0) {
     k = item / ntile;

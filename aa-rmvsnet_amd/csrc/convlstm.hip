@@ -65,6 +65,18 @@ __device__ __forceinline__ int xguard_exp(const unsigned* xb) {
   return k >= 134 ? 120 : k - 14;
 }
 
+// fp16 range guard of the GroupNorm(2,16)+ReLU part of cells 3 and 4 (deConvGnReLU's output,
+// module.py:286-287): y = relu(gamma xhat + beta) with xhat bounded by sqrt(n - 1) for n values
+// of mean 0 and unit biased variance (Samuelson's inequality), so |y| <= gn_relu_bound(); the part is
+// staged as y 2^-e and its partial sums rescaled by 2^e, as cell 0's x.  e = 0 (bit-identical
+// to no guard) whenever the bound is <= 32768: |gamma| below ~8-16 at the BASELINE sizes.
+__device__ __forceinline__ int gguard_exp(const float* gamma, const float* beta, int H, int W) {
+  const float bound = gn_relu_bound(gamma, beta, 8.0 * H * W);
+  if (bound <= 32768.0f) return 0;
+  const int k = ilogbf(bound);
+  return k >= 134 ? 120 : k - 14;
+}
+
 constexpr int kMaxParts = 3;
 
 // The five cells of the U-Net (drmvsnet.py:141-161): input parts in concatenation
@@ -173,7 +185,8 @@ struct H3PixStager {
   static_assert(NI <= 32, "item mask holds 32 items");
   float val[NI][8][4];   // [item][channel][POOL window: fine (2y,2x) (2y,2x+1) (2y+1,2x) (2y+1,2x+1)]
   uint32_t in_mask;      // bit j: item j is an in-image pixel of valid channels
-  float xs = 1.0f;       // cell 0: 2^-e of the fp16 range guard (xguard_exp), applied to x
+  float xs = 1.0f;       // 2^-e of the fp16 range guard of part 0: cell 0's x (xguard_exp), cells
+                         // 3 and 4's GroupNorm+ReLU part (gguard_exp)
 
   template <int CH>
   __device__ __forceinline__ void load(const CellArgs& a, int b, int y0, int x0, int tid) {
@@ -232,7 +245,7 @@ struct H3PixStager {
             x = fmaxf(fmaxf(val[j][k][0], val[j][k][1]), fmaxf(val[j][k][2], val[j][k][3]));
           } else if (MODE == SRC_GNRELU) {
             const int lc = LC0 + 8 * h + k;
-            x = fmaxf(val[j][k][0] * gn[lc] + gn[16 + lc], 0.0f);
+            x = fmaxf(val[j][k][0] * gn[lc] + gn[16 + lc], 0.0f) * xs;
           } else {
             x = val[j][k][0];
             if constexpr (KIND == 0 && C::chunk_part(CH) == 0) x *= xs;
@@ -250,11 +263,12 @@ struct H3PixStager {
   }
 };
 
-// Before the MFMAs of chunk CH: undo cell 0's x guard scale on the x chunks' partial sums
-// (CH is the first chunk past the x part).
+// Before the MFMAs of chunk CH: undo the range guard's scale of part 0 (cell 0's x, cells 3 and
+// 4's GroupNorm+ReLU part) on its chunks' partial sums (CH is the first chunk past part 0).
 template <class C, int KIND, int CH>
 __device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], float xr) {
-  if constexpr (KIND == 0 && CH > 0 && C::chunk_part(CH) != 0 && C::chunk_part(CH - 1) == 0) {
+  if constexpr ((KIND == 0 || C::D::MODE[0] == SRC_GNRELU) && CH > 0 && C::chunk_part(CH) != 0 &&
+                C::chunk_part(CH - 1) == 0) {
 #pragma unroll
     for (int m = 0; m < C::MT; ++m)
 #pragma unroll
@@ -452,7 +466,8 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     x0 = (rem % tiles_x) * C::TW;
   };
   H3PixStager<KIND, RW, WAVES> st;
-  const int xe = KIND == 0 ? xguard_exp(a.xbound) : 0;
+  const int xe = KIND == 0 ? xguard_exp(a.xbound)
+                 : D::MODE[0] == SRC_GNRELU ? gguard_exp(a.part[0].gamma, a.part[0].beta, H, W) : 0;
   st.xs = ldexpf(1.0f, -xe);
   const float xr = ldexpf(1.0f, xe);
   int tile = blockIdx.x;
@@ -552,7 +567,8 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
   int tile = blockIdx.x;
   if (tile >= ntiles) return;   // whole block
   H3PixStager<KIND, RW, WAVES> st;
-  const int xe = KIND == 0 ? xguard_exp(a.xbound) : 0;
+  const int xe = KIND == 0 ? xguard_exp(a.xbound)
+                 : D::MODE[0] == SRC_GNRELU ? gguard_exp(a.part[0].gamma, a.part[0].beta, H, W) : 0;
   st.xs = ldexpf(1.0f, -xe);
   const float xr = ldexpf(1.0f, xe);
   int b, y0, x0;

@@ -111,6 +111,17 @@ __device__ __forceinline__ void stat_add(double* stat, double s, double ss) {
   atomicAdd(slot + 1, ss);
 }
 
+// Bound on |relu(gamma_c xhat + beta_c)| over the 16 channels of a GroupNorm(2,16)+ReLU output
+// (deConvGnReLU, module.py:286-287) with n values per group: |xhat| <= sqrt(n - 1) (Samuelson),
+// 1% margin for the fp32 evaluation.  Uniform loads: every lane computes the same value.
+__device__ __forceinline__ float gn_relu_bound(const float* gamma, const float* beta, double n) {
+  const float s = 1.01f * (float)sqrt(n > 1.0 ? n - 1.0 : 0.0);
+  float m = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) m = fmaxf(m, fabsf(gamma[c]) * s + fabsf(beta[c]));
+  return m;
+}
+
 // GroupNorm fused parameters from fp64 slot sums: y = x * a + b with
 // a = rstd * gamma, b = beta - mean * a  (the ATen CPU group_norm form).
 struct GnStat {

@@ -1,5 +1,6 @@
 """GPU parity at BASELINE.json's full frames (configs 2, 3 and 5) against the CPU oracle,
-the cell-0 fp16 range guard, and the standalone §8b entries (aarmvs_cost_slice,
+the fp16 range guards (cell 0's cost slice, cells 3 and 4's GroupNorm+ReLU part), and the
+standalone §8b entries (aarmvs_cost_slice,
 aarmvs_wta_update).
 
 The oracle runs the first k planes of each full-frame workload (its F.grid_sample form,
@@ -106,6 +107,52 @@ def test_cell0_fp16_range_guard_with_large_features():
     c_ref, _ = orc.unet_step(x0, state, P)
     c_gpu = sw.unet_step(x0.to(DEV), 0)
     np.testing.assert_allclose(c_gpu.cpu().numpy(), c_ref.numpy(), atol=1e-4, rtol=1e-4)
+
+
+def test_gn_relu_fp16_range_guard_with_large_gamma():
+    """deConvGnReLU's GroupNorm affine x100000: relu(GN(u)) feeding cells 3 and 4 exceeds 65504
+    (fp16's largest finite; checked in the oracle), which their split-fp16 staging would turn
+    into inf without the guard (convlstm.hip gguard_exp: bound |gamma| sqrt(n - 1) + |beta|).
+    The sweep matches the oracle; the training backward (the weight gradients' GroupNorm+ReLU
+    chunks use the same bound) stays finite."""
+    from oracle import sweep_oracle as orc
+    from aarmvs import ops
+    B, N, H, W, D = 1, 3, 48, 64, 4
+    sc = syn.scene(B, N, H, W, D, seed=301)
+    feats = torch.from_numpy(sc["features"])
+    proj = torch.from_numpy(sc["proj_matrices"])
+    dv = torch.from_numpy(sc["depth_values"])
+    P = real_P()
+    for j in (0, 1):
+        for t in ("weight", "bias"):
+            P[f"cost_regularization.deconv_{j}.gn.{t}"] = P[f"cost_regularization.deconv_{j}.gn.{t}"] * 1e5
+    views = _views(feats, proj)
+    rels = [orc.relative_projection(sp, views[2]) for sp in views[3]]
+    x0 = orc.cost_slice(views[0], views[1], rels, dv[:, 0], P)
+    st = orc.init_state(B, H, W)
+    cw = lambda i: (P[f"cost_regularization.cell_list.{i}.conv.weight"],   # noqa: E731
+                    P[f"cost_regularization.cell_list.{i}.conv.bias"])
+    h0, _ = orc.lstm_cell(x0, *st[0], *cw(0))
+    h1, _ = orc.lstm_cell(torch.nn.functional.max_pool2d(h0, 2, 2), *st[1], *cw(1))
+    h2, _ = orc.lstm_cell(torch.nn.functional.max_pool2d(h1, 2, 2), *st[2], *cw(2))
+    assert float(orc.deconv_gn_relu(h2, P, "deconv_0").max()) > 65504.0
+    ref = orc.sweep(*views, dv, P)
+    sw = ops.DepthSweep({n: v.to(DEV) for n, v in P.items()}, DEV)
+    args = _views(feats.to(DEV), proj)
+    out = sw(*args, dv, want_cost=True)
+    cost = out["cost"].cpu().numpy()
+    assert np.isfinite(cost).all()
+    np.testing.assert_allclose(cost, ref["cost"].numpy(), atol=1e-3, rtol=1e-3)
+    assert rel_l1(out["depth"].cpu().numpy(), ref["depth"].numpy()) <= 1e-3
+    # the BPTT on the same weights
+    rec = sw.record_buffers(B, H, W, D, DEV)
+    rel = sw.relative(args[2], args[3], B)
+    cvol = torch.empty(B, D, H, W, device=DEV)
+    sw(*args, dv, want_depth=False, cost_out=cvol, rel=rel, record=rec)
+    g_ref, g_srcs, g_par, _ = sw.backward(args[0], args[1], rel, dv, rec, torch.ones_like(cvol))
+    torch.cuda.synchronize()
+    assert torch.isfinite(g_ref).all() and all(torch.isfinite(g).all() for g in g_srcs)
+    assert all(torch.isfinite(g).all() for g in g_par.values())
 
 
 def test_standalone_cost_slice_matches_reference_fixture():
