@@ -49,6 +49,44 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f);
 }
 
+// Wave-wide reductions on DPP (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror,
+// row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3): plain VALU operations,
+// no LDS round trips (a __shfl_xor butterfly is six dependent ds_bpermute_b32 per dword).
+// The 64 lanes combine in a fixed order; the result is lane 63's, returned wave-uniform.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_i32(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWS, 0xF, false);
+}
+template <class Op>
+__device__ __forceinline__ int wave_reduce_i32(int v, int ident, Op op) {
+  v = op(v, dpp_i32<0xB1, 0xF>(ident, v));
+  v = op(v, dpp_i32<0x4E, 0xF>(ident, v));
+  v = op(v, dpp_i32<0x141, 0xF>(ident, v));
+  v = op(v, dpp_i32<0x140, 0xF>(ident, v));
+  v = op(v, dpp_i32<0x142, 0xA>(ident, v));
+  v = op(v, dpp_i32<0x143, 0xC>(ident, v));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64(double v) {   // lanes not written read +0.0
+  const long long b = __double_as_longlong(v);
+  const int lo = dpp_i32<CTRL, ROWS>(0, (int)(b & 0xffffffffll));
+  const int hi = dpp_i32<CTRL, ROWS>(0, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+  v += dpp_f64<0xB1, 0xF>(v);
+  v += dpp_f64<0x4E, 0xF>(v);
+  v += dpp_f64<0x141, 0xF>(v);
+  v += dpp_f64<0x140, 0xF>(v);
+  v += dpp_f64<0x142, 0xA>(v);
+  v += dpp_f64<0x143, 0xC>(v);
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -84,9 +122,7 @@ template <int NV>
 __device__ __forceinline__ void block_sum_d(double (&v)[NV], double* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #pragma unroll
-  for (int i = 0; i < NV; ++i)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o, 64);
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum_d(v[i]);
   __syncthreads();
   if (lane == 0) {
 #pragma unroll

@@ -331,13 +331,12 @@ struct Box {
 template <int NW = kTileWaves>
 __device__ __forceinline__ Box box_reduce(int lx, int ly, int hx, int hy, int (*red)[4]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lx = min(lx, __shfl_xor(lx, o, 64));
-    ly = min(ly, __shfl_xor(ly, o, 64));
-    hx = max(hx, __shfl_xor(hx, o, 64));
-    hy = max(hy, __shfl_xor(hy, o, 64));
-  }
+  auto mn = [](int a, int b) { return min(a, b); };
+  auto mx = [](int a, int b) { return max(a, b); };
+  lx = wave_reduce_i32(lx, INT_MAX, mn);
+  ly = wave_reduce_i32(ly, INT_MAX, mn);
+  hx = wave_reduce_i32(hx, INT_MIN, mx);
+  hy = wave_reduce_i32(hy, INT_MIN, mx);
   if (lane == 0) {
     red[wave][0] = lx;
     red[wave][1] = ly;
@@ -862,11 +861,8 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     ps = ((double)out.x + (double)out.y) + ((double)out.z + (double)out.w);
     pss = ((double)out.x * out.x + (double)out.y * out.y) + ((double)out.z * out.z + (double)out.w * out.w);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    ps += __shfl_xor(ps, o, 64);
-    pss += __shfl_xor(pss, o, 64);
-  }
+  ps = wave_sum_d(ps);
+  pss = wave_sum_d(pss);
   if (lane == 0) {
     wsum[wave][0] = ps;
     wsum[wave][1] = pss;
