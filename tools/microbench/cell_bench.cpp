@@ -135,19 +135,17 @@ int main() {
   run("cell4 h3 RW2 W4 DB0", [&] { return run_cell_h3<4, 2, 4, 0, 0, 0>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
   run("cell3 h3 RW2 W8 DB0", [&] { return run_cell_h3<3, 2, 8, 0, 0, 1>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
   run("cell1 h3 RW2 W8 DB0", [&] { return run_cell_h3<1, 2, 8, 0, 0, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
-  // 16 waves (16 rows) per block: 4 waves per SIMD on the one block a CU holds
-  run("cell0 h3 W16 DB0 PIPE1", [&] { return run_cell_h3<0, 1, 16, 0, 0, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell0 h3 W16 DB0 PIPE0", [&] { return run_cell_h3<0, 1, 16, 0, 0, 0>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell0 h3 W16 MFMA only (6)", [&] { return run_cell_h3<0, 1, 16, 6, 0, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
-  run("cell1 h3 W16 DB0 PIPE1", [&] { return run_cell_h3<1, 1, 16, 0, 0, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
-  run("cell1 h3 W16 DB1 PIPE1", [&] { return run_cell_h3<1, 1, 16, 0, 1, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
-  run("cell3 h3 W16 DB0 PIPE1", [&] { return run_cell_h3<3, 1, 16, 0, 0, 1>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
-  run("cell4 h3 W16 DB0 PIPE0", [&] { return run_cell_h3<4, 1, 16, 0, 0, 0>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
-  run("cell4 h3 W16 DB1 PIPE0", [&] { return run_cell_h3<4, 1, 16, 0, 1, 0>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
   run("cell0 h3 no MFMA (1)", [&] { return run_cell_h3<0, 1, 8, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 no staging (2)", [&] { return run_cell_h3<0, 1, 8, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 MFMA only (6)", [&] { return run_cell_h3<0, 1, 8, 6>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 skeleton (7)", [&] { return run_cell_h3<0, 1, 8, 7>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell1 h3 DB1 no MFMA (1)", [&] { return run_cell_h3<1, 1, 8, 1, 1, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell1 h3 DB1 no staging (2)", [&] { return run_cell_h3<1, 1, 8, 2, 1, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell1 h3 DB1 MFMA only (6)", [&] { return run_cell_h3<1, 1, 8, 6, 1, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell1 h3 DB1 skeleton (7)", [&] { return run_cell_h3<1, 1, 8, 7, 1, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell3 h3 no MFMA (1)", [&] { return run_cell_h3<3, 1, 8, 1, 0, 1>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+  run("cell3 h3 MFMA only (6)", [&] { return run_cell_h3<3, 1, 8, 6, 0, 1>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+  run("cell3 h3 skeleton (7)", [&] { return run_cell_h3<3, 1, 8, 7, 0, 1>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
   run("cell4 h3 no MFMA (1)", [&] { return run_cell_h3<4, 1, 8, 1>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
   run("cell4 h3 MFMA only (6)", [&] { return run_cell_h3<4, 1, 8, 6>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
   return 0;
