@@ -20,7 +20,7 @@ c_int, c_size_t, c_void_p, c_char_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_vo
 class TrainRecord(ctypes.Structure):
     """Mirror of ``aarmvs_train_record``."""
     _fields_ = [("x", c_void_p), ("state", c_void_p), ("z", c_void_p), ("u", c_void_p),
-                ("stats", c_void_p)]
+                ("stats", c_void_p), ("t1", c_void_p), ("ostats", c_void_p)]
 
 
 class SweepArgs(ctypes.Structure):

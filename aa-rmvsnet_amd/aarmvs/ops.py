@@ -302,25 +302,40 @@ class DepthSweep:
         rel = torch.stack([relative_projection(sp, ref_proj) for sp in src_projs])  # [nsrc,B,3,4]
         return rel.reshape(len(src_projs), B, 12).to(self.device).contiguous()
 
+    RECORD_KEYS = ("x", "state", "z", "u", "stats", "t1", "ostats")
+
     @staticmethod
-    def record_buffers(B: int, H: int, W: int, D: int, device) -> dict:
-        """Device buffers of a training record (aarmvs_train_record) for D planes: the cost
-        slices, D + 1 regulariser state slabs, the gate pre-activations, the deconv outputs and
-        their GroupNorm statistics (~1 KB per pixel and plane at B = 1)."""
+    def _record_sizes(B: int, H: int, W: int, D: int, nsrc: int) -> dict:
         L = lib()
+        counts = (D, D + 1, D, D, D, D * nsrc, D * nsrc)
         out = {}
-        for i, (name, count) in enumerate((("x", D), ("state", D + 1), ("z", D), ("u", D),
-                                           ("stats", D))):
+        for i, (name, count) in enumerate(zip(DepthSweep.RECORD_KEYS, counts)):
             n = L.aarmvs_train_record_bytes(B, H, W, i)
             if n == 0:
                 raise AarmvsError(f"aarmvs: invalid record geometry B={B} H={H} W={W}")
-            out[name] = torch.empty(n * count, dtype=torch.uint8, device=device)
+            out[name] = n * count
         return out
 
     @staticmethod
-    def _record_struct(rec: dict):
+    def record_buffers(B: int, H: int, W: int, D: int, device, *, nsrc: int) -> dict:
+        """Device buffers of a training record (aarmvs_train_record) for D planes and nsrc
+        source views: the cost slices, D + 1 regulariser state slabs, the gate pre-activations,
+        the deconv outputs and their GroupNorm statistics, the omega conv output and its
+        statistics (~1 KB per pixel and plane at B = 1, N = 3)."""
+        return {k: torch.empty(n, dtype=torch.uint8, device=device)
+                for k, n in DepthSweep._record_sizes(B, H, W, D, nsrc).items()}
+
+    @staticmethod
+    def _record_struct(rec: dict, B: int, H: int, W: int, D: int, nsrc: int):
+        """ctypes view of a record, after checking every buffer holds this geometry's bytes
+        (the library writes them without bounds)."""
+        for k, n in DepthSweep._record_sizes(B, H, W, D, nsrc).items():
+            t = rec.get(k)
+            if t is None or not t.is_cuda or t.numel() * t.element_size() < n:
+                raise AarmvsError(f"aarmvs: training record '{k}' missing or smaller than {n} B "
+                                  f"(record_buffers(B, H, W, D, nsrc={nsrc}))")
         r = _lib.TrainRecord()
-        r.x, r.state, r.z, r.u, r.stats = (rec[k].data_ptr() for k in ("x", "state", "z", "u", "stats"))
+        (r.x, r.state, r.z, r.u, r.stats, r.t1, r.ostats) = (rec[k].data_ptr() for k in DepthSweep.RECORD_KEYS)
         return r
 
     @_on_tensor_device
@@ -333,7 +348,7 @@ class DepthSweep:
         later ranges continue from the state the previous call left in the workspace).
         ``cost_out`` is an optional caller-owned [B,D,H,W] buffer for the regulariser output.
         ``rel`` is an optional precomputed ``self.relative(ref_proj, src_projs, B)``.
-        ``record`` (``record_buffers(B, H, W, D)``) keeps every plane's tensors for
+        ``record`` (``record_buffers(B, H, W, D, nsrc=...)``) keeps every plane's tensors for
         ``backward`` (the training forward).
         """
         ref = ref_fea.contiguous()
@@ -395,7 +410,7 @@ class DepthSweep:
         a.aux_stream = self._aux.cuda_stream if self._aux is not None else None
         rec_struct = None
         if record is not None:
-            rec_struct = self._record_struct(record)
+            rec_struct = self._record_struct(record, B, H, W, D, nsrc)
             a.record = ctypes.pointer(rec_struct)
         check(lib().aarmvs_sweep(ctypes.byref(a), _stream()), "sweep")
         out["_keepalive"] = (rel, dv, srcs, ref, rec_struct)
@@ -442,7 +457,7 @@ class DepthSweep:
         a.rel_proj = rel.data_ptr()
         a.depth_values = dv.data_ptr()
         a.packed_params = self.packed.data_ptr()
-        rs = self._record_struct(record)
+        rs = self._record_struct(record, B, H, W, D, nsrc)
         a.record = ctypes.pointer(rs)
         a.grad_cost = g.data_ptr()
         a.grad_ref = _ptr(grad_ref)

@@ -517,6 +517,8 @@ size_t aarmvs_train_record_bytes(int B, int H, int W, int which) {
     case 2: return T.z_slab * sizeof(float);
     case 3: return T.u_slab * sizeof(float);
     case 4: return T.stats_slab * sizeof(double);
+    case 5: return (size_t)B * H * W * 16;                        // t1 of one view
+    case 6: return (size_t)B * 3 * kSlots * 2 * sizeof(double);   // omega statistics of one view
     default: return 0;
   }
 }
@@ -551,7 +553,7 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   for (int v = 0; v < a->nsrc; ++v)
     if (!a->src_fea[v]) return fail(AARMVS_ERR_INVALID, "sweep: null src_fea pointer");
   const aarmvs_train_record* rec = a->record;
-  if (rec && (!rec->x || !rec->state || !rec->z || !rec->u || !rec->stats))
+  if (rec && (!rec->x || !rec->state || !rec->z || !rec->u || !rec->stats || !rec->t1 || !rec->ostats))
     return fail(AARMVS_ERR_INVALID, "sweep: training record with a null buffer");
   const TrainLayout T = train_layout(a->B, a->H, a->W);
 
@@ -651,6 +653,13 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     if ((e = launch_cost_x_group(ca, g, ws, g0, n, xs, ok >= 0 ? a->omega_out : nullptr, ok, cs)) !=
         hipSuccess)
       return sweep_fail(e, "sweep: cost slices");
+    // training: the group's omega conv output and statistics into the record (the backward
+    // reads them instead of recomputing the omega conv), before the next group reuses the slots
+    if (rec && ((e = hipMemcpyAsync(rec->t1 + (size_t)g0 * ws.t1_plane * 4, ws.t1, (size_t)n * ws.t1_plane * 16,
+                                    hipMemcpyDeviceToDevice, cs)) != hipSuccess ||
+                (e = hipMemcpyAsync(rec->ostats + (size_t)g0 * (ws.omega_stats_bytes / 8), ws.omega_stats,
+                                    (size_t)n * ws.omega_stats_bytes, hipMemcpyDeviceToDevice, cs)) != hipSuccess))
+      return sweep_fail(e, "sweep: record omega");
     if (aux && ((e = hipEventRecord(ev_cost[gi & 1], aux)) != hipSuccess ||
                 (e = hipStreamWaitEvent(stream, ev_cost[gi & 1], 0)) != hipSuccess))
       return sweep_fail(e, "sweep: event");
@@ -698,7 +707,7 @@ int aarmvs_sweep_backward(const aarmvs_backward_args* a, hipStream_t stream) {
       !a->record || !a->grad_cost || !a->workspace || !a->scratch)
     return fail(AARMVS_ERR_INVALID, "sweep_backward: null pointer argument or D < 1");
   const aarmvs_train_record* rec = a->record;
-  if (!rec->x || !rec->state || !rec->z || !rec->u || !rec->stats)
+  if (!rec->x || !rec->state || !rec->z || !rec->u || !rec->stats || !rec->t1 || !rec->ostats)
     return fail(AARMVS_ERR_INVALID, "sweep_backward: training record with a null buffer");
   for (int v = 0; v < a->nsrc; ++v)
     if (!a->src_fea[v]) return fail(AARMVS_ERR_INVALID, "sweep_backward: null src_fea pointer");

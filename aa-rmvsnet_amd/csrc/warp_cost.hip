@@ -1166,9 +1166,9 @@ hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t
 //   backwards, each needing a grid-wide sum per (plane, sample, view))
 //   dL/dwarp_v = 2 (warp_v - ref) dL/dsq_v;  dL/dref = -sum_v dL/dwarp_v;
 //   dL/dsrc_v = bilinear scatter of dL/dwarp_v (module.py:36: grid_sample's backward).
-// The forward's t1 and GroupNorm statistics are recomputed with launch_omega_group (bit
-// identical); every pixel's warp, sq and omega chain is recomputed with the forward's own
-// arithmetic (same helpers, contraction off), so the ReLU masks are the forward's.
+// The forward's t1 and GroupNorm statistics come from the training record (the forward copies
+// them there per group); every pixel's warp, sq and omega chain is recomputed with the
+// forward's own arithmetic (same helpers, contraction off), so the ReLU masks are the forward's.
 // Stages per group: cbw_chain<1> (dL/dw from the warp, dL/do; GN3 sums), <2> (GN2 sums),
 // <3> (GN1 sums), <4> (dL/dt1), each with a fixed-order reduce; cbw_feat (dL/dsq, the
 // feature gradients, the conv3x3 weight gradient).  Source gradients are scattered into an
@@ -1858,8 +1858,13 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   const SweepGeom g{a->B, a->H, a->W, a->nsrc, a->D, cu_count()};
   const CostArgs ca = cost_args_of(a);
   hipError_t e;
-  // the forward's omega conv output and GroupNorm statistics of the group's planes
-  if ((e = launch_omega_group(ca, g, c.ws, g0, n, s)) != hipSuccess) return e;
+  // the forward's omega conv output and GroupNorm statistics of the group's planes, as the
+  // recorded forward kept them
+  if ((e = hipMemcpyAsync(c.ws.t1, a->record->t1 + (size_t)g0 * c.ws.t1_plane * 4, (size_t)n * c.ws.t1_plane * 16,
+                          hipMemcpyDeviceToDevice, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(c.ws.omega_stats, a->record->ostats + (size_t)g0 * (c.ws.omega_stats_bytes / 8),
+                          (size_t)n * c.ws.omega_stats_bytes, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+    return e;
   CbwArgs ba{};
   ba.p = pipe_args_c8(ca, g, c.ws);
   group_strides(ba.p, c.ws, n);

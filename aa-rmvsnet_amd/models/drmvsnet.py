@@ -218,14 +218,13 @@ class _SweepTrain(torch.autograd.Function):
         D = depth_values.shape[1]
         cost = torch.empty(B, D, H, W, device=ref.device)
         rel = sweep.relative(ref_proj, src_projs, B)
-        rec = sweep.record_buffers(B, H, W, D, ref.device)
+        rec = sweep.record_buffers(B, H, W, D, ref.device, nsrc=nsrc)
         sweep(ref, srcs, ref_proj, src_projs, depth_values, want_depth=False, cost_out=cost,
               rel=rel, record=rec)
         ctx.sweep = sweep
         ctx.nsrc = nsrc
         ctx.nparams = len(params)
-        ctx.save_for_backward(ref, *srcs, rel, depth_values, rec["x"], rec["state"], rec["z"],
-                              rec["u"], rec["stats"])
+        ctx.save_for_backward(ref, *srcs, rel, depth_values, *(rec[k] for k in _ops.DepthSweep.RECORD_KEYS))
         return cost
 
     @staticmethod
@@ -235,7 +234,7 @@ class _SweepTrain(torch.autograd.Function):
         nsrc = ctx.nsrc
         ref, srcs = saved[0], list(saved[1:1 + nsrc])
         rel, dv = saved[1 + nsrc], saved[2 + nsrc]
-        rec = dict(zip(("x", "state", "z", "u", "stats"), saved[3 + nsrc:]))
+        rec = dict(zip(_ops.DepthSweep.RECORD_KEYS, saved[3 + nsrc:]))
         g_ref, g_srcs, g_par, _ = ctx.sweep.backward(ref, srcs, rel, dv, rec, grad_cost)
         g_params = [g_par[k] for k in _ops.SWEEP_KEYS]
         return (None, None, None, None, None, g_ref, *g_srcs, *g_params)

@@ -95,6 +95,9 @@ int aarmvs_homo_warp_backward(const float* grad_out, const float* rel_proj, cons
  *            [B][hid/4 channel quads][gates i,f,o,g][H*W][4];           D slabs
  *   3 u      the two deconvs' outputs before GroupNorm;                  D slabs
  *   4 stats  the two deconvs' GroupNorm statistics (fp64);               D slabs
+ *   5 t1     the omega conv output (4 ch) of ONE source view;        D x nsrc slabs
+ *   6 ostats the omega chain's GroupNorm statistics of ONE view (fp64); D x nsrc slabs
+ *   (5 and 6 let the backward skip recomputing the omega conv of every plane)
  * ~1 KB per pixel and plane at B = 1 (63 GB for 640x512, D = 192). */
 typedef struct aarmvs_train_record {
   float* x;
@@ -102,6 +105,8 @@ typedef struct aarmvs_train_record {
   float* z;
   float* u;
   double* stats;
+  float* t1;
+  double* ostats;
 } aarmvs_train_record;
 size_t aarmvs_train_record_bytes(int B, int H, int W, int which);
 

@@ -54,7 +54,7 @@ def _setup(B, N, H, W, D, seed, wseed):
 
 def _record_forward(sw, args, B, H, W, D):
     ref, srcs, ref_proj, src_projs, dv = args
-    rec = sw.record_buffers(B, H, W, D, DEV)
+    rec = sw.record_buffers(B, H, W, D, DEV, nsrc=len(srcs))
     rel = sw.relative(ref_proj, src_projs, B)
     cost = torch.empty(B, D, H, W, device=DEV)
     sw(ref, srcs, ref_proj, src_projs, dv, want_depth=False, cost_out=cost, rel=rel, record=rec)

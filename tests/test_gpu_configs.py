@@ -145,7 +145,7 @@ def test_gn_relu_fp16_range_guard_with_large_gamma():
     np.testing.assert_allclose(cost, ref["cost"].numpy(), atol=1e-3, rtol=1e-3)
     assert rel_l1(out["depth"].cpu().numpy(), ref["depth"].numpy()) <= 1e-3
     # the BPTT on the same weights
-    rec = sw.record_buffers(B, H, W, D, DEV)
+    rec = sw.record_buffers(B, H, W, D, DEV, nsrc=N - 1)
     rel = sw.relative(args[2], args[3], B)
     cvol = torch.empty(B, D, H, W, device=DEV)
     sw(*args, dv, want_depth=False, cost_out=cvol, rel=rel, record=rec)

@@ -94,7 +94,8 @@ int main() {
   a.d_begin = 0, a.nsrc = 2;
   CHECK(aarmvs_sweep(&a, nullptr) == AARMVS_ERR_INVALID);   // src_fea[1] null
   // training record: sizes grow with the frame; a record with a null buffer is rejected
-  CHECK(aarmvs_train_record_bytes(1, 8, 8, 1) > 0 && aarmvs_train_record_bytes(1, 8, 8, 5) == 0);
+  CHECK(aarmvs_train_record_bytes(1, 8, 8, 1) > 0 && aarmvs_train_record_bytes(1, 8, 8, 7) == 0);
+  CHECK(aarmvs_train_record_bytes(1, 8, 8, 5) == 8 * 8 * 16 && aarmvs_train_record_bytes(1, 8, 8, 6) > 0);
   CHECK(aarmvs_train_record_bytes(1, 8, 8, 2) < aarmvs_train_record_bytes(1, 16, 8, 2));
   CHECK(aarmvs_train_record_bytes(1, 6, 8, 0) == 0 && has_error());
   aarmvs_train_record rec;
@@ -115,6 +116,8 @@ int main() {
   CHECK(aarmvs_sweep_backward(&ba, nullptr) == AARMVS_ERR_INVALID);   // record buffers null
   float* rb = dummy;
   rec.x = rb, rec.state = rb, rec.z = rb, rec.u = rb, rec.stats = reinterpret_cast<double*>(rb);
+  CHECK(aarmvs_sweep_backward(&ba, nullptr) == AARMVS_ERR_INVALID);   // t1 / ostats null
+  rec.t1 = rb, rec.ostats = reinterpret_cast<double*>(rb);
   CHECK(aarmvs_sweep_backward(&ba, nullptr) == AARMVS_ERR_INVALID);   // grad_ref required
   ba.C = 16;
   CHECK(aarmvs_sweep_backward(&ba, nullptr) == AARMVS_ERR_INVALID);   // C != 32

@@ -20,7 +20,7 @@ f = torch.from_numpy(sc["features"]).cuda()
 proj = torch.from_numpy(sc["proj_matrices"])
 dv = torch.from_numpy(sc["depth_values"])
 ref, srcs = f[0], [f[v] for v in range(1, N)]
-rec = sw.record_buffers(B, H, W, D, "cuda")
+rec = sw.record_buffers(B, H, W, D, "cuda", nsrc=N - 1)
 rel = sw.relative(proj[:, 0], [proj[:, v] for v in range(1, N)], B)
 cost = torch.empty(B, D, H, W, device="cuda")
 sw(ref, srcs, proj[:, 0], [proj[:, v] for v in range(1, N)], dv, want_depth=False, cost_out=cost,
