@@ -1222,6 +1222,7 @@ struct CbwArgs {
   PipeArgs p;            // forward pipeline arguments (c8 features, rel, depths, params, t1, stats)
   const float* gx;       // [n][B][HW][32] dL/dx of the group's planes
   float* go;             // [n][B][nsrc][HW] dL/do (stage 1 out, later in)
+  float* wo;             // [n][B][nsrc][HW] the omega weights w (stage 1 out, for cbw_feat)
   float4* gt1;           // [n][B][nsrc][HW] dL/dt1 (stage 4 out)
   const double* gsum;    // [n][B][nsrc][3][2] GroupNorm backward sums (stage 1: GN3, 2: GN2, 3: GN1)
   double* part;          // [n][B][nsrc][pblk][32] per-block partial sums
@@ -1284,6 +1285,7 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
       dw = -dw / (float)nsrc;
       g_o = dw * c.w * (1.0f - c.w);
       gop[p] = g_o;
+      a.wo[kbv * HW + p] = c.w;
     } else {
       g_o = gop[p];
     }
@@ -1439,6 +1441,7 @@ struct CbfArgs {
   PipeArgs p;
   const float* gx;          // [n][B][HW][32]
   const float4* gt1;        // [n][B][nsrc][HW]
+  const float* w;           // [n][B][nsrc][HW] omega weights (cbw_chain<1>'s)
   float* gsrc8;             // [nsrc][B][4][HW][8] dL/dsrc (c8 layout) accumulated
   float* grefv;             // [nsrc][B][32][HW] dL/dref per view (NCHW) accumulated
   float* wpart;             // [4 chunks][nsrc][B][tiles][288] conv3x3 weight-gradient partials
@@ -1465,7 +1468,6 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
   unsigned short (*const lst)[kFbSlots] =
       reinterpret_cast<unsigned short (*)[kFbSlots]>(fbs + kFbLstOff);         // their tile indices
   float (*const wsum)[kWgSubs][16] = reinterpret_cast<float (*)[kWgSubs][16]>(fbs);   // after the loop
-  __shared__ GnStat gsk[kPlaneGroup][3];
   __shared__ int bred[4][4];
   __shared__ int bad;
   const PipeArgs& pa = a.p;
@@ -1483,13 +1485,7 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
     const float* w = P + pa.off_ow0 + (8 * c + j) * 9 + tap;
     w0q[tap][j] = make_float4(w[0], w[288], w[576], w[864]);
   }
-  if (tid < 3 * a.n) {
-    const int k = tid / 3, st = tid % 3;
-    gsk[k][st] = stat_read(pa.st_prev + k * pa.st_kstride + st_index(b, v, st, nsrc), 4.0 * HW);
-  }
   if (tid == 0) bad = 0;
-  OmegaP o;
-  load_omega(pa, P, o);
   const uint32_t fbytes = (uint32_t)((size_t)kC * HW * 4);
   const __amdgpu_buffer_rsrc_t rref = uniform_rsrc(pa.ref + (size_t)b * kC * HW, fbytes);
   const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(pa.src[v] + (size_t)b * kC * HW, fbytes);
@@ -1553,14 +1549,15 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
     return (i < 18 * 18 && gy >= 0 && gy < H && gxx >= 0 && gxx < W) ? a.gt1[kbv * HW + gy * W + gxx]
                                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
   };
-  float4 nh0, nh1, nt1, ngx0, ngx1, ns[4][2];
+  float4 nh0, nh1, ngx0, ngx1, ns[4][2];
+  float nw = 0.f;
   TapF ntf;
   auto fetch = [&](int k) {
     const size_t kbv = ((size_t)k * pa.B + b) * nsrc + v;
     nh0 = halo(hi0, kbv);
     nh1 = halo(hi1, kbv);
     if (in) {
-      nt1 = pa.t1_prev[k * pa.t1_kstride + ((size_t)b * nsrc + v) * HW + p];
+      nw = a.w[kbv * HW + p];
       const float* gxp = gxb + (((size_t)k * pa.B + b) * HW + p) * kC;
       ngx0 = *reinterpret_cast<const float4*>(gxp);
       ngx1 = *reinterpret_cast<const float4*>(gxp + 4);
@@ -1587,7 +1584,8 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
     if (mycell >= 0) cnt[mycell] = 0;
     mycell = -1;
     __syncthreads();
-    const float4 t1v = nt1, gx0 = ngx0, gx1 = ngx1;
+    const float wk = nw;
+    const float4 gx0 = ngx0, gx1 = ngx1;
     const TapF tf = ntf;
     float4 sv4[4][2];
 #pragma unroll
@@ -1608,10 +1606,8 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
       const float rv[8] = {rf0.x, rf0.y, rf0.z, rf0.w, rf1.x, rf1.y, rf1.z, rf1.w};
       sqv[0] = s0.x; sqv[1] = s0.y; sqv[2] = s0.z; sqv[3] = s0.w;
       sqv[4] = s1.x; sqv[5] = s1.y; sqv[6] = s1.z; sqv[7] = s1.w;
-      OmegaChain ch;
-      omega_chain(t1v, gsk[k], o, ch);
       const float gxv[8] = {gx0.x, gx0.y, gx0.z, gx0.w, gx1.x, gx1.y, gx1.z, gx1.w};
-      const float dsc = -(ch.w + 1.0f) / (float)nsrc;
+      const float dsc = -(wk + 1.0f) / (float)nsrc;
       float gsq[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) gsq[j] = dsc * gxv[j];
@@ -1790,6 +1786,7 @@ __global__ void __launch_bounds__(256) c8_to_nchw_kernel(const float* __restrict
 // ---- host side ----
 struct CostBwdLayout {
   float* go;
+  float* wo;
   float4* gt1;
   double* gsum;
   double* part;
@@ -1816,6 +1813,7 @@ static CostBwdLayout cost_bwd_layout(void* base, int B, int H, int W, int nsrc) 
   L.pblk = std::max(1, std::min((int)((HW + 4095) / 4096), 64));
   L.ntiles16 = ((W + kFbT - 1) / kFbT) * ((H + kFbT - 1) / kFbT);
   L.go = reinterpret_cast<float*>(take((size_t)G * B * nsrc * HW * 4));
+  L.wo = reinterpret_cast<float*>(take((size_t)G * B * nsrc * HW * 4));
   L.gt1 = reinterpret_cast<float4*>(take((size_t)G * B * nsrc * HW * 16));
   L.gsum = reinterpret_cast<double*>(take((size_t)G * B * nsrc * 6 * 8));
   L.part = reinterpret_cast<double*>(take((size_t)G * B * nsrc * L.pblk * 32 * 8));
@@ -1872,6 +1870,7 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   ba.p.st_prev = c.ws.omega_stats;
   ba.gx = gx;
   ba.go = L.go;
+  ba.wo = L.wo;
   ba.gt1 = L.gt1;
   ba.gsum = L.gsum;
   ba.part = L.part;
@@ -1928,6 +1927,7 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   fa.p = ba.p;
   fa.gx = gx;
   fa.gt1 = L.gt1;
+  fa.w = L.wo;
   fa.gsrc8 = L.gsrc8;
   fa.grefv = L.grefv;
   fa.wpart = L.wpart;
