@@ -624,7 +624,7 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
           hipSuccess)
         return sweep_fail(e, "sweep: c8 copy");
   }
-  // a record's statistics slabs accumulate from zero (gn_reduce fills slot 0 of each)
+  // a record's statistics slabs accumulate from zero (block 0 of cells 3 and 4 fills slot 0 of each)
   if (rec && (e = hipMemsetAsync(rec->stats + (size_t)a->d_begin * T.stats_slab, 0,
                                  (size_t)(a->d_end - a->d_begin) * T.stats_slab * sizeof(double),
                                  stream)) != hipSuccess)

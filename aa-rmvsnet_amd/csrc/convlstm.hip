@@ -36,7 +36,52 @@ struct ChanSrc {
   const double* stats;  // SRC_GNRELU: 2 statistics (groups of 8 channels)
   const float* gamma;
   const float* beta;
+  // SRC_GNRELU from the deconv's per-block partials (when set): every block reduces them as
+  // a fixed-order reduce does, block 0 stores the statistics at stats_out
+  const double* part;   // [nblk][4]: (sum, sumsq) of groups 0 and 1
+  int nblk;
+  double* stats_out;
 };
+
+// The GroupNorm table (gn[c] = rstd gamma_c, gn[16 + c] = beta_c - mean gn[c]) of a SRC_GNRELU
+// part.  From partials: strided sums over 256 lanes and a fixed tree (the reduce kernel these
+// replaced: bit-identical statistics), in `red` (>= 8 KB of LDS the staging has not used yet); all
+// threads of the block take part in the barriers.
+__device__ __forceinline__ void gn_table(const ChanSrc& s, float* gn, double* red, int tid, int H, int W) {
+  if (!s.part) {
+    if (tid < 16) {
+      const GnStat st = stat_read(s.stats + (tid >> 3) * kSlots * 2, 8.0 * H * W);
+      const float sc = st.rstd * s.gamma[tid];
+      gn[tid] = sc;
+      gn[16 + tid] = s.beta[tid] - st.mean * sc;
+    }
+    return;
+  }
+  if (tid < 256) {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = tid; i < s.nblk; i += 256)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += s.part[4 * i + j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[j * 256 + tid] = acc[j];
+  }
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[j * 256 + tid] += red[j * 256 + tid + o];
+    __syncthreads();
+  }
+  if (tid < 16) {
+    const int g = tid >> 3;
+    const GnStat st = gn_stat_from(red[2 * g * 256], red[(2 * g + 1) * 256], 8.0 * H * W);
+    const float sc = st.rstd * s.gamma[tid];
+    gn[tid] = sc;
+    gn[16 + tid] = s.beta[tid] - st.mean * sc;
+  }
+  if (blockIdx.x == 0 && tid < 4) s.stats_out[(tid >> 1) * kSlots * 2 + (tid & 1)] = red[tid * 256];
+  __syncthreads();   // the scratch is the staging's buffer
+}
 
 struct CellArgs {
   ChanSrc part[3];
@@ -448,14 +493,8 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     for (int i = tid; i < N4; i += C::THREADS) d[i] = s[i];
   }
 #pragma unroll
-  for (int p = 0; p < D::NP; ++p) {
-    if (D::MODE[p] == SRC_GNRELU && tid < 16) {
-      const GnStat st = stat_read(a.part[p].stats + (tid >> 3) * kSlots * 2, 8.0 * H * W);
-      const float sc = st.rstd * a.part[p].gamma[tid];
-      gn[tid] = sc;
-      gn[16 + tid] = a.part[p].beta[tid] - st.mean * sc;
-    }
-  }
+  for (int p = 0; p < D::NP; ++p)
+    if (D::MODE[p] == SRC_GNRELU) gn_table(a.part[p], gn, reinterpret_cast<double*>(in_hi), tid, H, W);
 
   const int tiles_x = (W + C::TW - 1) / C::TW, tiles_y = (H + C::TH - 1) / C::TH;
   const int ntiles = a.B * tiles_x * tiles_y;
@@ -548,14 +587,8 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
     for (int i = tid; i < N4; i += C::THREADS) d[i] = s[i];
   }
 #pragma unroll
-  for (int p = 0; p < D::NP; ++p) {
-    if (D::MODE[p] == SRC_GNRELU && tid < 16) {
-      const GnStat st = stat_read(a.part[p].stats + (tid >> 3) * kSlots * 2, 8.0 * H * W);
-      const float sc = st.rstd * a.part[p].gamma[tid];
-      gn[tid] = sc;
-      gn[16 + tid] = a.part[p].beta[tid] - st.mean * sc;
-    }
-  }
+  for (int p = 0; p < D::NP; ++p)
+    if (D::MODE[p] == SRC_GNRELU) gn_table(a.part[p], gn, reinterpret_cast<double*>(inb), tid, H, W);
   const int tiles_x = (W + C::TW - 1) / C::TW, tiles_y = (H + C::TH - 1) / C::TH;
   const int ntiles = a.B * tiles_x * tiles_y;
   auto coords = [&](int tile, int& b, int& y0, int& x0) {
@@ -892,37 +925,6 @@ __global__ void __launch_bounds__(256) deconv_mfma_kernel(const float* __restric
   }
 }
 
-// GroupNorm statistics of one deconv output per batch element (blockIdx.x) from its
-// deconv_px blocks' partials: strided sequential sums, then a fixed tree; the result goes
-// to slot 0 of each group's statistic (the other slots are zero).
-__global__ void __launch_bounds__(256) gn_reduce_kernel(const double* __restrict__ part, int nblk,
-                                                        double* __restrict__ stats,
-                                                        int stats_bstride) {
-  __shared__ double red[4][256];
-  const int b = blockIdx.x, t = threadIdx.x;
-  const double* pp = part + 4 * (size_t)b * nblk;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int i = t; i < nblk; i += 256)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] += pp[4 * i + j];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) red[j][t] = acc[j];
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (t < o)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) red[j][t] += red[j][t + o];
-    __syncthreads();
-  }
-  if (t == 0) {
-    double* st = stats + (size_t)b * stats_bstride;
-    st[0] = red[0][0];
-    st[1] = red[1][0];
-    st[kSlots * 2] = red[2][0];
-    st[kSlots * 2 + 1] = red[3][0];
-  }
-}
-
 // ---------------------------------------------------------------------------
 // conv_0 head (drmvsnet.py:117,165: Conv2d(8,1,3,pad 1)) fused with the online
 // winner-take-all update (drmvsnet.py:324-334) and the optional cost-volume store.
@@ -1228,8 +1230,10 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   CellArgs a2 = cell(2, {{io.h_new[1], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {io.h_prev[2], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
   if ((e = run_cell_h3<2>(a2, params + L.h3_scale_off + 2, cu, K_CELL2, s)) != hipSuccess) return e;
-  // GroupNorm statistics are per batch element, so the deconvs and the two cells that
-  // consume their normalised output are launched per batch element.
+  // GroupNorm statistics are per batch element, so the two cells that consume the deconvs'
+  // normalised outputs are launched per batch element; each reduces its element's deconv
+  // partials itself (gn_table) and block 0 stores the statistics.
+  int nblk0 = 0, nblk1 = 0;
   // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
   {
     const int Hi = H / 4, Wi = W / 4;
@@ -1240,18 +1244,15 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
                          params + L.pk_off[P_D0B], Hi, Wi, io.u0, ws.reg_part);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    ProfScope pr(s, K_GN_REDUCE);
-    hipLaunchKernelGGL(gn_reduce_kernel, dim3(B), dim3(256), 0, s, ws.reg_part, (int)(grid.x * grid.y),
-                       io.reg_stats + reg_stat_index(0, 0, 0),
-                       (int)(reg_stat_index(1, 0, 0) - reg_stat_index(0, 0, 0)));
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    nblk0 = (int)(grid.x * grid.y);
   }
   // cell 3: [gnrelu(u0), h1', h3] @ H/2
   for (int b = 0; b < B; ++b) {
     const double* st = io.reg_stats + reg_stat_index(b, 0, 0);
     const size_t hq = (size_t)(H / 2) * (W / 2);
     CellArgs a3 = cell(3, {{io.u0 + b * 16 * hq, 16, SRC_GNRELU, st, params + L.pk_off[P_D0GW],
-                            params + L.pk_off[P_D0GB]},
+                            params + L.pk_off[P_D0GB], ws.reg_part + (size_t)b * nblk0 * 4, nblk0,
+                            io.reg_stats + reg_stat_index(b, 0, 0)},
                            {io.h_new[1] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr},
                            {io.h_prev[3] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr}},
                        2);
@@ -1268,18 +1269,15 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
                          params + L.pk_off[P_D1B], Hi, Wi, io.u1, ws.reg_part);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    ProfScope pr(s, K_GN_REDUCE);
-    hipLaunchKernelGGL(gn_reduce_kernel, dim3(B), dim3(256), 0, s, ws.reg_part, (int)(grid.x * grid.y),
-                       io.reg_stats + reg_stat_index(0, 1, 0),
-                       (int)(reg_stat_index(1, 1, 0) - reg_stat_index(0, 1, 0)));
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    nblk1 = (int)(grid.x * grid.y);
   }
   // cell 4: [gnrelu(u1), h0', h4] @ H
   for (int b = 0; b < B; ++b) {
     const double* st = io.reg_stats + reg_stat_index(b, 1, 0);
     const size_t hw = (size_t)H * W;
     CellArgs a4 = cell(4, {{io.u1 + b * 16 * hw, 16, SRC_GNRELU, st, params + L.pk_off[P_D1GW],
-                            params + L.pk_off[P_D1GB]},
+                            params + L.pk_off[P_D1GB], ws.reg_part + (size_t)b * nblk1 * 4, nblk1,
+                            io.reg_stats + reg_stat_index(b, 1, 0)},
                            {io.h_new[0] + b * 16 * hw, 16, SRC_PLAIN, nullptr, nullptr, nullptr},
                            {io.h_prev[4] + b * 8 * hw, 8, SRC_PLAIN, nullptr, nullptr, nullptr}},
                        1);

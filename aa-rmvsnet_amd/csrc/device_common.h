@@ -163,6 +163,15 @@ __device__ __forceinline__ float gn_relu_bound(const float* gamma, const float* 
 struct GnStat {
   float mean, rstd;
 };
+__device__ __forceinline__ GnStat gn_stat_from(double s, double ss, double n) {
+  const double mean = s / n;
+  double var = ss / n - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  GnStat r;
+  r.mean = (float)mean;
+  r.rstd = (float)(1.0 / sqrt(var + (double)kGnEps));
+  return r;
+}
 __device__ __forceinline__ GnStat stat_read(const double* stat, double n) {
   // slots summed in index order; the loads are issued 16 slots at a time (two round trips)
   static_assert(kSlots % 16 == 0, "slot batches");
@@ -179,13 +188,7 @@ __device__ __forceinline__ GnStat stat_read(const double* stat, double n) {
       ss += v[i].y;
     }
   }
-  const double mean = s / n;
-  double var = ss / n - mean * mean;
-  var = var < 0.0 ? 0.0 : var;
-  GnStat r;
-  r.mean = (float)mean;
-  r.rstd = (float)(1.0 / sqrt(var + (double)kGnEps));
-  return r;
+  return gn_stat_from(s, ss, n);
 }
 
 }  // namespace aarmvs
