@@ -154,14 +154,17 @@ struct GateBwdArgs {
 };
 
 __global__ void __launch_bounds__(256) gate_bwd_kernel(GateBwdArgs a) {
-  const int hid = a.hid, q4 = hid / 4;
-  const size_t P = (size_t)a.B * a.H * a.W;
-  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  // 32-bit index arithmetic (B H W hid < 2^31, checked by the caller): 64-bit divisions by
+  // the runtime W, H were most of this streaming kernel's instructions
+  const int hid = a.hid, qs = hid == 16 ? 2 : 1;   // log2(hid / 4): hid is 16 or 8
+  const uint32_t HWc = (uint32_t)a.H * (uint32_t)a.W, P = (uint32_t)a.B * HWc;
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
   float m = 0.f;
-  if (t < P * q4) {
-    const size_t p = t / q4;
-    const int c0 = (int)(t % q4) * 4;
-    const int x = (int)(p % a.W), y = (int)((p / a.W) % a.H), b = (int)(p / ((size_t)a.W * a.H));
+  if (t < (P << qs)) {
+    const uint32_t p = t >> qs;
+    const int c0 = (int)(t & ((1u << qs) - 1u)) * 4;
+    const uint32_t b32 = p / HWc, pl = p - b32 * HWc, y32 = pl / (uint32_t)a.W;
+    const int b = (int)b32, y = (int)y32, x = (int)(pl - y32 * (uint32_t)a.W);
     float4 dh4 = *reinterpret_cast<const float4*>(a.gh + p * hid + c0);
     float dh[4] = {dh4.x, dh4.y, dh4.z, dh4.w};
     if (a.mode == 1) {
@@ -173,7 +176,10 @@ __global__ void __launch_bounds__(256) gate_bwd_kernel(GateBwdArgs a) {
         if (qy >= 0 && qy < a.H && qx >= 0 && qx < a.W) {
           const float g = gcb[(size_t)qy * a.W + qx];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) dh[i] = fmaf(a.whead[(c0 + i) * 9 + tap], g, dh[i]);
+          for (int i = 0; i < 4; ++i) {   // hid 8: c0 is 0 or 4 (wave-uniform loads, then a select)
+            const float w0 = a.whead[i * 9 + tap], w4 = a.whead[(4 + i) * 9 + tap];
+            dh[i] = fmaf(c0 ? w4 : w0, g, dh[i]);
+          }
         }
       }
     } else if (a.mode == 2) {
@@ -204,12 +210,11 @@ __global__ void __launch_bounds__(256) gate_bwd_kernel(GateBwdArgs a) {
       }
     }
     // the record's planar gate layout [B][hid/4 quads][4 gates][H*W][4] (CellArgs::z_out)
-    const size_t HWc = (size_t)a.H * a.W;
-    const float* zp = a.z + (size_t)b * 4 * hid * HWc + ((size_t)(c0 >> 2) * 4 * HWc + (p - (size_t)b * HWc)) * 4;
+    const float* zp = a.z + (size_t)b * 4 * hid * HWc + ((size_t)(c0 >> 2) * 4 * HWc + pl) * 4;
     const float4 zi = *reinterpret_cast<const float4*>(zp);
-    const float4 zf = *reinterpret_cast<const float4*>(zp + HWc * 4);
-    const float4 zo = *reinterpret_cast<const float4*>(zp + 2 * HWc * 4);
-    const float4 zg = *reinterpret_cast<const float4*>(zp + 3 * HWc * 4);
+    const float4 zf = *reinterpret_cast<const float4*>(zp + (size_t)HWc * 4);
+    const float4 zo = *reinterpret_cast<const float4*>(zp + (size_t)HWc * 8);
+    const float4 zg = *reinterpret_cast<const float4*>(zp + (size_t)HWc * 12);
     const float4 cp = *reinterpret_cast<const float4*>(a.c_prev + p * hid + c0);
     const float4 cn = *reinterpret_cast<const float4*>(a.c_new + p * hid + c0);
     const float4 gc4 = *reinterpret_cast<const float4*>(a.gc + p * hid + c0);
@@ -1156,6 +1161,7 @@ __global__ void zmax_group_kernel(unsigned* zmax, int n) {
 // ---------------------------------------------------------------------------
 static hipError_t run_gate_bwd(const GateBwdArgs& a, hipStream_t s) {
   const size_t n = (size_t)a.B * a.H * a.W * (a.hid / 4);
+  if ((size_t)a.B * a.H * a.W * a.hid >= (1ull << 31)) return hipErrorInvalidValue;   // 32-bit indices
   hipLaunchKernelGGL(gate_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
