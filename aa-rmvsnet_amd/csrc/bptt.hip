@@ -463,12 +463,7 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(GnbArgs a) {
       }
     }
   }
-  block_sum_d<36>(s, red);
-  if (threadIdx.x == 0) {
-    double* pp = a.part + ((size_t)b * gridDim.x + blockIdx.x) * 36;
-#pragma unroll
-    for (int i = 0; i < 36; ++i) pp[i] = s[i];
-  }
+  block_sum_d_store<36>(s, red, a.part + ((size_t)b * gridDim.x + blockIdx.x) * 36);
 }
 
 // The affine sums of a group's planes -> gacc, once per group (one block per column 4 .. 35):
@@ -505,7 +500,7 @@ __global__ void __launch_bounds__(256) gnb_affine_kernel(const double* __restric
 // dL/dh[ci] = sum_{ky,kx,co} gu[2y-1+ky][2x-1+kx][co] W[ci][co][ky][kx], with the GroupNorm+ReLU
 // backward applied on the fly: gu = rstd (g_xhat - S1/n - xhat S2/n).  The coarse pixel's own
 // 2 x 2 output quad's gu is stored (weight and bias gradients).  dL/dh is added into gh.
-// One thread per coarse pixel; weights [tap][co][ci] in LDS.
+// Four lanes per coarse pixel (one output-channel quarter each); weights [tap][co][ci] in LDS.
 // ---------------------------------------------------------------------------
 struct DcbArgs {
   const float* gr;       // [B][Ho][Wo][16]
@@ -563,45 +558,43 @@ __global__ void __launch_bounds__(256) deconv_bwd_kernel(DcbArgs a) {
     }
   }
   __syncthreads();
-  const int pidx = blockIdx.x * 256 + tid;
-  if (pidx >= a.Hi * a.Wi) return;
+  // four lanes per coarse pixel, lane q the output channels 4q .. 4q + 3: its dL/dy and u
+  // loads are one float4 each per tap, its dL/dh partial over those channels is summed over
+  // the quad on DPP, and lane q adds input channels 4q .. 4q + 3 into gh
+  const int pidx = blockIdx.x * 64 + (tid >> 2), q = tid & 3;
+  if (pidx >= a.Hi * a.Wi) return;   // whole quads leave together
   const int iy = pidx / a.Wi, ix = pidx % a.Wi;
-  const float* grb = a.gr + (size_t)b * Ho * Wo * 16;
-  const float* ub = a.u + (size_t)b * Ho * Wo * 16;
+  const float* grb = a.gr + (size_t)b * Ho * Wo * 16 + 4 * q;
+  const float* ub = a.u + (size_t)b * Ho * Wo * 16 + 4 * q;
+  const int grp = q >> 1;
   float acc[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll 1
+#pragma unroll 3
   for (int tap = 0; tap < 9; ++tap) {
     const int oy = 2 * iy - 1 + tap / 3, ox = 2 * ix - 1 + tap % 3;
     if (oy < 0 || oy >= Ho || ox < 0 || ox >= Wo) continue;
     const size_t o = ((size_t)oy * Wo + ox) * 16;
-    float gu[16];
+    const float4 g4 = *reinterpret_cast<const float4*>(grb + o);
+    const float4 u4 = *reinterpret_cast<const float4*>(ub + o);
+    const float G[4] = {g4.x, g4.y, g4.z, g4.w}, U[4] = {u4.x, u4.y, u4.z, u4.w};
+    float gu[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 g4 = *reinterpret_cast<const float4*>(grb + o + 4 * q);
-      const float4 u4 = *reinterpret_cast<const float4*>(ub + o + 4 * q);
-      const float G[4] = {g4.x, g4.y, g4.z, g4.w}, U[4] = {u4.x, u4.y, u4.z, u4.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = 4 * q + i, grp = c >> 3;
-        const float yv = fmaf(U[i], coef[0][c], coef[1][c]);
-        const float gxh = (yv > 0.f ? G[i] : 0.f) * a.gamma[c];
-        const float xh = (U[i] - coef[2][c]) * coef[3][c];
-        gu[c] = coef[3][c] * (gxh - gco[grp][0] - xh * gco[grp][1]);
-      }
+    for (int i = 0; i < 4; ++i) {
+      const int c = 4 * q + i;
+      const float yv = fmaf(U[i], coef[0][c], coef[1][c]);
+      const float gxh = (yv > 0.f ? G[i] : 0.f) * a.gamma[c];
+      const float xh = (U[i] - coef[2][c]) * coef[3][c];
+      gu[i] = coef[3][c] * (gxh - gco[grp][0] - xh * gco[grp][1]);
     }
-    if (tap == 4 || tap == 5 || tap == 7 || tap == 8) {   // the owned quad (2y + a, 2x + b)
-      float4* d = reinterpret_cast<float4*>(a.gu + (size_t)b * Ho * Wo * 16 + o);
+    if (tap == 4 || tap == 5 || tap == 7 || tap == 8)   // the owned quad (2y + a, 2x + b)
+      *reinterpret_cast<float4*>(a.gu + (size_t)b * Ho * Wo * 16 + o + 4 * q) = make_float4(gu[0], gu[1], gu[2], gu[3]);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) d[q] = make_float4(gu[4 * q], gu[4 * q + 1], gu[4 * q + 2], gu[4 * q + 3]);
-    }
-#pragma unroll
-    for (int co = 0; co < 16; ++co) {
-      const float g = gu[co];
+    for (int i = 0; i < 4; ++i) {
+      const float g = gu[i];
 #pragma unroll
       for (int c4 = 0; c4 < 4; ++c4) {
-        const float4 wv = wsh[(tap * 16 + co) * 4 + c4];
+        const float4 wv = wsh[(tap * 16 + 4 * q + i) * 4 + c4];
         acc[4 * c4 + 0] = fmaf(g, wv.x, acc[4 * c4 + 0]);
         acc[4 * c4 + 1] = fmaf(g, wv.y, acc[4 * c4 + 1]);
         acc[4 * c4 + 2] = fmaf(g, wv.z, acc[4 * c4 + 2]);
@@ -609,16 +602,24 @@ __global__ void __launch_bounds__(256) deconv_bwd_kernel(DcbArgs a) {
       }
     }
   }
-  float4* gh = reinterpret_cast<float4*>(a.gh + (((size_t)b * a.Hi + iy) * a.Wi + ix) * 16);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float4 o = gh[q];
-    o.x += acc[4 * q];
-    o.y += acc[4 * q + 1];
-    o.z += acc[4 * q + 2];
-    o.w += acc[4 * q + 3];
-    gh[q] = o;
+  for (int i = 0; i < 16; ++i) {   // (a0 + a1) + (a2 + a3) in every lane of the quad
+    float v = acc[i];
+    v += __int_as_float(dpp_i32<0xB1, 0xF>(0, __float_as_int(v)));
+    v += __int_as_float(dpp_i32<0x4E, 0xF>(0, __float_as_int(v)));
+    acc[i] = v;
   }
+  float4 mine = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  if (q == 1) mine = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  if (q == 2) mine = make_float4(acc[8], acc[9], acc[10], acc[11]);
+  if (q == 3) mine = make_float4(acc[12], acc[13], acc[14], acc[15]);
+  float4* gh = reinterpret_cast<float4*>(a.gh + (((size_t)b * a.Hi + iy) * a.Wi + ix) * 16 + 4 * q);
+  float4 o = *gh;
+  o.x += mine.x;
+  o.y += mine.y;
+  o.z += mine.z;
+  o.w += mine.w;
+  *gh = o;
 }
 
 // ---------------------------------------------------------------------------
@@ -1336,7 +1337,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     a.j = j;
     a.Hi = Ho / 2;
     a.Wi = Wo / 2;
-    hipLaunchKernelGGL(deconv_bwd_kernel, dim3((a.Hi * a.Wi + 255) / 256, B), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(deconv_bwd_kernel, dim3((a.Hi * a.Wi + 63) / 64, B), dim3(256), 0, s, a);
     return hipGetLastError();
   };
   const size_t xs = T.x_plane;   // floats per plane of gx

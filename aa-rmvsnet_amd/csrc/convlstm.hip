@@ -917,12 +917,7 @@ __global__ void __launch_bounds__(256) deconv_mfma_kernel(const float* __restric
       }
     }
   }
-  block_sum_d<4>(part, red);
-  if (tid == 0) {
-    double* pp = gn_part + 4 * (((size_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) pp[j] = part[j];
-  }
+  block_sum_d_store<4>(part, red, gn_part + 4 * (((size_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x));
 }
 
 // ---------------------------------------------------------------------------

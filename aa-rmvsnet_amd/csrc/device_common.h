@@ -140,6 +140,26 @@ __device__ __forceinline__ void block_sum_d(double (&v)[NV], double* red) {
   __syncthreads();
 }
 
+// block_sum_d whose block totals go straight to out[0 .. NV): thread i < NV sums value i over
+// the waves (same order as block_sum_d, so the same bits), instead of one thread summing all
+// NV values serially.
+template <int NV>
+__device__ __forceinline__ void block_sum_d_store(double (&v)[NV], double* red, double* out) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum_d(v[i]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[i * nw + wid] = v[i];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < NV) {
+    double s = 0.0;
+    for (int w = 0; w < nw; ++w) s += red[threadIdx.x * nw + w];
+    out[threadIdx.x] = s;
+  }
+}
+
 // Add (sum, sumsq) into the statistic's slot picked by the block id.
 __device__ __forceinline__ void stat_add(double* stat, double s, double ss) {
   double* slot = stat + 2 * (blockIdx.x % kSlots);

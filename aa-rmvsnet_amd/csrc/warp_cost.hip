@@ -1371,12 +1371,7 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
     }
     a.gt1[kbv * HW + p] = make_float4(g_t1[0], g_t1[1], g_t1[2], g_t1[3]);
   }
-  block_sum_d<NCOL>(s, red);
-  if (threadIdx.x == 0) {
-    double* pp = a.part + (kbv * a.pblk + blockIdx.x) * 32;
-#pragma unroll
-    for (int i = 0; i < NCOL; ++i) pp[i] = s[i];
-  }
+  block_sum_d_store<NCOL>(s, red, a.part + (kbv * a.pblk + blockIdx.x) * 32);
 }
 
 // GroupNorm-backward sums per (plane, b, v): columns 0, 1 of the stage's partial rows
