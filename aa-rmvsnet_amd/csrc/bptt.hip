@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <initializer_list>
 
 #include "device_common.h"
@@ -75,6 +76,8 @@ struct BpttLayout {
   float* gz[5];        // [G][Pk][4 hid] gate gradients of the group's planes
   unsigned* zmax;      // [5][G] float bits of max |gz| per (cell, group plane)
   float* gr[2];        // dL/d relu(GN(u_j)) of the current plane [B][Hu][Wu][16]
+  float* gr0b;         // gr[0]'s second buffer (odd planes: stage A writes it, stage B reads it)
+  float* gskip[2][2];  // [plane parity][cell 0, 1] cells 4 and 3's skip-input dL/dh0, dL/dh1 [Pk][16]
   float* gpool[2];     // dL/d maxpool(h0'), maxpool(h1') [B][H/2^(j+1)][.][16]
   float* gu[2];        // [G][B][Hu][Wu][16] dL/du_j (deconv outputs) of the group's planes
   float* gx;           // [G][B][H][W][32] dL/dx of the group's planes
@@ -112,6 +115,9 @@ BpttLayout bptt_layout(void* base, int B, int H, int W) {
   L.zmax = reinterpret_cast<unsigned*>(take(5 * G * 4));
   L.gr[0] = reinterpret_cast<float*>(take((size_t)B * (HW / 4) * 16 * 4));
   L.gr[1] = reinterpret_cast<float*>(take((size_t)B * HW * 16 * 4));
+  L.gr0b = reinterpret_cast<float*>(take((size_t)B * (HW / 4) * 16 * 4));
+  for (int q = 0; q < 2; ++q)
+    for (int k = 0; k < 2; ++k) L.gskip[q][k] = reinterpret_cast<float*>(take(L.cell_px[k] * 16 * 4));
   L.gpool[0] = reinterpret_cast<float*>(take((size_t)B * (HW / 4) * 16 * 4));
   L.gpool[1] = reinterpret_cast<float*>(take((size_t)B * (HW / 16) * 16 * 4));
   L.gu[0] = reinterpret_cast<float*>(take((size_t)G * B * (HW / 4) * 16 * 4));
@@ -141,6 +147,7 @@ struct GateBwdArgs {
   const float* c_prev;   // [P][hid]
   const float* c_new;    // [P][hid]
   const float* gh;       // [P][hid] dL/dh'
+  const float* gh_add;   // null or [P][hid]: a second term of dL/dh' (the skip input's), added to gh
   float* gc;             // [P][hid] dL/dc' in, dL/dc (previous plane) out
   float* gz;             // [P][4 hid] out
   unsigned* zmax;        // max |gz| (float bits)
@@ -166,6 +173,13 @@ __global__ void __launch_bounds__(256) gate_bwd_kernel(GateBwdArgs a) {
     const uint32_t b32 = p / HWc, pl = p - b32 * HWc, y32 = pl / (uint32_t)a.W;
     const int b = (int)b32, y = (int)y32, x = (int)(pl - y32 * (uint32_t)a.W);
     float4 dh4 = *reinterpret_cast<const float4*>(a.gh + p * hid + c0);
+    if (a.gh_add) {
+      const float4 s4 = *reinterpret_cast<const float4*>(a.gh_add + p * hid + c0);
+      dh4.x += s4.x;
+      dh4.y += s4.y;
+      dh4.z += s4.z;
+      dh4.w += s4.w;
+    }
     float dh[4] = {dh4.x, dh4.y, dh4.z, dh4.w};
     if (a.mode == 1) {
       // cost[q] = sum_{ci,tap} w[ci][tap] h4[q + off(tap)] + b  ->  dh4[p][ci] = sum_tap w[ci][tap] gcost[p - off(tap)]
@@ -1264,12 +1278,13 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
   CK(hipMemsetAsync(L.gacc, 0, PL.raw_total * 8, s));
   const int res_div[5] = {1, 2, 4, 2, 1};
   auto zslot = [&](int k, int slot) { return L.gz[k] + (size_t)slot * L.cell_px[k] * 4 * kCellHid[k]; };
-  auto gate = [&](int k, int slot, const UnetIO& io, int mode, int d) {
+  auto gate = [&](hipStream_t s, int k, int slot, const UnetIO& io, int mode, int d, const float* gh_add = nullptr) {
     GateBwdArgs a{};
     a.z = io.z[k];
     a.c_prev = io.c_prev[k];
     a.c_new = io.c_new[k];
     a.gh = L.gh[k];
+    a.gh_add = gh_add;
     a.gc = L.gc[k];
     a.gz = zslot(k, slot);
     a.zmax = L.zmax + k * G + slot;
@@ -1288,7 +1303,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     }
     return run_gate_bwd(a, s);
   };
-  auto dgrad = [&](int k, int slot, std::initializer_list<DgPart> parts) {
+  auto dgrad = [&](hipStream_t s, int k, int slot, std::initializer_list<DgPart> parts) {
     DgradArgs a{};
     a.gz = zslot(k, slot);
     a.zmax = L.zmax + k * G + slot;
@@ -1308,11 +1323,11 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     const size_t hwo = (size_t)(j ? H : H / 2) * (j ? W : W / 2);
     return std::max(1, std::min(L.gnb_nblk, (int)((hwo + 1023) / 1024)));
   };
-  auto deconv_bwd = [&](int j, int slot, const UnetIO& io) {
+  auto deconv_bwd = [&](hipStream_t s, int j, int slot, const UnetIO& io, float* gr) {
     const int Ho = j ? H : H / 2, Wo = j ? W : W / 2;
     const size_t hwo = (size_t)Ho * Wo;
     GnbArgs g{};
-    g.gr = L.gr[j];
+    g.gr = gr;
     g.u = j ? io.u1 : io.u0;
     g.stats = io.reg_stats;
     g.gamma = pk + PL.pk_off[j ? P_D1GW : P_D0GW];
@@ -1324,7 +1339,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     hipLaunchKernelGGL(gnb_partial_kernel, dim3(nblk, B), dim3(256), 0, s, g);
     CK(hipGetLastError());
     DcbArgs a{};
-    a.gr = L.gr[j];
+    a.gr = gr;
     a.u = g.u;
     a.stats = io.reg_stats;
     a.part = g.part;
@@ -1341,24 +1356,82 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     return hipGetLastError();
   };
   const size_t xs = T.x_plane;   // floats per plane of gx
+  // Two-stage plane pipeline on two streams: stage A of plane d (cells 4 and 3 and the
+  // deconv_1 backward) on the aux stream beside stage B of plane d + 1 (the deconv_0 backward,
+  // cells 2, 1, 0) on the caller's stream.  The only values crossing from A to B are cell 3's
+  // dL/d relu(GN(u_0)) and cells 4 and 3's skip-input gradients dL/dh0, dL/dh1: stored (not
+  // added into gh[0], gh[1], which stage B of plane d + 1 still owns) into per-parity buffers
+  // and added by cells 0 and 1's gate backward (the same single fp32 add: the same bits in
+  // either schedule).  Events: evA[p] "stage A of a parity-p plane done" (aux -> main),
+  // evB[p] "stage B of a parity-p plane done" (main -> aux: its parity buffers are free).
+  // AARMVS_BWD_PIPE=0 runs both stages on the caller's stream (A/B runs; tested bit-equal).
+  struct PipeSet {
+    int dev = -1;
+    hipStream_t aux = nullptr;
+    hipEvent_t ev[5] = {};   // evA[2], evB[2], fork
+  };
+  static thread_local PipeSet ps;
+  static const bool pipe_on = [] {
+    const char* v = getenv("AARMVS_BWD_PIPE");
+    return !(v && v[0] == '0');
+  }();
+  hipStream_t sa = s;
+  if (pipe_on) {
+    int dev = 0;
+    CK(hipGetDevice(&dev));
+    if (ps.dev != dev) {
+      ps.dev = -1;
+      CK(hipStreamCreateWithFlags(&ps.aux, hipStreamNonBlocking));
+      for (hipEvent_t& x : ps.ev) CK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+      ps.dev = dev;
+    }
+    sa = ps.aux;
+  }
+  hipEvent_t* evA = ps.ev;
+  hipEvent_t* evB = ps.ev + 2;
+  auto gr0_of = [&](int d) { return (d & 1) ? L.gr0b : L.gr[0]; };
   for (int g0 = ((D - 1) / G) * G; g0 >= 0; g0 -= G) {
     const int n = std::min(G, D - g0);
     CK(hipMemsetAsync(L.zmax, 0, 5 * G * 4, s));
-    for (int d = g0 + n - 1; d >= g0; --d) {
-      const int k = d - g0;
+    if (sa != s) {   // the aux stream starts after everything the group's stage A overwrites is consumed
+      CK(hipEventRecord(ps.ev[4], s));
+      CK(hipStreamWaitEvent(sa, ps.ev[4], 0));
+    }
+    auto stage_a = [&](int d) -> hipError_t {
+      const int k = d - g0, q = d & 1;
       const UnetIO io = unet_io_record(T, rec, d);
-      CK(gate(4, k, io, 1, d));
-      CK(dgrad(4, k, {{L.gr[1], 0, 16, 0}, {L.gh[0], 16, 16, 1}, {L.gh[4], 32, 8, 0}}));
-      CK(deconv_bwd(1, k, io));
-      CK(gate(3, k, io, 0, d));
-      CK(dgrad(3, k, {{L.gr[0], 0, 16, 0}, {L.gh[1], 16, 16, 1}, {L.gh[3], 32, 16, 0}}));
-      CK(deconv_bwd(0, k, io));
-      CK(gate(2, k, io, 0, d));
-      CK(dgrad(2, k, {{L.gpool[1], 0, 16, 0}, {L.gh[2], 16, 16, 0}}));
-      CK(gate(1, k, io, 2, d));
-      CK(dgrad(1, k, {{L.gpool[0], 0, 16, 0}, {L.gh[1], 16, 16, 0}}));
-      CK(gate(0, k, io, 2, d));
-      CK(dgrad(0, k, {{L.gx + (size_t)k * xs, 0, 32, 0}, {L.gh[0], 32, 16, 0}}));
+      CK(gate(sa, 4, k, io, 1, d));
+      CK(dgrad(sa, 4, k, {{L.gr[1], 0, 16, 0}, {L.gskip[q][0], 16, 16, 0}, {L.gh[4], 32, 8, 0}}));
+      CK(deconv_bwd(sa, 1, k, io, L.gr[1]));
+      CK(gate(sa, 3, k, io, 0, d));
+      CK(dgrad(sa, 3, k, {{gr0_of(d), 0, 16, 0}, {L.gskip[q][1], 16, 16, 0}, {L.gh[3], 32, 16, 0}}));
+      return hipSuccess;
+    };
+    auto stage_b = [&](int d) -> hipError_t {
+      const int k = d - g0, q = d & 1;
+      const UnetIO io = unet_io_record(T, rec, d);
+      CK(deconv_bwd(s, 0, k, io, gr0_of(d)));
+      CK(gate(s, 2, k, io, 0, d));
+      CK(dgrad(s, 2, k, {{L.gpool[1], 0, 16, 0}, {L.gh[2], 16, 16, 0}}));
+      CK(gate(s, 1, k, io, 2, d, L.gskip[q][1]));
+      CK(dgrad(s, 1, k, {{L.gpool[0], 0, 16, 0}, {L.gh[1], 16, 16, 0}}));
+      CK(gate(s, 0, k, io, 2, d, L.gskip[q][0]));
+      CK(dgrad(s, 0, k, {{L.gx + (size_t)k * xs, 0, 32, 0}, {L.gh[0], 32, 16, 0}}));
+      return hipSuccess;
+    };
+    // step i: stage A of plane g0 + n - 1 - i, stage B of the plane after it
+    for (int i = 0; i <= n; ++i) {
+      const int d = g0 + n - 1 - i;
+      if (i < n) {
+        if (sa != s && i >= 2) CK(hipStreamWaitEvent(sa, evB[d & 1], 0));   // B(d + 2) done
+        CK(stage_a(d));
+        if (sa != s) CK(hipEventRecord(evA[d & 1], sa));
+      }
+      if (i >= 1) {
+        if (sa != s) CK(hipStreamWaitEvent(s, evA[(d + 1) & 1], 0));
+        CK(stage_b(d + 1));
+        if (sa != s) CK(hipEventRecord(evB[(d + 1) & 1], s));
+      }
     }
     // ---- weight gradients of the group ----
     for (int k = 0; k < 5; ++k) {

@@ -1,0 +1,45 @@
+"""Helper of tests/test_gpu_bptt.py::test_backward_pipeline_schedule_is_bit_exact: one recorded
+training sweep and its backward (aarmvs_sweep_backward) at a small geometry spanning two plane
+groups (D = 20: 16 + 4, odd and even planes), printing a SHA-256 of every gradient's bytes and saving the
+source-feature gradients to argv[1] (.npy: their scatter flushes overlapping boxes with fp32
+atomics, so they agree between runs to rounding only).  Run once per schedule
+(AARMVS_BWD_PIPE=0: both backward stages on one stream; default: the two-stream plane
+pipeline)."""
+import hashlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "aa-rmvsnet_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from aarmvs import ops, synthetic as syn  # noqa: E402
+
+B, N, H, W, D = 1, 3, 96, 128, 20
+sc = syn.scene(B, N, H, W, D, seed=3)
+P = {k: torch.from_numpy(v).cuda() for k, v in syn.sweep_weights(5).items()}
+sw = ops.DepthSweep(P, "cuda")
+f = torch.from_numpy(sc["features"]).cuda()
+proj = torch.from_numpy(sc["proj_matrices"])
+dv = torch.from_numpy(sc["depth_values"])
+ref, srcs = f[0], [f[v] for v in range(1, N)]
+rec = sw.record_buffers(B, H, W, D, "cuda", nsrc=N - 1)
+rel = sw.relative(proj[:, 0], [proj[:, v] for v in range(1, N)], B)
+cost = torch.empty(B, D, H, W, device="cuda")
+sw(ref, srcs, proj[:, 0], [proj[:, v] for v in range(1, N)], dv, want_depth=False, cost_out=cost,
+   rel=rel, record=rec)
+torch.manual_seed(0)
+g = torch.randn_like(cost)
+g_ref, g_src, g_par, g_x = sw.backward(ref, srcs, rel, dv, rec, g, want_grad_x=True)
+torch.cuda.synchronize()
+for name, ts in (("ref", [g_ref]), ("src", g_src), ("params", [g_par[k] for k in sorted(g_par)]),
+                 ("x", [g_x])):
+    h = hashlib.sha256()
+    for t in ts:
+        h.update(t.detach().cpu().contiguous().numpy().tobytes())
+    print("DIGEST", name, h.hexdigest(), flush=True)
+np.save(sys.argv[1], torch.stack(g_src).cpu().numpy())
