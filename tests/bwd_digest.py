@@ -32,6 +32,8 @@ rel = sw.relative(proj[:, 0], [proj[:, v] for v in range(1, N)], B)
 cost = torch.empty(B, D, H, W, device="cuda")
 sw(ref, srcs, proj[:, 0], [proj[:, v] for v in range(1, N)], dv, want_depth=False, cost_out=cost,
    rel=rel, record=rec)
+torch.cuda.synchronize()
+print("DIGEST cost", hashlib.sha256(cost.cpu().numpy().tobytes()).hexdigest(), flush=True)
 torch.manual_seed(0)
 g = torch.randn_like(cost)
 g_ref, g_src, g_par, g_x = sw.backward(ref, srcs, rel, dv, rec, g, want_grad_x=True)
@@ -43,3 +45,5 @@ for name, ts in (("ref", [g_ref]), ("src", g_src), ("params", [g_par[k] for k in
         h.update(t.detach().cpu().contiguous().numpy().tobytes())
     print("DIGEST", name, h.hexdigest(), flush=True)
 np.save(sys.argv[1], torch.stack(g_src).cpu().numpy())
+if len(sys.argv) > 2:
+    np.save(sys.argv[2], g_ref.cpu().numpy())

@@ -196,20 +196,22 @@ def test_backward_is_deterministic_in_the_parameter_gradients():
 def test_backward_pipeline_schedule_is_bit_exact(tmp_path):
     """The backward's two-stream plane pipeline (stage A of plane d beside stage B of plane
     d + 1, bptt.hip) against the one-stream schedule (AARMVS_BWD_PIPE=0), over two plane
-    groups (D = 20): dL/dref, dL/dx and every parameter gradient bit for bit (the schedule
-    only moves kernels between streams; a missing dependency shows up as a differing digest);
-    dL/dsrc to rounding (its fp32 atomics differ between any two runs)."""
+    groups (D = 20; the forward's cost volume digest too): dL/dref, dL/dx and every parameter
+    gradient bit for bit (the schedule only moves kernels between streams; a missing
+    dependency shows up as a differing digest, so the pipelined run is repeated); dL/dsrc to
+    rounding (its fp32 atomics differ between any two runs)."""
     import subprocess
     import sys
     helper = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bwd_digest.py")
     out, src = {}, {}
-    for pipe in ("0", "1"):
+    for run, pipe in (("0", "0"), ("1", "1"), ("2", "1")):   # the pipelined schedule twice (races)
         env = dict(os.environ, AARMVS_BWD_PIPE=pipe)
-        f = str(tmp_path / f"src{pipe}.npy")
+        f = str(tmp_path / f"src{run}.npy")
         r = subprocess.run([sys.executable, helper, f], env=env, capture_output=True, text=True, timeout=100)
         assert r.returncode == 0, r.stderr[-2000:]
-        out[pipe] = [ln for ln in r.stdout.splitlines() if ln.startswith("DIGEST") and " src " not in ln]
-        assert len(out[pipe]) == 3, r.stdout
-        src[pipe] = np.load(f)
-    assert out["0"] == out["1"], out
-    np.testing.assert_allclose(src["1"], src["0"], rtol=1e-5, atol=1e-6 * float(np.abs(src["0"]).max()))
+        out[run] = [ln for ln in r.stdout.splitlines() if ln.startswith("DIGEST") and " src " not in ln]
+        assert len(out[run]) == 4, r.stdout
+        src[run] = np.load(f)
+    assert out["0"] == out["1"] == out["2"], out
+    for run in ("1", "2"):
+        np.testing.assert_allclose(src[run], src["0"], rtol=1e-5, atol=1e-6 * float(np.abs(src["0"]).max()))
