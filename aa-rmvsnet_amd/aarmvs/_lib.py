@@ -124,6 +124,11 @@ SIGNATURES = {
     "aarmvs_wta_update": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                   c_void_p]),
     "aarmvs_fusion_filter": (c_int, [ctypes.POINTER(FusionArgs), c_void_p]),
+    "aarmvs_evidential_epilogue": (c_int, [ctypes.POINTER(c_void_p), c_void_p, c_int, c_int, c_void_p,
+                                           c_void_p, c_void_p]),
+    "aarmvs_evidential_epilogue_backward": (c_int, [ctypes.POINTER(c_void_p), c_void_p, c_int, c_int,
+                                                    c_void_p, c_void_p, ctypes.POINTER(c_void_p),
+                                                    c_void_p]),
     "aarmvs_profile_enable": (None, [c_int]),
     "aarmvs_profile_reset": (None, []),
     "aarmvs_profile_kernel_count": (c_int, []),

@@ -234,6 +234,54 @@ def softmax_depth(cost: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _ptr3(ts) -> ctypes.Array:
+    return (ctypes.c_void_p * 3)(*[t.data_ptr() for t in ts])
+
+
+class _EvidentialEpilogue(torch.autograd.Function):
+    """The evidential head's epilogue on HIP (aarmvs_evidential_epilogue, evidential/models.py:
+    385-459): the three classifier outputs [1,4,D,H,W] -> (evidential [4,H,W], prob_combine
+    [1,D,H,W]); backward through aarmvs_evidential_epilogue_backward (no gradient to the depths)."""
+
+    @staticmethod
+    def forward(ctx, dv, h0, h1, h2):
+        heads = [h.contiguous() for h in (h0, h1, h2)]
+        _require_device(*heads)
+        B, C, D, H, W = heads[0].shape
+        if B != 1 or C != 4 or any(tuple(h.shape) != (1, 4, D, H, W) for h in heads):
+            raise ValueError(f"evidential epilogue: heads must be [1, 4, D, H, W], got "
+                             f"{[tuple(h.shape) for h in heads]}")
+        dvc = dv.reshape(-1).float().contiguous()
+        if dvc.numel() != D:
+            raise ValueError(f"evidential epilogue: {dvc.numel()} depth values for D = {D}")
+        ev = torch.empty(4, H, W, device=heads[0].device)
+        pc = torch.empty(1, D, H, W, device=heads[0].device)
+        check(lib().aarmvs_evidential_epilogue(_ptr3(heads), dvc.data_ptr(), D, H * W, ev.data_ptr(),
+                                               pc.data_ptr(), _stream()), "evidential_epilogue")
+        ctx.save_for_backward(dvc, *heads)
+        return ev, pc
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g_ev, g_pc):
+        dvc, *heads = ctx.saved_tensors
+        D, H, W = heads[0].shape[2:]
+        g_ev = g_ev.contiguous() if g_ev is not None else None
+        g_pc = g_pc.contiguous() if g_pc is not None else None
+        gh = [torch.empty_like(h) for h in heads]
+        check(lib().aarmvs_evidential_epilogue_backward(_ptr3(heads), dvc.data_ptr(), D, H * W,
+                                                        _ptr(g_ev), _ptr(g_pc), _ptr3(gh), _stream()),
+              "evidential_epilogue_backward")
+        return (None, *gh)
+
+
+@_on_tensor_device
+def evidential_epilogue(h0: torch.Tensor, h1: torch.Tensor, h2: torch.Tensor, depth_values: torch.Tensor):
+    """(evidential [4,H,W], prob_combine [1,D,H,W]) from classif0/1/2's outputs [1,4,D,H,W]
+    (D = 32), differentiable w.r.t. the three head outputs."""
+    return _EvidentialEpilogue.apply(depth_values, h0, h1, h2)
+
+
 @_on_tensor_device
 def wta_update(cost: torch.Tensor, depth_d: torch.Tensor, max_prob: torch.Tensor,
                depth_map: torch.Tensor, exp_sum: torch.Tensor) -> None:

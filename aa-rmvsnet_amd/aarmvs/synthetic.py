@@ -69,6 +69,17 @@ def scene(B: int, N: int, H: int, W: int, D: int, seed: int = 0, C: int = 32,
     return out
 
 
+def depth_targets(depth_values: np.ndarray, H: int, W: int, seed: int):
+    """Training targets for a scene (dtu_yao.py's depth / mask, synthetic): depth_gt uniform
+    over the hypothesis range, ~70% valid pixels.  Returns (depth_gt [B,H,W], mask [B,H,W])."""
+    B = depth_values.shape[0]
+    rng = np.random.default_rng(seed + 1000)
+    lo, hi = float(depth_values.min()), float(depth_values.max())
+    depth_gt = rng.uniform(lo, hi, (B, H, W)).astype(np.float32)
+    mask = (rng.uniform(0, 1, (B, H, W)) > 0.3).astype(np.float32)
+    return depth_gt, mask
+
+
 def _fan_in(shape, name: str) -> int:
     if len(shape) <= 1:
         return 1

@@ -198,6 +198,11 @@ hipError_t launch_finalize(const SweepGeom& g, const Workspace& ws, float* depth
                            float* conf_out, hipStream_t s);
 hipError_t launch_softmax_depth(const float* cost, float* prob, int B, int D, int HW,
                                 hipStream_t s);
+// the evidential head's epilogue (evidential.hip): forward when g_head is null (ev [4][HW],
+// pc [D][HW]), else the backward from g_ev / g_pc (either may be null) into g_head
+hipError_t launch_evidential(const float* const head[3], const float* dv, int D, int HW, float* ev,
+                             float* pc, const float* g_ev, const float* g_pc, float* const g_head[3],
+                             hipStream_t s);
 // GroupNorm of NCHW [B][C][HW] fp32 (group_norm.hip): mean_rstd [B][G][2]; gamma / beta may
 // be null (1 / 0); scratch of gn_scratch_bytes(B, C, HW); bwd also writes s1 = sum dy xhat and
 // s2 = sum dy per (b, c) (the per-sample dgamma / dbeta terms)
@@ -262,7 +267,7 @@ enum KernelId : int {
   K_COST_X, K_OMEGA_CONV, K_FUSION, K_OMEGA1, K_OMEGA2,
   K_CELL0, K_CELL1, K_CELL2, K_CELL3, K_CELL4,
   K_DECONV0, K_DECONV1, K_HEAD_WTA, K_FINALIZE, K_SOFTMAX, K_WARP, K_TO_C8, K_STAT_REDUCE,
-  K_GN_REDUCE, K_COUNT
+  K_GN_REDUCE, K_EVIDENTIAL, K_COUNT
 };
 extern bool g_prof_on;
 void prof_mark(hipStream_t s, int id, bool begin);

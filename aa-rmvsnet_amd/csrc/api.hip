@@ -90,7 +90,7 @@ static const char* kKernelNames[K_COUNT] = {
     "cost_x", "omega_conv", "fusion", "omega_stats1", "omega_stats2",
     "lstm_cell0", "lstm_cell1", "lstm_cell2", "lstm_cell3", "lstm_cell4",
     "deconv0", "deconv1", "head_wta", "finalize", "softmax_depth", "homo_warp", "to_c8",
-    "omega_stat_reduce", "gn_reduce"};
+    "omega_stat_reduce", "gn_reduce", "evidential"};
 
 static hipEvent_t prof_event() {
   if (g_prof_used == g_prof_pool.size()) {
@@ -889,6 +889,32 @@ int aarmvs_softmax_depth(const float* cost, float* prob, int B, int D, int HW, h
     return fail(AARMVS_ERR_INVALID, "softmax_depth: bad arguments");
   hipError_t e = launch_softmax_depth(cost, prob, B, D, HW, stream);
   return e == hipSuccess ? AARMVS_OK : hip_fail(e, "softmax_depth");
+}
+
+int aarmvs_evidential_epilogue(const float* const head[3], const float* depth_values, int D, int HW,
+                               float* evidential, float* prob_combine, hipStream_t stream) {
+  if (!head || !head[0] || !head[1] || !head[2] || !depth_values || !evidential || !prob_combine ||
+      HW < 1)
+    return fail(AARMVS_ERR_INVALID, "evidential_epilogue: null pointer or HW < 1");
+  if (D != AARMVS_EVIDENTIAL_D)
+    return fail(AARMVS_ERR_INVALID, "evidential_epilogue: D must be 32 (the head's maxdisp)");
+  hipError_t e = launch_evidential(head, depth_values, D, HW, evidential, prob_combine, nullptr,
+                                   nullptr, nullptr, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "evidential_epilogue");
+}
+
+int aarmvs_evidential_epilogue_backward(const float* const head[3], const float* depth_values, int D,
+                                        int HW, const float* grad_evidential,
+                                        const float* grad_prob_combine, float* const grad_head[3],
+                                        hipStream_t stream) {
+  if (!head || !head[0] || !head[1] || !head[2] || !depth_values || !grad_head || !grad_head[0] ||
+      !grad_head[1] || !grad_head[2] || HW < 1)
+    return fail(AARMVS_ERR_INVALID, "evidential_epilogue_backward: null pointer or HW < 1");
+  if (D != AARMVS_EVIDENTIAL_D)
+    return fail(AARMVS_ERR_INVALID, "evidential_epilogue_backward: D must be 32 (the head's maxdisp)");
+  hipError_t e = launch_evidential(head, depth_values, D, HW, nullptr, nullptr, grad_evidential,
+                                   grad_prob_combine, grad_head, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "evidential_epilogue_backward");
 }
 
 }  // extern "C"

@@ -722,13 +722,16 @@ __global__ void __launch_bounds__(512) wgrad2_kernel(WgradArgs a) {
   const int ntile = a.B * tiles_x * tiles_y;
   const int nitem = ntile * a.nplanes;
   // staging scale of a chunk
-  // GroupNorm+ReLU chunks: the nominal 16 lowered so that bound 16 2^-e <= 2^15 (the forward
-  // cells' range guard, gn_relu_bound)
+  // GroupNorm+ReLU chunks: bound 2^-e in [2^14, 2^15) (the forward cells' staging scale,
+  // gn_relu_bound), so that neither fp16 overflows nor the lo parts of small values go subnormal
   auto chunk_scale = [&](const WgChunk& ch) {
     if (ch.bound) return ldexpf(1.0f, -scale_exp(*ch.bound));
     if (ch.mode == WG_GNRELU) {
-      const float b16 = gn_relu_bound(ch.gamma - 8 * ch.gn0, ch.beta - 8 * ch.gn0, 8.0 * a.H * a.W) * ch.scale;
-      if (b16 > 32768.0f) return ch.scale * ldexpf(1.0f, -(ilogbf(b16) >= 134 ? 120 : ilogbf(b16) - 14));
+      const float bnd = gn_relu_bound(ch.gamma - 8 * ch.gn0, ch.beta - 8 * ch.gn0, 8.0 * a.H * a.W);
+      if (bnd > 0.0f) {
+        const int k = ilogbf(bnd);
+        return ldexpf(1.0f, -(k >= 134 ? 120 : (k < -100 ? -114 : k - 14)));
+      }
     }
     return ch.scale;
   };

@@ -97,29 +97,31 @@ struct CellArgs {
   int B, H, W;          // cell resolution
 };
 
-// fp16 range guard of cell 0's input (the cost slice x = -sum (1 + w) sq / nsrc is
-// unbounded, unlike h, pooled h and the GroupNorm outputs of the other parts): x is staged
-// as x 2^-e and the partial sums of the x chunks are rescaled by 2^e (exact) before the h
-// chunk is accumulated, with e >= 0 the smallest exponent that keeps bound 2^-e <= 2^15
-// (fp16's largest finite is 65504).  e = 0 whenever |x| <= 32768: bit-identical to no guard.
-__device__ __forceinline__ int xguard_exp(const unsigned* xb) {
-  if (!xb) return 0;
-  const float bound = __uint_as_float(*xb);
-  if (bound <= 32768.0f) return 0;
-  const int k = ilogbf(bound);   // 2^k <= bound < 2^(k+1); INT_MAX for inf
-  return k >= 134 ? 120 : k - 14;
-}
+// Staging scales of the split-fp16 operands.  An fp32 value a is staged as fp16 hi + lo with
+// lo = a - hi; lo keeps fp16's 11 significant bits only while it is a normal number
+// (|lo| >= 2^-14, i.e. |a| >~ 2^-3): below that its quantum is the subnormal step 2^-24, an
+// absolute error that, for the h values of typical magnitude 1e-2, is 10-50x fp32's rounding
+// and was the source of the BPTT's excess error in the omega network's gradients.
+// So every part is staged at a power-of-two scale that puts its largest possible magnitude
+// just under fp16's range, and the accumulators are rescaled (exactly) between parts:
+//  * h and pooled h (|h| < 1: sigmoid x tanh): x 2^kHScaleExp;
+//  * cell 0's x (the cost slice x = -sum (1 + w) sq / nsrc, bounded by the sweep's ws.xbound)
+//    and cells 3 and 4's GroupNorm+ReLU part (deConvGnReLU's output, module.py:286-287,
+//    bounded by gn_relu_bound: |xhat| <= sqrt(n - 1) for n values of mean 0 and unit biased
+//    variance, Samuelson's inequality): x 2^-e with bound 2^-e in [2^14, 2^15) (fp16's largest
+//    finite is 65504), e of either sign.
+constexpr int kHScaleExp = 12;
 
-// fp16 range guard of the GroupNorm(2,16)+ReLU part of cells 3 and 4 (deConvGnReLU's output,
-// module.py:286-287): y = relu(gamma xhat + beta) with xhat bounded by sqrt(n - 1) for n values
-// of mean 0 and unit biased variance (Samuelson's inequality), so |y| <= gn_relu_bound(); the part is
-// staged as y 2^-e and its partial sums rescaled by 2^e, as cell 0's x.  e = 0 (bit-identical
-// to no guard) whenever the bound is <= 32768: |gamma| below ~8-16 at the BASELINE sizes.
+__device__ __forceinline__ int guard_exp_of(float bound) {
+  if (!(bound > 0.0f)) return 0;
+  const int k = ilogbf(bound);   // 2^k <= bound < 2^(k+1); INT_MAX for inf
+  return k >= 134 ? 120 : (k < -100 ? -114 : k - 14);
+}
+__device__ __forceinline__ int xguard_exp(const unsigned* xb) {
+  return xb ? guard_exp_of(__uint_as_float(*xb)) : -kHScaleExp;
+}
 __device__ __forceinline__ int gguard_exp(const float* gamma, const float* beta, int H, int W) {
-  const float bound = gn_relu_bound(gamma, beta, 8.0 * H * W);
-  if (bound <= 32768.0f) return 0;
-  const int k = ilogbf(bound);
-  return k >= 134 ? 120 : k - 14;
+  return guard_exp_of(gn_relu_bound(gamma, beta, 8.0 * H * W));
 }
 
 constexpr int kMaxParts = 3;
@@ -230,8 +232,8 @@ struct H3PixStager {
   static_assert(NI <= 32, "item mask holds 32 items");
   float val[NI][8][4];   // [item][channel][POOL window: fine (2y,2x) (2y,2x+1) (2y+1,2x) (2y+1,2x+1)]
   uint32_t in_mask;      // bit j: item j is an in-image pixel of valid channels
-  float xs = 1.0f;       // 2^-e of the fp16 range guard of part 0: cell 0's x (xguard_exp), cells
-                         // 3 and 4's GroupNorm+ReLU part (gguard_exp)
+  float xs = 1.0f;       // 2^-e staging scale of part 0: cell 0's x (xguard_exp), cells 3 and
+                         // 4's GroupNorm+ReLU part (gguard_exp); h parts: 2^kHScaleExp
 
   template <int CH>
   __device__ __forceinline__ void load(const CellArgs& a, int b, int y0, int x0, int tid) {
@@ -286,14 +288,16 @@ struct H3PixStager {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float x;
+          constexpr float HS = (float)(1 << kHScaleExp);
           if (MODE == SRC_POOL) {
-            x = fmaxf(fmaxf(val[j][k][0], val[j][k][1]), fmaxf(val[j][k][2], val[j][k][3]));
+            x = fmaxf(fmaxf(val[j][k][0], val[j][k][1]), fmaxf(val[j][k][2], val[j][k][3])) * HS;
           } else if (MODE == SRC_GNRELU) {
             const int lc = LC0 + 8 * h + k;
             x = fmaxf(val[j][k][0] * gn[lc] + gn[16 + lc], 0.0f) * xs;
+          } else if constexpr (KIND == 0 && C::chunk_part(CH) == 0) {
+            x = val[j][k][0] * xs;
           } else {
-            x = val[j][k][0];
-            if constexpr (KIND == 0 && C::chunk_part(CH) == 0) x *= xs;
+            x = val[j][k][0] * HS;
           }
           v[k] = in ? x : 0.0f;
         }
@@ -308,8 +312,9 @@ struct H3PixStager {
   }
 };
 
-// Before the MFMAs of chunk CH: undo the range guard's scale of part 0 (cell 0's x, cells 3 and
-// 4's GroupNorm+ReLU part) on its chunks' partial sums (CH is the first chunk past part 0).
+// Before the MFMAs of chunk CH: bring part 0's partial sums (cell 0's x, cells 3 and 4's
+// GroupNorm+ReLU part, staged x 2^-e) to the h parts' scale 2^kHScaleExp (CH is the first chunk
+// past part 0); the epilogue undoes 2^kHScaleExp with the weight scale.
 template <class C, int KIND, int CH>
 __device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], float xr) {
   if constexpr ((KIND == 0 || C::D::MODE[0] == SRC_GNRELU) && CH > 0 && C::chunk_part(CH) != 0 &&
@@ -483,7 +488,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, W = a.W;
-  const float inv_scale = *inv_scale_ptr;
+  const float inv_scale = ldexpf(*inv_scale_ptr, -kHScaleExp);   // weight scale and staging scale
   // split-fp16 weights -> LDS once per block
   {
     const float4* s = reinterpret_cast<const float4*>(a.wpk);
@@ -508,7 +513,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
   const int xe = KIND == 0 ? xguard_exp(a.xbound)
                  : D::MODE[0] == SRC_GNRELU ? gguard_exp(a.part[0].gamma, a.part[0].beta, H, W) : 0;
   st.xs = ldexpf(1.0f, -xe);
-  const float xr = ldexpf(1.0f, xe);
+  const float xr = ldexpf(1.0f, xe + kHScaleExp);   // part 0's units -> the h parts' 2^kHScaleExp
   int tile = blockIdx.x;
   if (tile < ntiles && !(ABL & 2)) {
     int b, y0, x0;
@@ -578,7 +583,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, W = a.W;
-  const float inv_scale = *inv_scale_ptr;
+  const float inv_scale = ldexpf(*inv_scale_ptr, -kHScaleExp);   // weight scale and staging scale
   {
     const float4* s = reinterpret_cast<const float4*>(a.wpk);
     float4* d = reinterpret_cast<float4*>(wl_hi);
@@ -603,7 +608,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
   const int xe = KIND == 0 ? xguard_exp(a.xbound)
                  : D::MODE[0] == SRC_GNRELU ? gguard_exp(a.part[0].gamma, a.part[0].beta, H, W) : 0;
   st.xs = ldexpf(1.0f, -xe);
-  const float xr = ldexpf(1.0f, xe);
+  const float xr = ldexpf(1.0f, xe + kHScaleExp);   // part 0's units -> the h parts' 2^kHScaleExp
   int b, y0, x0;
   coords(tile, b, y0, x0);
   if (!(ABL & 2)) st.template load<0>(a, b, y0, x0, tid);

@@ -711,13 +711,14 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   };
   // this lane's reference pixel in the c8 image (past the buffer: zeros)
   const uint32_t rpix = in_img ? (uint32_t)(gy * W + gx) : fbytes / 32u;
-  // sq guard: sq 2^-e <= 2^15 (sq <= 4 max|f|^2 <= bound)
+  // sq staging scale: bound 2^-e in [2^14, 2^15) (sq <= 4 max|f|^2 <= bound), e of either
+  // sign, so that fp16 cannot overflow and the lo parts of small sq stay normal numbers
   int e = 0;
   {
     const float bound = __uint_as_float(*xbound);
-    if (bound > 32768.0f) {
+    if (bound > 0.0f) {
       const int k = ilogbf(bound);
-      e = k >= 134 ? 120 : k - 14;
+      e = k >= 134 ? 120 : (k < -100 ? -114 : k - 14);
     }
   }
   const float sqs = ldexpf(1.0f, -e);

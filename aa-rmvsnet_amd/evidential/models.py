@@ -212,12 +212,24 @@ class EvidentialModule(nn.Module):
         out1 = self.dres2(mid)
         out2 = self.dres3(out1)
 
+        outs = [head(feat) for head, feat in ((self.classif0, cost0), (self.classif1, out1),
+                                              (self.classif2, out2))]
+        if input.is_cuda:
+            # the epilogue (softmax, disparity_regression, softplus evidence, moe_nig, mean) as
+            # one HIP kernel (aarmvs_evidential_epilogue); the heads are at [md, H, W] already,
+            # where get_pred / get_logits' align_corners=True resampling is the identity
+            if any(tuple(o.shape[2:]) != (md, H, W) for o in outs):
+                raise EvidentialShapeError(f"evidential head: classifier outputs "
+                                           f"{[tuple(o.shape) for o in outs]} are not at [{md}, {H}, {W}]")
+            from aarmvs import ops as _ops
+            return _ops.evidential_epilogue(*outs, depth_value)
+
         def upsample(t):
             return F.interpolate(t, [md, H, W], mode="trilinear", align_corners=True).squeeze(1)
 
         ests, probs = [], []
-        for head, feat in ((self.classif0, cost0), (self.classif1, out1), (self.classif2, out2)):
-            cost, logla, logalpha, logbeta = torch.split(head(feat), 1, dim=1)
+        for o in outs:
+            cost, logla, logalpha, logbeta = torch.split(o, 1, dim=1)
             prob = F.softmax(upsample(cost), dim=1)
             pred = disparity_regression(prob, depth_value)
             # logits of the evidential parameters, weighted by this level's probabilities

@@ -274,6 +274,28 @@ typedef struct aarmvs_fusion_args {
 int aarmvs_fusion_filter(const aarmvs_fusion_args* args, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Epilogue of the evidential head (evidential/models.py:385-459): from the three
+ * classifier outputs head[i] = classif_i(...) [1][4][D][H][W] (channels: cost, log nu, log
+ * alpha, log beta; at the head's full [maxdisp, H, W] resolution, where get_pred / get_logits'
+ * align_corners=True trilinear resampling is the identity) and depth_values [D]:
+ *   prob_i = softmax_D(cost_i) (:421), pred_i = sum_d prob_i depth_values (disparity_regression,
+ *   :40-45), nu_i / alpha_i / beta_i = softplus(sum_d prob_i logit_i) (+1 for alpha; :426-430,
+ *   :281-285), the NIG mixture moe_nig(moe_nig(e0, e1), e2) (:287-304) -> evidential [4][H*W]
+ *   = (gamma, nu, alpha, beta), and prob_combine [D][H*W] = the mean of the three prob_i
+ *   (:457-458).  B == 1 and D == AARMVS_EVIDENTIAL_D only, the reference head's limits
+ *   (SURVEY F2).  HW = H * W.  The backward (for the training losses through the head,
+ *   :517-558) takes dL/d evidential and dL/d prob_combine (either may be NULL: zero) and
+ *   overwrites grad_head[i] [1][4][D][H][W]; no gradient flows to depth_values.
+ * ------------------------------------------------------------------------- */
+#define AARMVS_EVIDENTIAL_D 32
+int aarmvs_evidential_epilogue(const float* const head[3], const float* depth_values, int D, int HW,
+                               float* evidential, float* prob_combine, hipStream_t stream);
+int aarmvs_evidential_epilogue_backward(const float* const head[3], const float* depth_values, int D,
+                                        int HW, const float* grad_evidential,
+                                        const float* grad_prob_combine, float* const grad_head[3],
+                                        hipStream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Opt-in per-kernel timing (a diagnostic, not part of the reference interface).
  * When enabled, every launch made by the entry points above is bracketed by
  * hipEvents on its stream; aarmvs_profile_read synchronises on the recorded

@@ -244,3 +244,42 @@ def sweep(ref_fea, src_feas, ref_proj, src_projs, depth_values, P, planes=None,
         out["cost"] = vol
         out["prob"] = F.softmax(vol, dim=1)
     return out
+
+
+# ----------------------------------------------------------------------------------
+# training step through the sweep (train.py:297-306)
+# ----------------------------------------------------------------------------------
+def cls_loss(prob_volume, depth_gt, mask, depth_value):
+    """mvsnet_cls_loss (drmvsnet.py:347-372): masked cross entropy of the one-hot nearest
+    hypothesis (argmin |d - gt|, :357; index 0 where the mask is 0, :359-360) against
+    log(prob), summed per sample over valid pixels / (count + 1e-6), mean over the batch."""
+    B, D, H, W = prob_volume.shape
+    dvm = depth_value.to(prob_volume.dtype).view(B, D, 1, 1).expand(B, D, H, W)
+    idx = torch.argmin((dvm - depth_gt.to(prob_volume.dtype).unsqueeze(1)).abs(), dim=1)
+    idx = torch.round(mask.to(prob_volume.dtype) * idx.to(prob_volume.dtype)).long().unsqueeze(1)
+    onehot = torch.zeros_like(prob_volume).scatter_(1, idx, 1)
+    ce = -(onehot * torch.log(prob_volume)).sum(dim=1)
+    m = mask.to(prob_volume.dtype)
+    return ((m * ce).sum(dim=[1, 2]) / (m.sum(dim=[1, 2]) + 1e-6)).mean()
+
+
+def train_grads(features, proj, depth_values, P, depth_gt, mask, dtype=torch.float32):
+    """The training step's gradients through the sweep by CPU autograd in ``dtype``:
+    EMVSNet.forward train branch (drmvsnet.py:272-291, features as the leaves: identity
+    FeatNet) -> softmax -> cls_loss -> backward.  float32 is the reference's arithmetic,
+    float64 the anchor.  features [N,B,32,H,W], proj [B,N,4,4].
+    Returns (loss, prob, dL/dfeatures [N,B,32,H,W], {param: dL/dparam})."""
+    N, B, C, H, W = features.shape
+    fc = features.to(dtype).clone().requires_grad_(True)
+    Pp = {k: v.detach().to(dtype).clone().requires_grad_(True) for k, v in P.items()}
+    rels = [relative_projection(proj[:, v], proj[:, 0]) for v in range(1, N)]
+    state = [(h.to(dtype), c.to(dtype)) for h, c in init_state(B, H, W)]
+    costs = []
+    for d in range(depth_values.shape[1]):
+        x = cost_slice(fc[0], [fc[v] for v in range(1, N)], rels, depth_values[:, d], Pp, fast=True)
+        cost, state = unet_step(x, state, Pp)
+        costs.append(cost)
+    prob = F.softmax(torch.stack(costs, 1).squeeze(2), dim=1)
+    loss = cls_loss(prob, depth_gt, mask, depth_values)
+    loss.backward()
+    return loss.detach(), prob.detach(), fc.grad, {k: v.grad for k, v in Pp.items()}

@@ -350,6 +350,46 @@ def gen_overflow(drm, mod, out):
     out.append("wta_overflow.npz")
 
 
+# Training-gradient cases (the BPTT's fixtures): (N, D, H, W, seed), B = 1, real weights.
+# D = 192 is configs[3]'s depth count; the frame is small so the reference's CPU autograd
+# finishes in seconds.
+TRAIN_CASES = {"train_grads_n3_d192.npz": (3, 192, 32, 48, 71),
+               "train_grads_n5_d48.npz": (5, 48, 48, 64, 72)}
+
+
+def gen_train_grads(drm, mod, out):
+    """The reference's training step through the sweep (train.py:297-306): train-mode
+    EMVSNet.forward (drmvsnet.py:272-295: the depth loop with autograd, F.softmax) ->
+    mvsnet_cls_loss (:347-381) -> backward(), identity FeatNet (the features are the leaves),
+    evidential head stubbed, the real model_dtu_v2 core weights.  Stored: the loss, the
+    gradient of every omega.* / cost_regularization.* parameter and dL/d features
+    [N,B,32,H,W], all in the reference's float32."""
+    sd = _real_core_weights()
+    for name, (N, D, H, W, seed) in TRAIN_CASES.items():
+        sc = syn.scene(1, N, H, W, D, seed=seed)
+        model = drm.EMVSNet(disparity_level=D, image_scale=1.0, max_h=H, max_w=W, return_depth=False)
+        model.load_state_dict(sd, strict=False)
+        model.feature = nn.Identity()
+        model.evidential = _NoEvidential()
+        model.train()
+        imgs = t(np.moveaxis(sc["features"], 0, 1)).requires_grad_(True)
+        dv = t(sc["depth_values"])
+        depth_gt, mask = syn.depth_targets(sc["depth_values"], H, W, seed)
+        prob, _, _ = model(imgs, t(sc["proj_matrices"]), dv)
+        loss, wta = drm.mvsnet_cls_loss(prob, t(depth_gt), t(mask), dv)
+        loss.backward()
+        grads = {"g:" + k: p.grad.numpy().copy() for k, p in model.named_parameters()
+                 if k in syn.SWEEP_SHAPES}
+        assert len(grads) == len(syn.SWEEP_SHAPES), sorted(set(syn.SWEEP_SHAPES) - set(grads))
+        np.savez_compressed(os.path.join(HERE, name), loss=loss.detach().numpy(),
+                            grad_features=np.moveaxis(imgs.grad.numpy(), 1, 0).copy(),
+                            wta=wta.numpy(), prob_plane_mean=prob.detach().numpy().mean(axis=(2, 3)),
+                            seed=seed, shape=np.array([1, N, H, W, D]),
+                            digest=syn.array_digest(sc["features"], sc["proj_matrices"],
+                                                    sc["depth_values"]), **grads)
+        out.append(name)
+
+
 def gen_evidential(drm, mod, out):
     """The evidential head (evidential/models.py:183-459) and loss_der (:517-558), which the
     reference's drivers consume (train.py:297-304, eval.py:151-153): the full EMVSNet
@@ -431,7 +471,7 @@ def gen_datasets(drm, mod, out):
 
 
 GENERATORS = (gen_warp, gen_slice_omega, gen_unet, gen_sweeps, gen_config1, gen_e2e, gen_ckpt,
-              gen_evidential, gen_datasets, gen_long, gen_overflow)
+              gen_evidential, gen_datasets, gen_long, gen_overflow, gen_train_grads)
 
 
 def main():

@@ -203,3 +203,33 @@ def test_wta_overflow_semantics_match_reference():
     fin = ok & ~np.isnan(g["conf"])
     np.testing.assert_allclose(conf[fin], g["conf"][fin], atol=1e-4)
     assert rel_l1(out["depth"].numpy()[ok], g["depth"][ok]) <= 1e-3
+
+
+@pytest.mark.parametrize("name", ["train_grads_n3_d192.npz", "train_grads_n5_d48.npz"])
+def test_train_grads_match_reference(name):
+    """The oracle's training step (orc.train_grads: forward, softmax, cls_loss, autograd)
+    against the reference's own float32 gradients (make_golden.gen_train_grads, real weights,
+    D=192 at 32x48 N=3 and D=48 at 48x64 N=5): in float32 the oracle repeats the reference's
+    arithmetic to rounding (<=1e-5 relative L2 per tensor; measured <=1.3e-6), and the
+    reference's float32 error against the oracle's float64 is the oracle's own float32 error
+    (within 1.5x + 1e-6): the float64 oracle is the anchor the GPU backward is measured
+    against (tests/test_gpu_train_fixtures.py)."""
+    import train_fixture as tf
+    c = tf.load_case(name)
+    fix = c["fixture"]
+    l32, f32, p32 = tf.oracle_grads(name, "float32")
+    l64, f64, p64 = tf.oracle_grads(name, "float64")
+    assert abs(l32 - fix["loss"]) <= 1e-6 * abs(fix["loss"])
+    assert abs(l64 - fix["loss"]) <= 1e-5 * abs(fix["loss"])
+    checks = [("features", fix["features"], f32, f64)]
+    checks += [(k, fix["params"][k], p32[k], p64[k]) for k in fix["params"] if k != tf.ZERO_GRAD]
+    assert len(checks) == len(syn.SWEEP_SHAPES)
+    bad = []
+    for k, g_ref, g32, g64 in checks:
+        e_same, e_ref, e_o32 = tf.rel_l2(g32, g_ref), tf.rel_l2(g_ref, g64), tf.rel_l2(g32, g64)
+        if not (e_same <= 1e-5 and e_ref <= 1.5 * e_o32 + 1e-6):
+            bad.append((k, e_same, e_ref, e_o32))
+    assert not bad, bad
+    # the zero-gradient bias: a float32 residue only, in the reference as in the oracle
+    scale = float(np.abs(fix["params"]["cost_regularization.conv_0.weight"]).max())
+    assert abs(float(fix["params"][tf.ZERO_GRAD])) <= 1e-3 * scale
