@@ -374,14 +374,16 @@ class DepthSweep:
                 for k, n in DepthSweep._record_sizes(B, H, W, D, nsrc).items()}
 
     @staticmethod
-    def _record_struct(rec: dict, B: int, H: int, W: int, D: int, nsrc: int):
-        """ctypes view of a record, after checking every buffer holds this geometry's bytes
-        (the library writes them without bounds)."""
+    def _record_struct(rec: dict, B: int, H: int, W: int, D: int, nsrc: int, device=None):
+        """ctypes view of a record, after checking every buffer holds this geometry's bytes,
+        is contiguous and lives on the sweep's device (the library writes them without bounds)."""
         for k, n in DepthSweep._record_sizes(B, H, W, D, nsrc).items():
             t = rec.get(k)
-            if t is None or not t.is_cuda or t.numel() * t.element_size() < n:
-                raise AarmvsError(f"aarmvs: training record '{k}' missing or smaller than {n} B "
-                                  f"(record_buffers(B, H, W, D, nsrc={nsrc}))")
+            if t is None or not t.is_cuda or t.numel() * t.element_size() < n or not t.is_contiguous():
+                raise AarmvsError(f"aarmvs: training record '{k}' missing, non-contiguous or smaller "
+                                  f"than {n} B (record_buffers(B, H, W, D, nsrc={nsrc}))")
+            if device is not None and t.device != torch.device(device):
+                raise AarmvsError(f"aarmvs: training record '{k}' is on {t.device}, the sweep on {device}")
         r = _lib.TrainRecord()
         (r.x, r.state, r.z, r.u, r.stats, r.t1, r.ostats) = (rec[k].data_ptr() for k in DepthSweep.RECORD_KEYS)
         return r
@@ -458,7 +460,7 @@ class DepthSweep:
         a.aux_stream = self._aux.cuda_stream if self._aux is not None else None
         rec_struct = None
         if record is not None:
-            rec_struct = self._record_struct(record, B, H, W, D, nsrc)
+            rec_struct = self._record_struct(record, B, H, W, D, nsrc, ref.device)
             a.record = ctypes.pointer(rec_struct)
         check(lib().aarmvs_sweep(ctypes.byref(a), _stream()), "sweep")
         out["_keepalive"] = (rel, dv, srcs, ref, rec_struct)
@@ -505,7 +507,12 @@ class DepthSweep:
         a.rel_proj = rel.data_ptr()
         a.depth_values = dv.data_ptr()
         a.packed_params = self.packed.data_ptr()
-        rs = self._record_struct(record, B, H, W, D, nsrc)
+        if (not torch.is_tensor(rel) or tuple(rel.shape) != (nsrc, B, 12) or rel.dtype != torch.float32
+                or rel.device != ref.device or not rel.is_contiguous()):
+            raise AarmvsError(f"aarmvs: rel must be a contiguous float32 [nsrc={nsrc}, B={B}, 12] tensor on "
+                              f"{ref.device} (DepthSweep.relative), got "
+                              f"{tuple(rel.shape) if torch.is_tensor(rel) else type(rel)}")
+        rs = self._record_struct(record, B, H, W, D, nsrc, ref.device)
         a.record = ctypes.pointer(rs)
         a.grad_cost = g.data_ptr()
         a.grad_ref = _ptr(grad_ref)

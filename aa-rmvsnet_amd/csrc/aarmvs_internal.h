@@ -223,6 +223,38 @@ hipError_t launch_group_norm_bwd(const float* dy, const float* x, const float* g
 
 int cu_count();
 
+// Per-device host state (func attributes, aux streams and events) is kept in arrays indexed by
+// the current device, so that one process driving several devices (nn.DataParallel) gets each
+// device its own.
+constexpr int kMaxDevices = 64;
+inline hipError_t current_device(int& dev) {
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess && (dev < 0 || dev >= kMaxDevices)) e = hipErrorInvalidDevice;
+  return e;
+}
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per device for a kernel
+inline hipError_t ensure_dyn_lds(const void* fn, int bytes, bool (&done)[kMaxDevices]) {
+  int dev = 0;
+  hipError_t e = current_device(dev);
+  if (e != hipSuccess || done[dev]) return e;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done[dev] = true;
+  return e;
+}
+// Joins an auxiliary stream back into the caller's stream when it goes out of scope: on every
+// return after a fork (errors included), nothing the call enqueued on the aux stream is left
+// unordered with the caller's stream, whose buffers the caller may free on an error.
+struct StreamJoin {
+  hipStream_t main, aux;
+  hipEvent_t ev;
+  ~StreamJoin() {
+    if (aux && aux != main && ev) {
+      (void)hipEventRecord(ev, aux);
+      (void)hipStreamWaitEvent(main, ev, 0);
+    }
+  }
+};
+
 // Backward of the regulariser (bptt.hip) over every plane of a training record: the
 // parameter gradients of the cells / deconvs / head into the fp64 accumulators of its scratch
 // (written to grad_params as float at the end, the cost-slice part included if group_done
@@ -267,7 +299,13 @@ enum KernelId : int {
   K_COST_X, K_OMEGA_CONV, K_FUSION, K_OMEGA1, K_OMEGA2,
   K_CELL0, K_CELL1, K_CELL2, K_CELL3, K_CELL4,
   K_DECONV0, K_DECONV1, K_HEAD_WTA, K_FINALIZE, K_SOFTMAX, K_WARP, K_TO_C8, K_STAT_REDUCE,
-  K_GN_REDUCE, K_EVIDENTIAL, K_COUNT
+  K_GN_REDUCE, K_EVIDENTIAL,
+  // the training backward (bptt.hip, the cbw_* kernels of warp_cost.hip)
+  K_GATE_BWD0, K_GATE_BWD1, K_GATE_BWD2, K_GATE_BWD3, K_GATE_BWD4,
+  K_DGRAD0, K_DGRAD1, K_DGRAD2, K_DGRAD3, K_DGRAD4,
+  K_WGRAD0, K_WGRAD1, K_WGRAD2, K_WGRAD3, K_WGRAD4,
+  K_GNB_PARTIAL, K_DECONV_BWD, K_BWD_SMALL, K_CBW_CHAIN, K_CBW_FEAT, K_CBW_SMALL,
+  K_COUNT
 };
 extern bool g_prof_on;
 void prof_mark(hipStream_t s, int id, bool begin);

@@ -90,7 +90,11 @@ static const char* kKernelNames[K_COUNT] = {
     "cost_x", "omega_conv", "fusion", "omega_stats1", "omega_stats2",
     "lstm_cell0", "lstm_cell1", "lstm_cell2", "lstm_cell3", "lstm_cell4",
     "deconv0", "deconv1", "head_wta", "finalize", "softmax_depth", "homo_warp", "to_c8",
-    "omega_stat_reduce", "gn_reduce", "evidential"};
+    "omega_stat_reduce", "gn_reduce", "evidential",
+    "gate_bwd0", "gate_bwd1", "gate_bwd2", "gate_bwd3", "gate_bwd4",
+    "dgrad0", "dgrad1", "dgrad2", "dgrad3", "dgrad4",
+    "wgrad0", "wgrad1", "wgrad2", "wgrad3", "wgrad4",
+    "gnb_partial", "deconv_bwd", "bwd_small", "cbw_chain", "cbw_feat", "cbw_small"};
 
 static hipEvent_t prof_event() {
   if (g_prof_used == g_prof_pool.size()) {
@@ -252,7 +256,9 @@ __global__ void __launch_bounds__(256) pack_cell_h3_kernel(const float* __restri
     const int r = l & 31, h = l >> 5;
     const int co = (r >> 3) * hid + 8 * mt + (r & 7);
     const int ci = 16 * c + 8 * h + j;
-    const float v = ci < cin ? w[(co * cin + ci) * 9 + tap] * sc : 0.f;
+    // taps with (tap + chunk) odd negated: the cells' sign-balanced accumulation (convlstm.hip)
+    const float sg = ((tap + c) & 1) ? -1.0f : 1.0f;
+    const float v = ci < cin ? w[(co * cin + ci) * 9 + tap] * sc * sg : 0.f;
     const _Float16 vh = (_Float16)v;
     hi[i] = vh;
     lo[i] = (_Float16)(v - (float)vh);
@@ -396,7 +402,9 @@ __global__ void __launch_bounds__(256) pack_dgrad_kernel(const float* __restrict
     const int j = i & 7, l = (i >> 3) & 63, hl = (i >> 9) & 1, rest = i >> 10;
     const int tap = rest % 9, c = (rest / 9) % nch, mt = rest / (9 * nch);
     const int ci = 32 * mt + (l & 31), z = 16 * c + 8 * (l >> 5) + j;
-    const float v = ci < cin ? w[(z * cin + ci) * 9 + (8 - tap)] * sc : 0.f;
+    // taps with (tap + chunk) odd negated: dgrad's sign-balanced accumulation (bptt.hip)
+    const float sg = ((tap + c) & 1) ? -1.0f : 1.0f;
+    const float v = ci < cin ? w[(z * cin + ci) * 9 + (8 - tap)] * sc * sg : 0.f;
     const _Float16 vh = (_Float16)v;
     f[i] = hl == 0 ? vh : (_Float16)(v - (float)vh);
   }
@@ -583,21 +591,17 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     int dev = -1;
     hipEvent_t ev[5] = {};
   };
-  static thread_local EventSet evs;
-  hipEvent_t* ev = evs.ev;
+  static thread_local EventSet evs_dev[kMaxDevices];   // one set per device
   auto sweep_fail = [&](hipError_t err, const char* where) { return hip_fail(err, where); };
-  if (aux) {
-    int dev = 0;
-    if ((e = hipGetDevice(&dev)) != hipSuccess) return sweep_fail(e, "sweep: get device");
-    if (evs.dev != dev) {
-      for (hipEvent_t& x : evs.ev)
-        if (x) (void)hipEventDestroy(x), x = nullptr;
-      evs.dev = -1;
-      for (hipEvent_t& x : evs.ev)
-        if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
-          return sweep_fail(e, "sweep: event create");
-      evs.dev = dev;
-    }
+  int dev = 0;
+  if ((e = current_device(dev)) != hipSuccess) return sweep_fail(e, "sweep: get device");
+  EventSet& evs = evs_dev[dev];
+  hipEvent_t* ev = evs.ev;
+  if (aux && evs.dev != dev) {
+    for (hipEvent_t& x : evs.ev)
+      if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
+        return sweep_fail(e, "sweep: event create");
+    evs.dev = dev;
   }
   hipEvent_t* ev_cost = ev;
   hipEvent_t* ev_used = ev + 2;
@@ -634,6 +638,8 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         (e = hipStreamWaitEvent(aux, ev[4], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: fork");
   }
+  // every return from here on (errors included) leaves the aux stream's work ordered on `stream`
+  StreamJoin join{stream, aux, ev[4]};
   // the WTA images are maintained on every plane, whether or not this call returns depth:
   // a sweep split into d_range calls gives the same depth/confidence however its earlier
   // pieces were requested (24 B/px per plane, <0.5% of a plane's time)
@@ -682,6 +688,7 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
       return sweep_fail(e, "sweep: event record");
   }
   if (aux) {   // join: everything the call enqueued is ordered on `stream` at return
+    join.aux = nullptr;
     if ((e = hipEventRecord(ev[4], aux)) != hipSuccess ||
         (e = hipStreamWaitEvent(stream, ev[4], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: join");

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <initializer_list>
 
@@ -366,11 +367,14 @@ __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
     int b, y0, x0;
     coords(tile, b, y0, x0);
     const int next = tile + (int)gridDim.x;
-    bfloatx16 acc;
+    // sign-balanced accumulation (convlstm.hip h3_mfma_chunk): taps with (tap + chunk) odd
+    // carry negated fragments (pack_dgrad_kernel) and go to accn; the result is acc - accn
+    bfloatx16 acc, accn;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-#pragma unroll 1
-    for (int c = 0; c < NCHK; ++c) {
+    for (int j = 0; j < 16; ++j) acc[j] = accn[j] = 0.f;
+    static_assert(NCHK % 2 == 0, "chunk pairs (the accumulators' sign pattern)");
+    auto chunk = [&](int c, auto PAR) {
+      constexpr int CP = decltype(PAR)::value;   // c & 1
       __syncthreads();   // previous chunk's fragment reads done (fragments visible the first time)
       store();
       __syncthreads();
@@ -386,11 +390,18 @@ __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
         const char* af = wl + (size_t)(((c * 9 + tap) * 2) * 512 + lane * 8) * 2;
         const bhalf8 ah = *reinterpret_cast<const bhalf8*>(af);
         const bhalf8 alo = *reinterpret_cast<const bhalf8*>(af + 512 * 2);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bh, acc, 0, 0, 0);
+        bfloatx16& d = ((tap + CP) & 1) ? accn : acc;
+        d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bh, d, 0, 0, 0);
       }
+    };
+#pragma unroll 1
+    for (int c = 0; c < NCHK; c += 2) {
+      chunk(c, std::integral_constant<int, 0>{});
+      chunk(c + 1, std::integral_constant<int, 1>{});
     }
+    acc -= accn;
     const int y = y0 + wave, x = x0 + col;
     if (y < a.H && x < a.W) {
       const size_t p = ((size_t)b * a.H + y) * a.W + x;
@@ -825,10 +836,21 @@ __global__ void __launch_bounds__(512) wgrad2_kernel(WgradArgs a) {
   const int item0 = blockIdx.x;
   Pre pre;
   if (item0 < nitem) pre = fetch(item0);
+  // sign-balanced accumulation (convlstm.hip h3_mfma_chunk): odd items stage -gz and the
+  // accumulators are negated between items, so they hold (-1)^item x the running sums and the
+  // MFMAs' low-side drift alternates sign
+  float zsg = zs;
 #pragma unroll 1
   for (int item = item0; item < nitem; item += gridDim.x) {
     int k, b, y0, x0;
     item_pos(item, k, b, y0, x0);
+    if (item != item0) {
+      zsg = -zsg;
+#pragma unroll
+      for (int i = 0; i < CPW; ++i)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) acc[i][dx] = -acc[i][dx];
+    }
     __syncthreads();   // the previous item's fragment reads are done
     const float4(&zq)[4] = pre.z;
     if (zrole) {
@@ -838,8 +860,8 @@ __global__ void __launch_bounds__(512) wgrad2_kernel(WgradArgs a) {
       for (int i = 0; i < 8; ++i) {
         bacc[i] += v0[i] + v1[i];
         _Float16 h0, l0, h1, l1;
-        split16(v0[i] * zs, h0, l0);
-        split16(v1[i] * zs, h1, l1);
+        split16(v0[i] * zsg, h0, l0);
+        split16(v1[i] * zsg, h1, l1);
         const int o = (8 * zcg + i) * kW2ZS + zr * 32 + zx;
         *reinterpret_cast<unsigned*>(zt + o) = pack_h2(h0, h1);
         *reinterpret_cast<unsigned*>(zt + CZ * kW2ZS + o) = pack_h2(l0, l1);
@@ -944,8 +966,8 @@ __global__ void __launch_bounds__(512) wgrad2_kernel(WgradArgs a) {
       }
     }
   }
-  // the group's zmax slots share one exponent (zmax_group_kernel)
-  const float zinv = ldexpf(1.0f, scale_exp(a.zmax[0]));
+  // the group's zmax slots share one exponent (zmax_group_kernel); the accumulators' sign
+  const float zinv = zsg < 0.f ? -ldexpf(1.0f, scale_exp(a.zmax[0])) : ldexpf(1.0f, scale_exp(a.zmax[0]));
   float* wp = a.wpart + (size_t)blockIdx.x * kWgPartMax;
   const int cinp = 16 * ((a.cin + 15) / 16);
 #pragma unroll
@@ -1177,29 +1199,27 @@ __global__ void zmax_group_kernel(unsigned* zmax, int n) {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-static hipError_t run_gate_bwd(const GateBwdArgs& a, hipStream_t s) {
+static hipError_t run_gate_bwd(const GateBwdArgs& a, hipStream_t s, int kid) {
   const size_t n = (size_t)a.B * a.H * a.W * (a.hid / 4);
   if ((size_t)a.B * a.H * a.W * a.hid >= (1ull << 31)) return hipErrorInvalidValue;   // 32-bit indices
+  ProfScope ps(s, kid);
   hipLaunchKernelGGL(gate_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 template <int CZ>
-static hipError_t run_dgrad(const DgradArgs& a, hipStream_t s) {
+static hipError_t run_dgrad(const DgradArgs& a, hipStream_t s, int kid) {
   constexpr size_t lds = (size_t)(CZ / 16) * 9 * 2 * 512 * 2 + 2 * kDgNPIX * 32;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)dgrad_kernel<CZ>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static bool attr[kMaxDevices] = {};
+  if (hipError_t e = ensure_dyn_lds((const void*)dgrad_kernel<CZ>, (int)lds, attr); e != hipSuccess)
+    return e;
   const int tiles = a.B * ((a.W + kDgTW - 1) / kDgTW) * ((a.H + kDgTH - 1) / kDgTH);
   const int mtn = (a.cout + 31) / 32;
   // persistent blocks: as many as the CUs hold (LDS-bound), split over the m-tiles
   const int cu = cu_count();
   const int per_cu = std::max(1, (int)((160 * 1024) / lds));
   const int grid = std::max(1, std::min(tiles, std::max(1, cu * per_cu / mtn)));
+  ProfScope ps(s, kid);
   hipLaunchKernelGGL(dgrad_kernel<CZ>, dim3(grid, mtn), dim3(512), lds, s, a);
   return hipGetLastError();
 }
@@ -1229,23 +1249,23 @@ static void fill_chunks(WgradArgs& a) {
 }
 
 template <int CZ, int NCH>
-static hipError_t run_wgrad(WgradArgs a, double* gw, double* gb, hipStream_t s) {
+static hipError_t run_wgrad(WgradArgs a, double* gw, double* gb, hipStream_t s, int kid) {
   fill_chunks(a);
   a.gn_chunk = -1;
   for (int c = 0; c < NCH; ++c)
     if (a.chunk[c].mode == WG_GNRELU) a.gn_chunk = c;
   const size_t lds = wgrad2_lds<CZ, NCH>() + (size_t)kPlaneGroup * a.B * 2 * sizeof(float2);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)wgrad2_kernel<CZ, NCH>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
+  static bool attr[kMaxDevices] = {};
+  if (hipError_t e = ensure_dyn_lds((const void*)wgrad2_kernel<CZ, NCH>, 160 * 1024, attr); e != hipSuccess)
+    return e;
+  {
+    ProfScope ps(s, kid);
+    hipLaunchKernelGGL((wgrad2_kernel<CZ, NCH>), dim3(kWgBlocks), dim3(512), lds, s, a);
   }
-  hipLaunchKernelGGL((wgrad2_kernel<CZ, NCH>), dim3(kWgBlocks), dim3(512), lds, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  ProfScope ps(s, K_BWD_SMALL);
   return reduce_partials(a.wpart, kWgBlocks, (int)kWgPartMax, CZ * 16 * NCH * 9 + CZ, CZ, a.cin,
                          CZ * a.cin * 9 + CZ, CZ * a.cin * 9, a.rseg, gw, gb, s);
 }
@@ -1304,7 +1324,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       a.gpool = L.gpool[k];
       a.hnew = io.h_new[k];
     }
-    return run_gate_bwd(a, s);
+    return run_gate_bwd(a, s, K_GATE_BWD0 + k);
   };
   auto dgrad = [&](hipStream_t s, int k, int slot, std::initializer_list<DgPart> parts) {
     DgradArgs a{};
@@ -1319,7 +1339,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     a.B = B;
     a.H = H / res_div[k];
     a.W = W / res_div[k];
-    return kCellHid[k] == 16 ? run_dgrad<64>(a, s) : run_dgrad<32>(a, s);
+    return kCellHid[k] == 16 ? run_dgrad<64>(a, s, K_DGRAD0 + k) : run_dgrad<32>(a, s, K_DGRAD0 + k);
   };
   // GroupNorm-backward partial blocks per (plane, sample) of deconv j's output
   auto gnb_nblk = [&](int j) {
@@ -1339,7 +1359,10 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     g.part = L.gnb_part[j] + (size_t)slot * B * nblk * 36;
     g.j = j;
     g.HW = (int)hwo;
-    hipLaunchKernelGGL(gnb_partial_kernel, dim3(nblk, B), dim3(256), 0, s, g);
+    {
+      ProfScope ps(s, K_GNB_PARTIAL);
+      hipLaunchKernelGGL(gnb_partial_kernel, dim3(nblk, B), dim3(256), 0, s, g);
+    }
     CK(hipGetLastError());
     DcbArgs a{};
     a.gr = gr;
@@ -1355,6 +1378,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     a.j = j;
     a.Hi = Ho / 2;
     a.Wi = Wo / 2;
+    ProfScope ps(s, K_DECONV_BWD);
     hipLaunchKernelGGL(deconv_bwd_kernel, dim3((a.Hi * a.Wi + 63) / 64, B), dim3(256), 0, s, a);
     return hipGetLastError();
   };
@@ -1373,23 +1397,25 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     hipStream_t aux = nullptr;
     hipEvent_t ev[5] = {};   // evA[2], evB[2], fork
   };
-  static thread_local PipeSet ps;
+  static thread_local PipeSet ps_dev[kMaxDevices];   // one aux stream + events per device
   static const bool pipe_on = [] {
     const char* v = getenv("AARMVS_BWD_PIPE");
     return !(v && v[0] == '0');
   }();
+  int dev = 0;
+  CK(current_device(dev));
+  PipeSet& ps = ps_dev[dev];
   hipStream_t sa = s;
-  if (pipe_on) {
-    int dev = 0;
-    CK(hipGetDevice(&dev));
+  if (pipe_on && !g_prof_on) {   // (per-kernel timing runs on one stream: isolated kernel spans)
     if (ps.dev != dev) {
-      ps.dev = -1;
       CK(hipStreamCreateWithFlags(&ps.aux, hipStreamNonBlocking));
       for (hipEvent_t& x : ps.ev) CK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
       ps.dev = dev;
     }
     sa = ps.aux;
   }
+  // every return from here on (errors included) leaves the aux stream's work ordered on s
+  StreamJoin join{s, sa, ps.ev[4]};
   hipEvent_t* evA = ps.ev;
   hipEvent_t* evB = ps.ev + 2;
   auto gr0_of = [&](int d) { return (d & 1) ? L.gr0b : L.gr[0]; };
@@ -1438,7 +1464,10 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     }
     // ---- weight gradients of the group ----
     for (int k = 0; k < 5; ++k) {
-      hipLaunchKernelGGL(zmax_group_kernel, dim3(1), dim3(64), 0, s, L.zmax + k * G, n);
+      {
+        ProfScope ps(s, K_BWD_SMALL);
+        hipLaunchKernelGGL(zmax_group_kernel, dim3(1), dim3(64), 0, s, L.zmax + k * G, n);
+      }
       CK(hipGetLastError());
     }
     const float hsc = 16384.0f;   // |h| < 1
@@ -1506,12 +1535,13 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       double* gw = L.gacc + PL.raw_off[P_C0W + 2 * k];
       double* gb = L.gacc + PL.raw_off[P_C0B + 2 * k];
       const int nch = (a.cin + 15) / 16;
-      const hipError_t we = kCellHid[k] == 8 ? run_wgrad<32, 3>(a, gw, gb, s)
-                            : nch == 3     ? run_wgrad<64, 3>(a, gw, gb, s)
-                                           : run_wgrad<64, 2>(a, gw, gb, s);
+      const hipError_t we = kCellHid[k] == 8 ? run_wgrad<32, 3>(a, gw, gb, s, K_WGRAD0 + k)
+                            : nch == 3     ? run_wgrad<64, 3>(a, gw, gb, s, K_WGRAD0 + k)
+                                           : run_wgrad<64, 2>(a, gw, gb, s, K_WGRAD0 + k);
       CK(we);
     }
     for (int j = 0; j < 2; ++j) {   // the deconvs' GroupNorm affine gradients of the group
+      ProfScope ps(s, K_BWD_SMALL);
       hipLaunchKernelGGL(gnb_affine_kernel, dim3(32), dim3(256), 0, s, L.gnb_part[j], n, gnb_nblk(j), B,
                          L.gacc + PL.raw_off[j ? P_D1GW : P_D0GW], L.gacc + PL.raw_off[j ? P_D1GB : P_D0GB]);
       CK(hipGetLastError());
@@ -1526,7 +1556,10 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       a.Hi = j ? H / 2 : H / 4;
       a.Wi = j ? W / 2 : W / 4;
       a.wpart = L.wpart;
-      hipLaunchKernelGGL(deconv_wgrad_kernel, dim3(kDcwBlocks), dim3(256), 0, s, a);
+      {
+        ProfScope ps(s, K_BWD_SMALL);
+        hipLaunchKernelGGL(deconv_wgrad_kernel, dim3(kDcwBlocks), dim3(256), 0, s, a);
+      }
       CK(hipGetLastError());
       CK(reduce_partials(L.wpart, kDcwBlocks, kDcwPart, 2320, 0, 0, 2320, 2304, L.rseg,
                          L.gacc + PL.raw_off[j ? P_D1W : P_D0W], L.gacc + PL.raw_off[j ? P_D1B : P_D0B], s));
@@ -1543,7 +1576,10 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       a.H = H;
       a.W = W;
       a.wpart = L.wpart;
-      hipLaunchKernelGGL(head_wgrad_kernel, dim3(kWgBlocks), dim3(256), 0, s, a);
+      {
+        ProfScope ps(s, K_BWD_SMALL);
+        hipLaunchKernelGGL(head_wgrad_kernel, dim3(kWgBlocks), dim3(256), 0, s, a);
+      }
       CK(hipGetLastError());
       CK(reduce_partials(L.wpart, kWgBlocks, (int)kWgPartMax, 73, 0, 0, 73, 72, L.rseg,
                          L.gacc + PL.raw_off[P_HW], L.gacc + PL.raw_off[P_HB], s));

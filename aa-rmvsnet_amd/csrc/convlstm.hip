@@ -137,6 +137,7 @@ struct CellDef<0> {   // [x, h0] @ H
   static constexpr int MODE[kMaxParts] = {SRC_PLAIN, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16;
   static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1, H3PIPE = 1;
+  static constexpr int MIN_WAVES = 1;   // amdgpu_waves_per_eu lower bound (register budget)
 };
 template <>
 struct CellDef<1> {   // [maxpool(h0'), h1] @ H/2
@@ -144,6 +145,7 @@ struct CellDef<1> {   // [maxpool(h0'), h1] @ H/2
   static constexpr int MODE[kMaxParts] = {SRC_POOL, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16;
   static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1, H3PIPE = 1;
+  static constexpr int MIN_WAVES = 1;
 };
 template <>
 struct CellDef<2> : CellDef<1> {};   // [maxpool(h1'), h2] @ H/4
@@ -153,6 +155,7 @@ struct CellDef<3> {   // [gnrelu(u0), h1', h3] @ H/2
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16;
   static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 0, H3PIPE = 1;
+  static constexpr int MIN_WAVES = 1;
 };
 template <>
 struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
@@ -160,6 +163,9 @@ struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 8;
   static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 0, H3PIPE = 0;
+  // <= 128 VGPRs: two 512-thread blocks per CU (the sign-balanced accumulator pair took the
+  // compiler's choice to 130, one block per CU: 160 -> 202 us per plane at the headline)
+  static constexpr int MIN_WAVES = 4;
 };
 
 // ---------------------------------------------------------------------------
@@ -316,13 +322,17 @@ struct H3PixStager {
 // GroupNorm+ReLU part, staged x 2^-e) to the h parts' scale 2^kHScaleExp (CH is the first chunk
 // past part 0); the epilogue undoes 2^kHScaleExp with the weight scale.
 template <class C, int KIND, int CH>
-__device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], float xr) {
+__device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], floatx16 (&accn)[C::MT][C::RW],
+                                               float xr) {
   if constexpr ((KIND == 0 || C::D::MODE[0] == SRC_GNRELU) && CH > 0 && C::chunk_part(CH) != 0 &&
                 C::chunk_part(CH - 1) == 0) {
 #pragma unroll
     for (int m = 0; m < C::MT; ++m)
 #pragma unroll
-      for (int r = 0; r < C::RW; ++r) acc[m][r] *= xr;
+      for (int r = 0; r < C::RW; ++r) {
+        acc[m][r] *= xr;
+        accn[m][r] *= xr;
+      }
   }
 }
 
@@ -330,9 +340,16 @@ __device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], fl
 // A/B fragments of tap t+1 are read from LDS into a second register set before tap t's
 // MFMAs issue (sched_barrier pins the order); otherwise the compiler's schedule reads
 // each tap's fragments just before use and waits on them every 2-3 MFMAs.
+// Sign-balanced accumulation: v_mfma_f32_*_f16 does not round its fp32 accumulation to
+// nearest -- each MFMA's result errs low by ~0.1 ulp of its largest addend on average
+// (tools/microbench/mfma_round.cpp: -0.33 ulp of the result over random inputs), so a long
+// chain drifts downwards, a bias that long cancelling gradient sums amplify.
+// Taps with (tap + chunk) odd carry negated weights (pack_cell_h3_kernel) and accumulate into
+// accn; the result is acc - accn, whose two drifts cancel (tools/microbench/mfma_chain.cpp:
+// -0.164 -> +0.001 ulp over 108 MFMAs).
 template <class C, int CH, bool PIPE = false>
-__device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], const char* wl_hi,
-                                              const char* wl_lo, const char* in_hi,
+__device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], floatx16 (&accn)[C::MT][C::RW],
+                                              const char* wl_hi, const char* wl_lo, const char* in_hi,
                                               const char* in_lo, int wave, int lane) {
   constexpr int MT = C::MT, RW = C::RW;
   const int col = lane & 31, h = lane >> 5;
@@ -362,9 +379,10 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], con
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
-          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s][m], bh[s][r], acc[m][r], 0, 0, 0);
-          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s][m], bl[s][r], acc[m][r], 0, 0, 0);
-          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s][m], bh[s][r], acc[m][r], 0, 0, 0);
+          floatx16& d = ((tap + CH) & 1) ? accn[m][r] : acc[m][r];
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s][m], bh[s][r], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s][m], bl[s][r], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s][m], bh[s][r], d, 0, 0, 0);
         }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -386,9 +404,10 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], con
         const half8 al = *reinterpret_cast<const half8*>(wl_lo + aoff);
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
-          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[r], acc[m][r], 0, 0, 0);
-          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[r], acc[m][r], 0, 0, 0);
-          acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[r], acc[m][r], 0, 0, 0);
+          floatx16& d = ((tap + CH) & 1) ? accn[m][r] : acc[m][r];
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[r], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[r], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[r], d, 0, 0, 0);
         }
       }
     }
@@ -474,7 +493,7 @@ __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 
 // gate math)
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
           int PIPE = CellDef<KIND>::H3PIPE>
-__global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
+__global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(CellDef<KIND>::MIN_WAVES))) lstm_cell_h3_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
   using D = typename C::D;
@@ -528,13 +547,13 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
     int nb = 0, ny0 = 0, nx0 = 0;
     if (next < ntiles) coords(next, nb, ny0, nx0);
     const int yw = y0 + wave * RW;   // this wave's first row
-    floatx16 acc[MT][RW];
+    floatx16 acc[MT][RW], accn[MT][RW];   // sign-balanced pair (h3_mfma_chunk)
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int r = 0; r < RW; ++r)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[m][r][j] = 0.0f;
+        for (int j = 0; j < 16; ++j) acc[m][r][j] = accn[m][r][j] = 0.0f;
     float cst[MT][RW][4];
     // chunk loop, fully unrolled so that every chunk's staging mode is compile-time
     auto chunk = [&](auto CHc) {
@@ -549,13 +568,16 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
         st.template load<0>(a, nb, ny0, nx0, tid);
       }
       if (CH == 0) cell_c_load<C>(a, b, yw, x0 + col, hi, cst);
-      xguard_rescale<C, KIND, CH>(acc, xr);
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0>(acc, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
+      xguard_rescale<C, KIND, CH>(acc, accn, xr);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0>(acc, accn, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
     };
     chunk(std::integral_constant<int, 0>{});
     if constexpr (NCHK > 1) chunk(std::integral_constant<int, 1>{});
     if constexpr (NCHK > 2) chunk(std::integral_constant<int, 2>{});
-
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < RW; ++r) acc[m][r] -= accn[m][r];
     cell_epilogue<C, ABL>(a, acc, cst, inv_scale, b, yw, x0 + col, hi);
   }
 }
@@ -568,7 +590,7 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3_kernel(
 // waves of a SIMD one wave's staging VALU work fills the other's MFMA issue gaps.
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
           int PIPE = CellDef<KIND>::H3PIPE>
-__global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
+__global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(CellDef<KIND>::MIN_WAVES))) lstm_cell_h3db_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
   using D = typename C::D;
@@ -627,14 +649,14 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
     if (next < ntiles) coords(next, nb, ny0, nx0);
     const int yw = y0 + wave * RW;   // this wave's first row
     const int x = x0 + col;
-    floatx16 acc[MT][RW];
+    floatx16 acc[MT][RW], accn[MT][RW];   // sign-balanced pair (h3_mfma_chunk)
     float cst[MT][RW][4];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int r = 0; r < RW; ++r)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[m][r][j] = 0.0f;
+        for (int j = 0; j < 16; ++j) acc[m][r][j] = accn[m][r][j] = 0.0f;
     cell_c_load<C>(a, b, yw, x, hi, cst);
     auto step = [&](auto CHc) {
       constexpr int CH = decltype(CHc)::value;
@@ -644,8 +666,8 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
       constexpr int AC = A_NEXT ? CH + 2 - NCHK : CH + 2;
       const char* cur = inb + 2 * par * PB;
       char* oth = inb + 2 * (par ^ 1) * PB;
-      xguard_rescale<C, KIND, CH>(acc, xr);
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0>(acc, wl_hi, wl_lo, cur, cur + PB, wave, lane);
+      xguard_rescale<C, KIND, CH>(acc, accn, xr);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0>(acc, accn, wl_hi, wl_lo, cur, cur + PB, wave, lane);
       if (!(ABL & 2)) {
         if (!F_NEXT || next < ntiles) st.template store<F>(oth, oth + PB, gn, tid, 0, W);
         if (!A_NEXT)
@@ -653,7 +675,13 @@ __global__ void __launch_bounds__(WAVES * 64) lstm_cell_h3db_kernel(
         else if (next < ntiles)
           st.template load<AC>(a, nb, ny0, nx0, tid);
       }
-      if constexpr (CH == NCHK - 1) cell_epilogue<C, ABL>(a, acc, cst, inv_scale, b, yw, x, hi);
+      if constexpr (CH == NCHK - 1) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int r = 0; r < RW; ++r) acc[m][r] -= accn[m][r];
+        cell_epilogue<C, ABL>(a, acc, cst, inv_scale, b, yw, x, hi);
+      }
       __syncthreads();   // buffer `oth` staged; buffer `cur` free for the step after next
       par ^= 1;
     };
@@ -678,12 +706,8 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
   static_assert(lds <= 160 * 1024, "h3 cell tile exceeds LDS");
   const void* fn = DB ? (const void*)lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE>
                       : (const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  static bool attr_set[kMaxDevices] = {};
+  if (hipError_t e = ensure_dyn_lds(fn, (int)lds, attr_set); e != hipSuccess) return e;
   const int ntiles = a.B * ((a.W + C::TW - 1) / C::TW) * ((a.H + C::TH - 1) / C::TH);
   const int per_cu = std::max(1, (int)((160 * 1024) / lds));
   const int grid = std::max(1, std::min(ntiles, cu * per_cu));

@@ -913,7 +913,7 @@ __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
     gn_relu4(t, gs[0], o.g0w, o.g0b, true, aa);
     conv1x1_4(aa, o.w1, o.b1, t2);
     float r[4];
-    if (STAGE == 1) {
+    if constexpr (STAGE == 1) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) r[c] = t2[c];
     } else {
@@ -1267,7 +1267,7 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
     OmegaChain c;
     omega_chain(t1p[p], gs, o, c);
     float g_o;
-    if (STAGE == 1) {
+    if constexpr (STAGE == 1) {
       // dL/dw = -(1/nsrc) sum_c dL/dx sq (the warp and sq recomputed as cost_x does)
       const int x = p % W, y = p / W;
       const TapF tf = tap_f(m, dep, x, y, H, W);
@@ -1297,7 +1297,7 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
     float xh3[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) xh3[i] = (c.t3[i] - gs[2].mean) * gs[2].rstd;
-    if (STAGE == 1) {
+    if constexpr (STAGE == 1) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float gx3 = g_r[i] * o.g2w[i];
@@ -1323,7 +1323,7 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
       g_n2[ci] = c.v2[ci] > 0.f ? ga : 0.f;
       xh2[ci] = (c.t2[ci] - gs[1].mean) * gs[1].rstd;
     }
-    if (STAGE == 2) {
+    if constexpr (STAGE == 2) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float gx2 = g_n2[i] * o.g1w[i];
@@ -1350,7 +1350,7 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
       g_n1[ci] = c.v1[ci] > 0.f ? ga : 0.f;
       xh1[ci] = (c.t[ci] - gs[0].mean) * gs[0].rstd;
     }
-    if (STAGE == 3) {
+    if constexpr (STAGE == 3) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float gx1 = g_n1[i] * o.g0w[i];
@@ -1884,38 +1884,64 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
     return cc;
   };
   // stage 1: dL/do, GN3 sums; Wo, bo, gamma3, beta3
-  hipLaunchKernelGGL(cbw_chain_kernel<1>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  {
+    ProfScope ps(s, K_CBW_CHAIN);
+    hipLaunchKernelGGL(cbw_chain_kernel<1>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  { ProfScope ps_(s, K_CBW_SMALL);
   hipLaunchKernelGGL(cbw_gsum_kernel, dim3(nkbv), dim3(64), 0, s, L.part, L.pblk, L.gsum, 2);
+  }
   {
     const CbwCols cc = cols(2, {{P_OWO, 4}, {P_OBO, 1}, {P_OG2W, 4}, {P_OG2B, 4}});
+    { ProfScope ps_(s, K_CBW_SMALL);
     hipLaunchKernelGGL(cbw_param_kernel, dim3(cc.ncol), dim3(256), 0, s, L.part, nrow, cc, c.gacc);
+    }
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // stage 2: GN2 sums; W2, b2, gamma2, beta2
-  hipLaunchKernelGGL(cbw_chain_kernel<2>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  {
+    ProfScope ps(s, K_CBW_CHAIN);
+    hipLaunchKernelGGL(cbw_chain_kernel<2>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  { ProfScope ps_(s, K_CBW_SMALL);
   hipLaunchKernelGGL(cbw_gsum_kernel, dim3(nkbv), dim3(64), 0, s, L.part, L.pblk, L.gsum, 1);
+  }
   {
     const CbwCols cc = cols(2, {{P_OW2, 16}, {P_OB2, 4}, {P_OG1W, 4}, {P_OG1B, 4}});
+    { ProfScope ps_(s, K_CBW_SMALL);
     hipLaunchKernelGGL(cbw_param_kernel, dim3(cc.ncol), dim3(256), 0, s, L.part, nrow, cc, c.gacc);
+    }
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // stage 3: GN1 sums; W1, b1, gamma1, beta1
-  hipLaunchKernelGGL(cbw_chain_kernel<3>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  {
+    ProfScope ps(s, K_CBW_CHAIN);
+    hipLaunchKernelGGL(cbw_chain_kernel<3>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  { ProfScope ps_(s, K_CBW_SMALL);
   hipLaunchKernelGGL(cbw_gsum_kernel, dim3(nkbv), dim3(64), 0, s, L.part, L.pblk, L.gsum, 0);
+  }
   {
     const CbwCols cc = cols(2, {{P_OW1, 16}, {P_OB1, 4}, {P_OG0W, 4}, {P_OG0B, 4}});
+    { ProfScope ps_(s, K_CBW_SMALL);
     hipLaunchKernelGGL(cbw_param_kernel, dim3(cc.ncol), dim3(256), 0, s, L.part, nrow, cc, c.gacc);
+    }
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // stage 4: dL/dt1; b0
-  hipLaunchKernelGGL(cbw_chain_kernel<4>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  {
+    ProfScope ps(s, K_CBW_CHAIN);
+    hipLaunchKernelGGL(cbw_chain_kernel<4>, grid, dim3(256), 0, s, ba, ba.p.params, ba.p.rel);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   {
     const CbwCols cc = cols(0, {{P_OB0, 4}});
+    { ProfScope ps_(s, K_CBW_SMALL);
     hipLaunchKernelGGL(cbw_param_kernel, dim3(cc.ncol), dim3(256), 0, s, L.part, nrow, cc, c.gacc);
+    }
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // dL/dsq -> features, conv3x3 weights
@@ -1929,13 +1955,20 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   fa.wpart = L.wpart;
   fa.d0 = g0;
   fa.n = n;
-  hipLaunchKernelGGL(cbw_feat_kernel, dim3(L.ntiles16, 4 * a->nsrc, a->B), dim3(256), 0, s, fa,
-                     ba.p.params, ba.p.rel);
+  {
+    ProfScope ps(s, K_CBW_FEAT);
+    hipLaunchKernelGGL(cbw_feat_kernel, dim3(L.ntiles16, 4 * a->nsrc, a->B), dim3(256), 0, s, fa,
+                       ba.p.params, ba.p.rel);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  { ProfScope ps_(s, K_CBW_SMALL);
   hipLaunchKernelGGL(cbw_w0_seg_kernel, dim3(5, kW0Seg), dim3(256), 0, s, L.wpart,
                      a->nsrc * a->B * L.ntiles16, L.wseg);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  { ProfScope ps_(s, K_CBW_SMALL);
   hipLaunchKernelGGL(cbw_w0_reduce_kernel, dim3(5), dim3(256), 0, s, L.wseg, c.gacc + PL.raw_off[P_OW0]);
+  }
   return hipGetLastError();
 }
 

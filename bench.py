@@ -264,6 +264,69 @@ def e2e_bench(N: int, H: int, W: int, D: int, B: int, dev, reps: int = 2):
                 images=f"[{B},{N},3,{H},{W}] ~N(0,1)", depth_finite=ok)
 
 
+def backward_work(name: str, B: int, N: int, H: int, W: int, D: int, launches: int):
+    """(kind, amount per launch, peak) of a training-backward kernel (bptt.hip, warp_cost.hip
+    cbw_*), per DESIGN.md §6's per-unit figures, for `launches` launches over D planes:
+      gate_bwd k   52 hid B per cell pixel and plane (z, gz: 4 hid floats each; c, c', dL/dh,
+                   dL/dc read and dL/dc written: hid floats each);
+      dgrad k      2*9*Cin*4hid FLOP per cell pixel and plane (the forward conv transposed;
+                   three split-fp16 products: the cells' ceiling, f16 peak / 3);
+      wgrad k      the same FLOP (four split products: f16 peak / 4);
+      gnb_partial  128 B per deconv output pixel and plane (dL/dr and u, 16 ch each), both deconvs;
+      deconv_bwd   2*16*16*9 FLOP per deconv input pixel and plane (VALU fp32), both deconvs;
+      cbw_feat     per hypothesis: the reference and source features (128 (N) B), dL/dx (128 B),
+                   dL/dt1 and the omega weight per view (20 (N-1) B);
+      cbw_chain    per hypothesis and view: the omega conv output t1 (16 B) per stage (4), the
+                   stage-1 warp and dL/dx (3 x 128 B), dL/do / w / dL/dt1 out (24 B)."""
+    HW = H * W
+    nsrc = N - 1
+    cell = {0: (48, 16, 1), 1: (32, 16, 2), 2: (32, 16, 4), 3: (48, 16, 2), 4: (40, 8, 1)}
+    if name[:-1] in ("gate_bwd", "dgrad", "wgrad") and name[-1].isdigit():
+        cin, hid, sc = cell[int(name[-1])]
+        px = B * HW / (sc * sc) * D
+        if name.startswith("gate_bwd"):
+            return "bytes", 52.0 * hid * px / launches, HBM_PEAK_GBS
+        peak = CELL_PEAK_TFLOPS if name.startswith("dgrad") else F16_PEAK_TFLOPS / 4
+        return "flops", 2.0 * 9 * cin * 4 * hid * px / launches, peak
+    if name == "gnb_partial":
+        return "bytes", 128.0 * B * (HW + HW / 4) * D / launches, HBM_PEAK_GBS
+    if name == "deconv_bwd":
+        return "flops", 2.0 * 16 * 16 * 9 * B * (HW / 4 + HW / 16) * D / launches, FP32_PEAK_TFLOPS
+    if name == "cbw_feat":
+        return "bytes", (128.0 * N + 128.0 + 20.0 * nsrc) * B * HW * D / launches, HBM_PEAK_GBS
+    if name == "cbw_chain":
+        return "bytes", (16.0 * 4 + 3 * 128.0 + 24.0) * nsrc * B * HW * D / launches, HBM_PEAK_GBS
+    return None, 0.0, None
+
+
+def train_kernel_table(prof: dict, B: int, N: int, H: int, W: int, D: int):
+    """Per-kernel rows of one profiled training step: the forward sweep's kernels as in the
+    headline table (kernel_table), the backward's with backward_work's algorithmic work."""
+    fwd = {k: v for k, v in prof.items() if backward_work(k, B, N, H, W, D, 1)[0] is None
+           and k not in ("bwd_small", "cbw_small")}
+    rows = kernel_table(fwd, D, B, N, H, W)
+    total = sum(ms for _, ms in prof.values()) or 1.0
+    for name, (n, ms) in prof.items():
+        kind, amount, peak = backward_work(name, B, N, H, W, D, n)
+        avg_s = ms / n / 1e3
+        row = dict(launches=n, avg_us=round(avg_s * 1e6, 2), share=round(ms / total, 4))
+        if kind == "bytes":
+            ach = amount / avg_s / 1e9
+            row.update(bound="hbm", achieved=round(ach, 1), unit="GB/s", peak=peak, frac=round(ach / peak, 4))
+        elif kind == "flops":
+            ach = amount / avg_s / 1e12
+            row.update(bound="mfma" if name[:-1] in ("dgrad", "wgrad") else "valu", achieved=round(ach, 2),
+                       unit="TFLOP/s", peak=round(peak, 1), frac=round(ach / peak, 4))
+        elif name in ("bwd_small", "cbw_small"):
+            row.update(bound=None, note="fixed-order reductions / small per-group kernels")
+        else:
+            continue
+        rows[name] = row
+    for r in rows.values():
+        r.pop("per_launch", None)
+    return rows
+
+
 def train_bench(dev, D: int = 192, reps: int = 2):
     """Training-step time at config 4 as stated (BASELINE configs[3]: 640x512, N=3, D=192, one
     sample per GPU; train.py:288-307): the drop-in EMVSNet train forward (FeatNet + the HIP
@@ -300,13 +363,28 @@ def train_bench(dev, D: int = 192, reps: int = 2):
     peak = torch.cuda.max_memory_allocated(dev)
     ok = bool(torch.isfinite(loss)) and all(
         p.grad is None or bool(torch.isfinite(p.grad).all()) for p in model.parameters())
+    # one more step with a hipEvent pair around every library launch (the forward's and the
+    # backward's two-stream schedules serialised onto one stream): per-kernel rooflines
+    sw = model._sweep(dev)
+    sw.overlap = False
+    ops.profile_enable(True)
+    ops.profile_reset()
+    step()
+    torch.cuda.synchronize()
+    prof = ops.profile_read()
+    ops.profile_enable(False)
+    sw.overlap = True
+    kern = train_kernel_table(prof, B, N, H, W, D)
+    lib_ms = sum(ms for _, ms in prof.values())
     del model
     return dict(metric="training step (forward + mvsnet_cls_loss + backward), 1 sample / GPU",
                 config="dtu_train_640x512_n3_d192", D=D, s_per_step=round(dt, 4),
                 ms_per_plane=round(dt / D * 1e3, 3), steps_timed=reps,
                 peak_device_gb=round(peak / 1e9, 2),
                 backward=getattr(EMVSNet, "BACKWARD_PATH", "see DESIGN.md §6"),
-                loss_and_grads_finite=ok)
+                loss_and_grads_finite=ok,
+                kernels_timing="separate profiled step, one stream, hipEvents per launch",
+                library_ms_per_step=round(lib_ms, 2), kernels=kern)
 
 
 def spawn_ranks(n: int) -> int:

@@ -1,0 +1,82 @@
+"""Run-to-run bisection of the backward's nondeterminism: one recorded
+forward, then the backward R times on the same inputs and record; per run a SHA-256 of
+dL/dref, the parameter gradients, dL/dx and of the cost-slice backward's scratch buffers left
+by the last group (the omega weights wo, dL/dt1, dL/do, the per-view dL/dref accumulators grefv
+and the source-feature accumulators gsrc8).  Prints which digests vary across runs.
+usage: python tools/bwd_nondet.py [R] [D]   (AARMVS_BWD_PIPE=0 for the one-stream schedule)"""
+import hashlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "aa-rmvsnet_amd")]
+import torch  # noqa: E402
+
+from aarmvs import _lib, ops, synthetic as syn  # noqa: E402
+
+R = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+B, N, H, W = 1, 3, 96, 128
+D = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+nsrc, HW, G = N - 1, 96 * 128, 16
+
+
+def al(x):
+    return (x + 255) // 256 * 256
+
+
+def cost_layout():
+    pblk = max(1, min((HW + 4095) // 4096, 64))
+    nt = ((W + 15) // 16) * ((H + 15) // 16)
+    sizes = [("go", G * B * nsrc * HW * 4), ("wo", G * B * nsrc * HW * 4), ("gt1", G * B * nsrc * HW * 16),
+             ("gsum", G * B * nsrc * 6 * 8), ("part", G * B * nsrc * pblk * 32 * 8),
+             ("wpart", 4 * nsrc * B * nt * 288 * 4), ("wseg", 64 * 1152 * 8),
+             ("gsrc8", nsrc * B * 32 * HW * 4), ("grefv", nsrc * B * 32 * HW * 4)]
+    off, L = 0, {}
+    for k, n in sizes:
+        L[k] = (off, n)
+        off = al(off + n)
+    return L, off
+
+
+def main():
+    sc = syn.scene(B, N, H, W, D, seed=3)
+    P = {k: torch.from_numpy(v).cuda() for k, v in syn.sweep_weights(5).items()}
+    sw = ops.DepthSweep(P, "cuda")
+    f = torch.from_numpy(sc["features"]).cuda()
+    proj = torch.from_numpy(sc["proj_matrices"])
+    dv = torch.from_numpy(sc["depth_values"])
+    ref, srcs = f[0], [f[v] for v in range(1, N)]
+    rec = sw.record_buffers(B, H, W, D, "cuda", nsrc=nsrc)
+    rel = sw.relative(proj[:, 0], [proj[:, v] for v in range(1, N)], B)
+    cost = torch.empty(B, D, H, W, device="cuda")
+    sw(ref, srcs, proj[:, 0], [proj[:, v] for v in range(1, N)], dv, want_depth=False, cost_out=cost,
+       rel=rel, record=rec)
+    torch.manual_seed(0)
+    g = torch.randn_like(cost)
+    CL, cbytes = cost_layout()
+    total = _lib.lib().aarmvs_backward_scratch_bytes(B, H, W, nsrc)
+    breg = total - cbytes
+    runs = []
+    for r in range(R):
+        g_ref, g_src, g_par, g_x = sw.backward(ref, srcs, rel, dv, rec, g, want_grad_x=True)
+        torch.cuda.synchronize()
+        scratch = sw._ws[("bwd", B, H, W, nsrc)]
+        d = {}
+        for name, ts in (("ref", [g_ref]), ("params", [g_par[k] for k in sorted(g_par)]), ("x", [g_x]),
+                         ("src", g_src)):
+            h = hashlib.sha256()
+            for t in ts:
+                h.update(t.detach().cpu().contiguous().numpy().tobytes())
+            d[name] = h.hexdigest()[:12]
+        for k in ("wo", "gt1", "go", "grefv", "gsrc8", "gsum"):
+            o, n = CL[k]
+            d["s:" + k] = hashlib.sha256(scratch[breg + o: breg + o + n].cpu().numpy().tobytes()).hexdigest()[:12]
+        runs.append(d)
+        print(r, " ".join(f"{k}={v}" for k, v in d.items()), flush=True)
+    for k in runs[0]:
+        vals = sorted(set(r[k] for r in runs))
+        print(f"{k:8s} {'VARIES' if len(vals) > 1 else 'same'} ({len(vals)} distinct)")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,5 +1,5 @@
 """GPU half of the dL/dx error bisection: runs test_gpu_bptt's backward at one shape and saves
-the HIP dL/dx per plane ([D,B,32,H,W]) and the recorded cost volume, for the CPU-side analysis
+the HIP dL/dx per plane ([D,B,32,H,W]) and the recorded cost volume, dL/dcost and the record's cost slices and states, for the CPU-side analysis
 in tools/diag_gx_corr.py (which needs no GPU)."""
 import os
 import sys
@@ -24,5 +24,7 @@ for i, (B, N, H, W, D) in enumerate(shapes):
     out[f"gx{i}"] = gx.permute(0, 1, 4, 2, 3).cpu().numpy()
     out[f"cost{i}"] = cost.cpu().numpy()
     out[f"gcost{i}"] = gcost.cpu().numpy()
+    out[f"rec_x{i}"] = rec["x"].view(torch.float32).cpu().numpy()
+    out[f"rec_state{i}"] = rec["state"].view(torch.float32).cpu().numpy()
 np.savez_compressed(os.path.join(ROOT, "gpurun_out", sys.argv[1] if len(sys.argv) > 1 else "gx_dump.npz"), **out)
 print("saved")
