@@ -1398,10 +1398,11 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     hipEvent_t ev[5] = {};   // evA[2], evB[2], fork
   };
   static thread_local PipeSet ps_dev[kMaxDevices];   // one aux stream + events per device
-  static const bool pipe_on = [] {
+  static const int pipe_mode = [] {   // 1 pipelined (default), 0 one stream, 2 two streams in order (diagnostic)
     const char* v = getenv("AARMVS_BWD_PIPE");
-    return !(v && v[0] == '0');
+    return v ? atoi(v) : 1;
   }();
+  const bool pipe_on = pipe_mode != 0;
   int dev = 0;
   CK(current_device(dev));
   PipeSet& ps = ps_dev[dev];
@@ -1451,6 +1452,19 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     // step i: stage A of plane g0 + n - 1 - i, stage B of the plane after it
     for (int i = 0; i <= n; ++i) {
       const int d = g0 + n - 1 - i;
+      if (pipe_mode == 2 && sa != s) {   // diagnostic: B(d + 1), then A(d) after it (no overlap)
+        if (i >= 1) {
+          CK(hipStreamWaitEvent(s, evA[(d + 1) & 1], 0));
+          CK(stage_b(d + 1));
+        }
+        if (i < n) {
+          CK(hipEventRecord(evB[d & 1], s));
+          CK(hipStreamWaitEvent(sa, evB[d & 1], 0));
+          CK(stage_a(d));
+          CK(hipEventRecord(evA[d & 1], sa));
+        }
+        continue;
+      }
       if (i < n) {
         if (sa != s && i >= 2) CK(hipStreamWaitEvent(sa, evB[d & 1], 0));   // B(d + 2) done
         CK(stage_a(d));

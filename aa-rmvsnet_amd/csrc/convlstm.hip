@@ -436,7 +436,7 @@ __device__ __forceinline__ void cell_c_load(const CellArgs& a, int b, int yw, in
 }
 
 // gate epilogue (module.py:83-90): undo the weight scale, add the bias, LSTM update
-template <class C, int ABL>
+template <class C, int ABL, bool PRECISE>
 __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 (&acc)[C::MT][C::RW],
                                               const float (&cst)[C::MT][C::RW][4], float inv_scale,
                                               int b, int yw, int x, int hi) {
@@ -459,6 +459,9 @@ __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 
           if (ABL & 4) {
             cn[q] = gi + gf;
             hn[q] = go + gg + cst[m][r][q];
+          } else if (PRECISE) {   // the training sweep: unbiased activations (device_common.h)
+            cn[q] = precise_sigmoid(gf) * cst[m][r][q] + precise_sigmoid(gi) * precise_tanh(gg);
+            hn[q] = precise_sigmoid(go) * precise_tanh(cn[q]);
           } else {
             cn[q] = fast_sigmoid(gf) * cst[m][r][q] + fast_sigmoid(gi) * fast_tanh(gg);
             hn[q] = fast_sigmoid(go) * fast_tanh(cn[q]);
@@ -492,7 +495,7 @@ __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 
 // ablation bits for the microbenchmark only (1 no MFMA, 2 no staging loads/stores, 4 no
 // gate math)
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
-          int PIPE = CellDef<KIND>::H3PIPE>
+          int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false>
 __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(CellDef<KIND>::MIN_WAVES))) lstm_cell_h3_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
@@ -578,7 +581,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int r = 0; r < RW; ++r) acc[m][r] -= accn[m][r];
-    cell_epilogue<C, ABL>(a, acc, cst, inv_scale, b, yw, x0 + col, hi);
+    cell_epilogue<C, ABL, PRECISE>(a, acc, cst, inv_scale, b, yw, x0 + col, hi);
   }
 }
 
@@ -589,7 +592,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
 // the chunk after that; at a tile's last chunk, the gate epilogue.  Across the two
 // waves of a SIMD one wave's staging VALU work fills the other's MFMA issue gaps.
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
-          int PIPE = CellDef<KIND>::H3PIPE>
+          int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false>
 __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(CellDef<KIND>::MIN_WAVES))) lstm_cell_h3db_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
   using C = H3Cfg<KIND, RW, WAVES>;
@@ -680,7 +683,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
         for (int m = 0; m < MT; ++m)
 #pragma unroll
           for (int r = 0; r < RW; ++r) acc[m][r] -= accn[m][r];
-        cell_epilogue<C, ABL>(a, acc, cst, inv_scale, b, yw, x, hi);
+        cell_epilogue<C, ABL, PRECISE>(a, acc, cst, inv_scale, b, yw, x, hi);
       }
       __syncthreads();   // buffer `oth` staged; buffer `cur` free for the step after next
       par ^= 1;
@@ -698,14 +701,14 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
 // buffer or second fragment set costs it a block per CU).  A warp-specialised form (4
 // staging waves beside the 8 MFMA waves) measured slower (cell 0 0.43 vs 0.40 ms).
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
-          int DB = CellDef<KIND>::H3DB, int PIPE = CellDef<KIND>::H3PIPE>
-static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu, int kid,
-                              hipStream_t s) {
+          int DB = CellDef<KIND>::H3DB, int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false>
+static hipError_t run_cell_h3_(const CellArgs& a, const float* inv_scale, int cu, int kid,
+                               hipStream_t s) {
   using C = H3Cfg<KIND, RW, WAVES>;
   constexpr size_t lds = C::LDS_BYTES + (DB ? (size_t)C::NPIX * 32 * 2 : 0);
   static_assert(lds <= 160 * 1024, "h3 cell tile exceeds LDS");
-  const void* fn = DB ? (const void*)lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE>
-                      : (const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE>;
+  const void* fn = DB ? (const void*)lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE>
+                      : (const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE>;
   static bool attr_set[kMaxDevices] = {};
   if (hipError_t e = ensure_dyn_lds(fn, (int)lds, attr_set); e != hipSuccess) return e;
   const int ntiles = a.B * ((a.W + C::TW - 1) / C::TW) * ((a.H + C::TH - 1) / C::TH);
@@ -713,12 +716,21 @@ static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu,
   const int grid = std::max(1, std::min(ntiles, cu * per_cu));
   ProfScope ps(s, kid);
   if (DB)
-    hipLaunchKernelGGL((lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE>), dim3(grid),
+    hipLaunchKernelGGL((lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE>), dim3(grid),
                        dim3(C::THREADS), lds, s, a, inv_scale);
   else
-    hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE>), dim3(grid),
+    hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE>), dim3(grid),
                        dim3(C::THREADS), lds, s, a, inv_scale);
   return hipGetLastError();
+}
+// The training sweep (a.z_out set: the record for the BPTT) runs the unbiased gate activations
+// (PRECISE, device_common.h); the inference sweep the fast ones.
+template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
+          int DB = CellDef<KIND>::H3DB, int PIPE = CellDef<KIND>::H3PIPE>
+static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu, int kid,
+                              hipStream_t s) {
+  return a.z_out ? run_cell_h3_<KIND, RW, WAVES, ABL, DB, PIPE, true>(a, inv_scale, cu, kid, s)
+                 : run_cell_h3_<KIND, RW, WAVES, ABL, DB, PIPE, false>(a, inv_scale, cu, kid, s);
 }
 
 // ---------------------------------------------------------------------------

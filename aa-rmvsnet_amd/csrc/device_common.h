@@ -38,25 +38,38 @@ __device__ __forceinline__ float ld1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-// Gate activations of the LSTM epilogue: the hardware exp / rcp (v_exp_f32, v_rcp_f32) with the
-// corrections that keep them unbiased.  The bare forms rcp(1 + exp(-x)) and 1 - 2 rcp(exp(2x) + 1)
-// err by +0.30 ulp and, for |x| < 0.5, -0.84 ulp on average (tools/microbench/gate_fn_bias.cpp):
-// a systematic drift that a 192-plane recurrence and the long cancelling sums of the BPTT's
-// parameter gradients turn into errors well above float32's.
-//   sigmoid: one Newton step on the reciprocal (the division to ~0.5 ulp);
-//   tanh: for |x| < 0.625 the odd minimax polynomial x + x^3 P(x^2) (no cancellation), else
-//         1 - 2 / (exp(2|x|) + 1) with the corrected reciprocal.
+// Gate activations of the LSTM epilogue on the hardware exp / rcp (v_exp_f32, v_rcp_f32).
+// Fast forms (the inference sweep): rcp(1 + exp(-x)) and 1 - 2 rcp(exp(2x) + 1), ~1 ulp but
+// biased: +0.30 ulp and, for |tanh| arguments below 0.5, -0.84 ulp on average
+// (tools/microbench/gate_fn_bias.cpp) -- harmless for the depth maps, not for the BPTT, whose
+// 192-plane recurrence and long cancelling parameter-gradient sums turn a drift into errors
+// well above float32's.  Unbiased forms (the training sweep, PRECISE cells):
+//   exp_u: v_exp_f32 of x log2e with the rounding error of the fp32 constant log2e corrected
+//          (it made __expf's error grow as -1.3e-8 |x| relative: the sigmoid's +0.3 ulp);
+//   rcp_nr: one Newton step on the reciprocal (the division to ~0.5 ulp);
+//   tanh: for |x| < 0.625 the odd minimax polynomial x + x^3 P(x^2) (no cancellation).
+__device__ __forceinline__ float fast_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float fast_tanh(float x) {
+  // tanh(x) = 1 - 2 / (exp(2x) + 1); saturates cleanly for large |x| (exp -> inf / 0)
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f);
+}
+__device__ __forceinline__ float exp_u(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 1.44269502f);
+  return fmaf(e, x * 1.3349758e-8f, e);   // x (log2e - fp32(log2e)) ln 2
+}
 __device__ __forceinline__ float rcp_nr(float d) {   // 1 / d for d >= 1 (d = inf -> 0)
   const float r = __builtin_amdgcn_rcpf(d);
   return d < INFINITY ? fmaf(fmaf(-d, r, 1.0f), r, r) : 0.0f;
 }
-__device__ __forceinline__ float fast_sigmoid(float x) { return rcp_nr(1.0f + __expf(-x)); }
-__device__ __forceinline__ float fast_tanh(float x) {
+__device__ __forceinline__ float precise_sigmoid(float x) { return rcp_nr(1.0f + exp_u(-x)); }
+__device__ __forceinline__ float precise_tanh(float x) {
   const float ax = fabsf(x), z = x * x;
   const float p = fmaf(fmaf(fmaf(fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f), z, -5.37397155531e-2f), z,
                             1.33314422036e-1f), z, -3.33332819422e-1f);
   const float small = fmaf(p * z, x, x);
-  const float big = copysignf(1.0f - 2.0f * rcp_nr(__expf(2.0f * ax) + 1.0f), x);
+  const float big = copysignf(1.0f - 2.0f * rcp_nr(exp_u(2.0f * ax) + 1.0f), x);
   return ax < 0.625f ? small : big;
 }
 

@@ -1227,8 +1227,18 @@ struct CbwArgs {
   float4* gt1;           // [n][B][nsrc][HW] dL/dt1 (stage 4 out)
   const double* gsum;    // [n][B][nsrc][3][2] GroupNorm backward sums (stage 1: GN3, 2: GN2, 3: GN1)
   double* part;          // [n][B][nsrc][pblk][32] per-block partial sums
+  unsigned* gmax;        // float bits: [0] max |dL/dx| (stage 1), [1] max |dL/dt1| (stage 4)
   int d0, pblk;
 };
+
+// max |v| of a wave folded into *dst (float bits: non-negative floats order as unsigned; an
+// order-independent, hence deterministic, reduction)
+__device__ __forceinline__ void wave_absmax_bits(float m, unsigned* dst) {
+  const int b = wave_reduce_i32(__float_as_int(m != m ? INFINITY : m), 0,
+                                [](int x, int y) { return x > y ? x : y; });
+  if ((threadIdx.x & 63) == 0 && (unsigned)b > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(dst, (unsigned)b);
+}
 
 // columns of each stage's partial rows: 0, 1 = the GroupNorm sums of the stage's statistic;
 // then parameter-gradient sums (cbw_param_cols)
@@ -1263,6 +1273,7 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
   const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(pa.src[v] + (size_t)b * kC * HW, fbytes);
   const float4* t1p = pa.t1_prev + k * pa.t1_kstride + ((size_t)b * nsrc + v) * HW;
   float* gop = a.go + kbv * HW;
+  float amax = 0.f;   // stage 1: max |dL/dx|, stage 4: max |dL/dt1| (the dL/dsrc fixed-point scale)
   for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
     OmegaChain c;
     omega_chain(t1p[p], gs, o, c);
@@ -1282,6 +1293,7 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
         const float4 sq = sqdiff4(g, ld_c8(rref, (uint32_t)p, sl, HW));
         const float4 gg = *reinterpret_cast<const float4*>(gxp + 4 * sl);
         dw += gg.x * sq.x + gg.y * sq.y + gg.z * sq.z + gg.w * sq.w;
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(gg.x), fabsf(gg.y)), fmaxf(fabsf(gg.z), fabsf(gg.w))));
       }
       dw = -dw / (float)nsrc;
       g_o = dw * c.w * (1.0f - c.w);
@@ -1371,7 +1383,9 @@ __global__ void __launch_bounds__(256) cbw_chain_kernel(CbwArgs a, const float* 
       s[i] += g_t1[i];   // b0
     }
     a.gt1[kbv * HW + p] = make_float4(g_t1[0], g_t1[1], g_t1[2], g_t1[3]);
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(g_t1[0]), fabsf(g_t1[1])), fmaxf(fabsf(g_t1[2]), fabsf(g_t1[3]))));
   }
+  if constexpr (STAGE == 1 || STAGE == 4) wave_absmax_bits(amax, a.gmax + (STAGE == 1 ? 0 : 1));
   block_sum_d_store<NCOL>(s, red, a.part + (kbv * a.pblk + blockIdx.x) * 32);
 }
 
@@ -1406,6 +1420,58 @@ __global__ void __launch_bounds__(256) cbw_param_kernel(const double* __restrict
   if (t == 0) gacc[cols.off[j]] += red[0];
 }
 
+// dL/dsrc in fixed point: the scatter of grid_sample's backward adds contributions from many
+// blocks into one source pixel, and fp32 atomics would make the sum depend on their order.  Each
+// contribution (an fp32 value, or a block's fp32 register sum over its own gathers, formed in a
+// fixed order) is scaled by 2^k (exact) and rounded to a 64-bit integer; integer atomics are
+// associative, so the group's sums are bit-reproducible.  k is chosen per group from a bound on
+// any source pixel's total (cbw_scale_kernel), so nothing overflows and the fixed-point quantum
+// is ~2^-40 of that bound (far below float32's resolution of the values).
+__device__ __forceinline__ unsigned long long to_fixed(float v, int k) {
+  return (unsigned long long)(long long)rintf(ldexpf(v, k));
+}
+
+// k from the group's maxima: |dL/dwarp| = |2 (warp - ref) dL/dsq| <= 4 max|f| (2/nsrc max|dL/dx| +
+// 36 max|w0| max|dL/dt1|) =: G (|warp|, |ref| <= max|f| = sqrt(xbound / 8)), every reference pixel
+// and plane contributes at most G in total (bilinear weights sum to <= 1), so any source pixel's
+// sum over the group is <= HW n G; 2^k HW n G <= 2^61.
+__global__ void cbw_scale_kernel(const unsigned* __restrict__ gmax, const unsigned* __restrict__ xbound,
+                                 const float* __restrict__ w0, int HW, int n, int nsrc, int* __restrict__ fxk) {
+  __shared__ float red[64];
+  float mw = 0.f;
+  for (int i = threadIdx.x; i < 4 * 32 * 9; i += 64) mw = fmaxf(mw, fabsf(w0[i]));
+  red[threadIdx.x] = mw;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 64; ++i) mw = fmaxf(mw, red[i]);
+    const double mf = sqrt((double)__uint_as_float(*xbound) / 8.0);
+    const double g = 4.0 * mf * (2.0 / nsrc * (double)__uint_as_float(gmax[0]) +
+                                 36.0 * (double)mw * (double)__uint_as_float(gmax[1]));
+    const double tot = g * (double)HW * (double)n;
+    int k = 0;
+    if (tot > 0.0 && tot < 1e300) {
+      k = 61 - ilogb(tot) - 1;
+      k = k > 120 ? 120 : (k < -120 ? -120 : k);
+    }
+    *fxk = k;
+  }
+}
+
+// gsrc8 += the group's fixed-point sums (value 2^-k), which are cleared for the next group:
+// the groups are folded in their fixed (reverse plane) order
+__global__ void __launch_bounds__(256) cbw_fold_kernel(unsigned long long* __restrict__ g64,
+                                                       float* __restrict__ gsrc8, size_t n,
+                                                       const int* __restrict__ fxk) {
+  const int k = *fxk;
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const long long q = (long long)g64[i];
+    if (q != 0) {
+      gsrc8[i] += (float)ldexp((double)q, -k);
+      g64[i] = 0ull;
+    }
+  }
+}
+
 // dL/dsq, the feature gradients and the conv3x3 weight gradient.  Block: a 16 x 16 tile of one
 // sample, one source view and one 8-channel chunk, all planes of the group; thread = pixel.
 //   dL/dsq = -(1 + w)/nsrc dL/dx + conv3x3^T(dL/dt1)   (this chunk's 8 channels)
@@ -1438,7 +1504,8 @@ struct CbfArgs {
   const float* gx;          // [n][B][HW][32]
   const float4* gt1;        // [n][B][nsrc][HW]
   const float* w;           // [n][B][nsrc][HW] omega weights (cbw_chain<1>'s)
-  float* gsrc8;             // [nsrc][B][4][HW][8] dL/dsrc (c8 layout) accumulated
+  unsigned long long* gsrc64;   // [nsrc][B][4][HW][8] the group's dL/dsrc (c8 layout) in fixed point
+  const int* fxk;           // the fixed-point exponent k: value = integer 2^-k (cbw_scale_kernel)
   float* grefv;             // [nsrc][B][32][HW] dL/dref per view (NCHW) accumulated
   float* wpart;             // [4 chunks][nsrc][B][tiles][288] conv3x3 weight-gradient partials
   int d0, n;
@@ -1469,6 +1536,7 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
   const PipeArgs& pa = a.p;
   const int tid = threadIdx.x, b = blockIdx.z;
   const int v = blockIdx.y >> 2, c = blockIdx.y & 3;
+  const int fxk = *a.fxk;
   const int H = pa.H, W = pa.W, HW = H * W, nsrc = pa.nsrc;
   const int tiles_x = (W + kFbT - 1) / kFbT;
   const int tx0 = (blockIdx.x % tiles_x) * kFbT, ty0 = (blockIdx.x / tiles_x) * kFbT;
@@ -1651,9 +1719,9 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
         if (xi < 0 || xi >= W || yi < 0 || yi >= H) continue;   // zero padding
         const bool inbox = xi >= bxr.x0 && xi < bxr.x0 + bxr.nx && yi >= bxr.y0 && yi < bxr.y0 + bxr.ny;
         if (filed && inbox) continue;
-        float* gp = a.gsrc8 + ((((size_t)v * pa.B + b) * 4 + c) * HW + (size_t)yi * W + xi) * 8;
+        unsigned long long* gp = a.gsrc64 + ((((size_t)v * pa.B + b) * 4 + c) * HW + (size_t)yi * W + xi) * 8;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) atomicAdd(gp + j, tf.wt[q] * gw[j]);
+        for (int j = 0; j < 8; ++j) atomicAdd(gp + j, to_fixed(tf.wt[q] * gw[j], fxk));
       }
     }
     sq4[tid][0] = make_float4(sqv[0], sqv[1], sqv[2], sqv[3]);
@@ -1711,15 +1779,15 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
   }
   __syncthreads();
   if (use_box && !(AARMVS_CBF_ABL & 8)) {   // flush the owned box pixels (8 channels each)
-    float* gb = a.gsrc8 + (((size_t)v * pa.B + b) * 4 + c) * HW * 8;
+    unsigned long long* gb = a.gsrc64 + (((size_t)v * pa.B + b) * 4 + c) * HW * 8;
 #pragma unroll
     for (int j = 0; j < kFbOwn; ++j) {
       if (obase[j] < 0) continue;
       const int i = tid + 256 * j, ry = i / bxr.nx, rx = i - ry * bxr.nx;
-      float* gp = gb + ((size_t)(bxr.y0 + ry) * W + bxr.x0 + rx) * 8;
+      unsigned long long* gp = gb + ((size_t)(bxr.y0 + ry) * W + bxr.x0 + rx) * 8;
 #pragma unroll
       for (int ch = 0; ch < 8; ++ch)
-        if (own[j][ch] != 0.f) atomicAdd(gp + ch, own[j][ch]);
+        if (own[j][ch] != 0.f) atomicAdd(gp + ch, to_fixed(own[j][ch], fxk));
     }
   }
   const size_t blk = (((size_t)c * nsrc + v) * pa.B + b) * gridDim.x + blockIdx.x;
@@ -1790,6 +1858,9 @@ struct CostBwdLayout {
   double* wseg;
   float* gsrc8;
   float* grefv;
+  unsigned long long* gsrc64;   // the current group's dL/dsrc in fixed point (cbw_feat_kernel)
+  unsigned* gmax;               // [0] max |dL/dx|, [1] max |dL/dt1| of the group (float bits); then
+  int* fxk;                     // the fixed-point exponent
   size_t bytes;
   int pblk, ntiles16;
 };
@@ -1817,6 +1888,9 @@ static CostBwdLayout cost_bwd_layout(void* base, int B, int H, int W, int nsrc) 
   L.wseg = reinterpret_cast<double*>(take((size_t)kW0Seg * 1152 * 8));
   L.gsrc8 = reinterpret_cast<float*>(take((size_t)nsrc * B * 32 * HW * 4));
   L.grefv = reinterpret_cast<float*>(take((size_t)nsrc * B * 32 * HW * 4));
+  L.gsrc64 = reinterpret_cast<unsigned long long*>(take((size_t)nsrc * B * 32 * HW * 8));
+  L.gmax = reinterpret_cast<unsigned*>(take(256));
+  L.fxk = reinterpret_cast<int*>(L.gmax ? L.gmax + 4 : nullptr);
   L.bytes = off;
   return L;
 }
@@ -1841,6 +1915,7 @@ hipError_t cost_bwd_begin(CostBwdCtx& c, hipStream_t s) {
   hipError_t e;
   const size_t HW = (size_t)a->H * a->W;
   if ((e = hipMemsetAsync(L.gsrc8, 0, (size_t)a->nsrc * a->B * 32 * HW * 4, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(L.gsrc64, 0, (size_t)a->nsrc * a->B * 32 * HW * 8, s)) != hipSuccess) return e;
   return hipMemsetAsync(L.grefv, 0, (size_t)a->nsrc * a->B * 32 * HW * 4, s);
 }
 
@@ -1870,8 +1945,10 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   ba.gt1 = L.gt1;
   ba.gsum = L.gsum;
   ba.part = L.part;
+  ba.gmax = L.gmax;
   ba.d0 = g0;
   ba.pblk = L.pblk;
+  if ((e = hipMemsetAsync(L.gmax, 0, 8, s)) != hipSuccess) return e;
   const dim3 grid(L.pblk, a->nsrc, a->B * n);
   const int nkbv = n * a->B * a->nsrc, nrow = nkbv * L.pblk;
   auto cols = [&](int c0, std::initializer_list<std::pair<int, int>> ranges) {
@@ -1950,8 +2027,15 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   fa.gx = gx;
   fa.gt1 = L.gt1;
   fa.w = L.wo;
-  fa.gsrc8 = L.gsrc8;
+  fa.gsrc64 = L.gsrc64;
+  fa.fxk = L.fxk;
   fa.grefv = L.grefv;
+  {
+    ProfScope ps_(s, K_CBW_SMALL);
+    hipLaunchKernelGGL(cbw_scale_kernel, dim3(1), dim3(64), 0, s, L.gmax, c.ws.xbound,
+                       ba.p.params + ba.p.off_ow0, a->H * a->W, n, a->nsrc, L.fxk);
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   fa.wpart = L.wpart;
   fa.d0 = g0;
   fa.n = n;
@@ -1968,6 +2052,13 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   if ((e = hipGetLastError()) != hipSuccess) return e;
   { ProfScope ps_(s, K_CBW_SMALL);
   hipLaunchKernelGGL(cbw_w0_reduce_kernel, dim3(5), dim3(256), 0, s, L.wseg, c.gacc + PL.raw_off[P_OW0]);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  {
+    const size_t nel = (size_t)a->nsrc * a->B * 32 * a->H * a->W;
+    ProfScope ps_(s, K_CBW_SMALL);
+    hipLaunchKernelGGL(cbw_fold_kernel, dim3((unsigned)std::min<size_t>(4096, (nel + 255) / 256)), dim3(256), 0, s,
+                       L.gsrc64, L.gsrc8, nel, L.fxk);
+  }
   }
   return hipGetLastError();
 }

@@ -12,7 +12,7 @@ import torch  # noqa: E402
 from oracle import sweep_oracle as orc  # noqa: E402
 import test_gpu_bptt as T  # noqa: E402
 
-B, N, H, W, D = 1, 3, 32, 48, 6
+B, N, H, W, D = [int(v) for v in os.environ.get("SHAPE", "1,3,32,48,6").split(",")]
 if os.environ.get("ROUND_W"):
     # experiment: cell and deconv weights made exactly representable by the kernels' two fp16
     # terms (after their power-of-two scales), in the GPU and the CPU runs alike

@@ -2,14 +2,18 @@
 # Ceiling analysis of the cost-slice kernels (rocprofv3 PMC passes, one counter set per run,
 # within the gfx950 per-block limits of MI355X_MICROARCH.md): one 16-plane group of the
 # headline sweep (tools/pmc_sweep.py).  Summary: python tools/ceiling_summary.py gpurun_out/ceil
+# CEIL_PROG / CEIL_DIR: another driver (e.g. "tools/pmc_fusion.py" for the fusion kernel) and
+# output directory.
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/ceil
+D=${CEIL_DIR:-gpurun_out/ceil}
+PROG=${CEIL_PROG:-tools/pmc_sweep.py --planes 16}
+mkdir -p $D
 run() {  # run NAME counters...
   local name=$1; shift
-  rm -rf gpurun_out/ceil/$name
-  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/ceil/$name -o p -- \
-    python3 tools/pmc_sweep.py --planes 16 > gpurun_out/ceil/$name.log 2>&1 || { echo "pass $name failed"; tail -3 gpurun_out/ceil/$name.log; exit 1; }
+  rm -rf $D/$name
+  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d $D/$name -o p -- \
+    python3 $PROG > $D/$name.log 2>&1 || { echo "pass $name failed"; tail -3 $D/$name.log; exit 1; }
   echo "pass $name ok"
 }
 run sq_time SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE
