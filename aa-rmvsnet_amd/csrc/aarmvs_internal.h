@@ -153,7 +153,8 @@ hipError_t launch_layout(const float* in, float* out, int B, int C, int HW, bool
 hipError_t launch_to_c8(const float* src, float* dst, int B, int HW, hipStream_t s,
                         unsigned* xbound = nullptr);
 hipError_t launch_omega_group(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d0,
-                              int n, hipStream_t s);
+                              int n, hipStream_t s,
+                              bool balanced = false);
 hipError_t launch_cost_x_group(const CostArgs& a, const SweepGeom& g, const Workspace& ws, int d0,
                                int n, float* x0, float* omega_out, int omega_k, hipStream_t s);
 
@@ -247,12 +248,16 @@ inline hipError_t ensure_dyn_lds(const void* fn, int bytes, bool (&done)[kMaxDev
 struct StreamJoin {
   hipStream_t main, aux;
   hipEvent_t ev;
-  ~StreamJoin() {
+  hipError_t join() {   // order the aux stream's work so far on main (once)
+    hipError_t e = hipSuccess;
     if (aux && aux != main && ev) {
-      (void)hipEventRecord(ev, aux);
-      (void)hipStreamWaitEvent(main, ev, 0);
+      e = hipEventRecord(ev, aux);
+      if (e == hipSuccess) e = hipStreamWaitEvent(main, ev, 0);
     }
+    aux = nullptr;
+    return e;
   }
+  ~StreamJoin() { (void)join(); }
 };
 
 // Backward of the regulariser (bptt.hip) over every plane of a training record: the

@@ -653,7 +653,7 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     // cost stage: its slots were last read by group gi - 2's regulariser steps
     if (aux && gi >= 2 && (e = hipStreamWaitEvent(aux, ev_used[gi & 1], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: event wait");
-    if ((e = launch_omega_group(ca, g, ws, g0, n, cs)) != hipSuccess)
+    if ((e = launch_omega_group(ca, g, ws, g0, n, cs, rec != nullptr)) != hipSuccess)
       return sweep_fail(e, "sweep: omega stage");
     const int ok = d_last < g0 + n ? d_last - g0 : -1;
     if ((e = launch_cost_x_group(ca, g, ws, g0, n, xs, ok >= 0 ? a->omega_out : nullptr, ok, cs)) !=

@@ -86,6 +86,26 @@ struct BpttLayout {
   double* gacc;        // [raw param count] fp64 parameter-gradient accumulators
   float* wpart;        // [kWgBlocks][kWgPartMax] wgrad partials
   double* rseg;        // [kRedSeg][kWgPartMax] segment sums of the partials
+  // the per-group buffers above (gz, zmax, gu, gx, gnb_part) exist twice, one set per group
+  // parity, so that a group's weight-gradient and cost-slice stage can run beside the next
+  // group's planes; use_set(p) points the fields at set p
+  struct GroupSet {
+    float* gz[5];
+    unsigned* zmax;
+    float* gu[2];
+    float* gx;
+    double* gnb_part[2];
+  } set[2];
+  void use_set(int p) {
+    const GroupSet& g = set[p];
+    for (int k = 0; k < 5; ++k) gz[k] = g.gz[k];
+    zmax = g.zmax;
+    gu[0] = g.gu[0];
+    gu[1] = g.gu[1];
+    gx = g.gx;
+    gnb_part[0] = g.gnb_part[0];
+    gnb_part[1] = g.gnb_part[1];
+  }
   size_t bytes;
   size_t cell_px[5];
   int gnb_nblk;
@@ -111,9 +131,20 @@ BpttLayout bptt_layout(void* base, int B, int H, int W) {
     L.cell_px[k] = (size_t)B * px[k];
     L.gh[k] = reinterpret_cast<float*>(take(L.cell_px[k] * kCellHid[k] * 4));
     L.gc[k] = reinterpret_cast<float*>(take(L.cell_px[k] * kCellHid[k] * 4));
-    L.gz[k] = reinterpret_cast<float*>(take((size_t)G * L.cell_px[k] * 4 * kCellHid[k] * 4));
   }
-  L.zmax = reinterpret_cast<unsigned*>(take(5 * G * 4));
+  L.gnb_nblk = (int)std::min<size_t>(512, (HW + 1023) / 1024);
+  for (int q = 0; q < 2; ++q) {
+    BpttLayout::GroupSet& g = L.set[q];
+    for (int k = 0; k < 5; ++k)
+      g.gz[k] = reinterpret_cast<float*>(take((size_t)G * L.cell_px[k] * 4 * kCellHid[k] * 4));
+    g.zmax = reinterpret_cast<unsigned*>(take(5 * G * 4));
+    g.gu[0] = reinterpret_cast<float*>(take((size_t)G * B * (HW / 4) * 16 * 4));
+    g.gu[1] = reinterpret_cast<float*>(take((size_t)G * B * HW * 16 * 4));
+    g.gx = reinterpret_cast<float*>(take((size_t)G * B * HW * kC * 4));
+    for (int j = 0; j < 2; ++j)
+      g.gnb_part[j] = reinterpret_cast<double*>(take((size_t)G * B * L.gnb_nblk * 36 * 8));
+  }
+  L.use_set(0);
   L.gr[0] = reinterpret_cast<float*>(take((size_t)B * (HW / 4) * 16 * 4));
   L.gr[1] = reinterpret_cast<float*>(take((size_t)B * HW * 16 * 4));
   L.gr0b = reinterpret_cast<float*>(take((size_t)B * (HW / 4) * 16 * 4));
@@ -121,12 +152,6 @@ BpttLayout bptt_layout(void* base, int B, int H, int W) {
     for (int k = 0; k < 2; ++k) L.gskip[q][k] = reinterpret_cast<float*>(take(L.cell_px[k] * 16 * 4));
   L.gpool[0] = reinterpret_cast<float*>(take((size_t)B * (HW / 4) * 16 * 4));
   L.gpool[1] = reinterpret_cast<float*>(take((size_t)B * (HW / 16) * 16 * 4));
-  L.gu[0] = reinterpret_cast<float*>(take((size_t)G * B * (HW / 4) * 16 * 4));
-  L.gu[1] = reinterpret_cast<float*>(take((size_t)G * B * HW * 16 * 4));
-  L.gx = reinterpret_cast<float*>(take((size_t)G * B * HW * kC * 4));
-  L.gnb_nblk = (int)std::min<size_t>(512, (HW + 1023) / 1024);
-  for (int j = 0; j < 2; ++j)
-    L.gnb_part[j] = reinterpret_cast<double*>(take((size_t)G * B * L.gnb_nblk * 36 * 8));
   L.gacc = reinterpret_cast<double*>(take(param_layout().raw_total * 8));
   L.wpart = reinterpret_cast<float*>(take((size_t)kWgBlocks * kWgPartMax * 4));
   L.rseg = reinterpret_cast<double*>(take((size_t)kRedSeg * kWgPartMax * 8));
@@ -1391,37 +1416,54 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
   // and added by cells 0 and 1's gate backward (the same single fp32 add: the same bits in
   // either schedule).  Events: evA[p] "stage A of a parity-p plane done" (aux -> main),
   // evB[p] "stage B of a parity-p plane done" (main -> aux: its parity buffers are free).
-  // AARMVS_BWD_PIPE=0 runs both stages on the caller's stream (A/B runs; tested bit-equal).
+  // The group stage (weight gradients, dL/dx copy-out, the cost-slice backward of the group)
+  // runs on a third stream beside the next group's planes: it reads only the group's buffer
+  // set (gz, zmax, gu, gx, GroupNorm partials; two sets, by group parity) and the record, and
+  // writes only the parameter accumulators and the cost-slice scratch, which the plane chain
+  // never touches.  Events: evP "the group's planes done" (main -> group stream), evG[p] "the
+  // group stage of a parity-p group done" (its set is free again).
+  // AARMVS_BWD_PIPE: 3 the plane pipeline only (default), 1 both overlaps, 0 everything on the caller's
+  // stream, 2 the plane stages on two streams in order; diagnostics: 4 the group stage on its
+  // stream but waited for at once, 5 the group overlap without the plane pipeline.
   struct PipeSet {
     int dev = -1;
-    hipStream_t aux = nullptr;
-    hipEvent_t ev[5] = {};   // evA[2], evB[2], fork
+    hipStream_t aux = nullptr, grp = nullptr;
+    hipEvent_t ev[9] = {};   // evA[2], evB[2], fork, evP, evG[2], group join
   };
-  static thread_local PipeSet ps_dev[kMaxDevices];   // one aux stream + events per device
-  static const int pipe_mode = [] {   // 1 pipelined (default), 0 one stream, 2 two streams in order (diagnostic)
+  static thread_local PipeSet ps_dev[kMaxDevices];   // aux streams + events per device
+  static const int pipe_mode = [] {
     const char* v = getenv("AARMVS_BWD_PIPE");
-    return v ? atoi(v) : 1;
+    return v ? atoi(v) : 3;
   }();
   const bool pipe_on = pipe_mode != 0;
   int dev = 0;
   CK(current_device(dev));
   PipeSet& ps = ps_dev[dev];
-  hipStream_t sa = s;
+  hipStream_t sa = s, sg = s;
+  const hipStream_t sg0 = s;   // the caller's stream
   if (pipe_on && !g_prof_on) {   // (per-kernel timing runs on one stream: isolated kernel spans)
     if (ps.dev != dev) {
       CK(hipStreamCreateWithFlags(&ps.aux, hipStreamNonBlocking));
+      CK(hipStreamCreateWithFlags(&ps.grp, hipStreamNonBlocking));
       for (hipEvent_t& x : ps.ev) CK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
       ps.dev = dev;
     }
-    sa = ps.aux;
+    if (pipe_mode != 5) sa = ps.aux;
+    if (pipe_mode == 1 || pipe_mode == 4 || pipe_mode == 5) sg = ps.grp;
   }
-  // every return from here on (errors included) leaves the aux stream's work ordered on s
+  // every return from here on (errors included) leaves the aux streams' work ordered on s
   StreamJoin join{s, sa, ps.ev[4]};
+  StreamJoin join_g{s, sg, ps.ev[8]};
   hipEvent_t* evA = ps.ev;
   hipEvent_t* evB = ps.ev + 2;
+  hipEvent_t evP = ps.ev[5];
+  hipEvent_t* evG = ps.ev + 6;
   auto gr0_of = [&](int d) { return (d & 1) ? L.gr0b : L.gr[0]; };
-  for (int g0 = ((D - 1) / G) * G; g0 >= 0; g0 -= G) {
+  int gi = 0;
+  for (int g0 = ((D - 1) / G) * G; g0 >= 0; g0 -= G, ++gi) {
     const int n = std::min(G, D - g0);
+    L.use_set(gi & 1);
+    if (sg != s && gi >= 2) CK(hipStreamWaitEvent(s, evG[gi & 1], 0));   // set free again
     CK(hipMemsetAsync(L.zmax, 0, 5 * G * 4, s));
     if (sa != s) {   // the aux stream starts after everything the group's stage A overwrites is consumed
       CK(hipEventRecord(ps.ev[4], s));
@@ -1476,7 +1518,13 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
         if (sa != s) CK(hipEventRecord(evB[(d + 1) & 1], s));
       }
     }
-    // ---- weight gradients of the group ----
+    // ---- the group stage: weight gradients of the group, then its cost-slice backward ----
+    if (sg != s) {
+      CK(hipEventRecord(evP, s));
+      CK(hipStreamWaitEvent(sg, evP, 0));
+    }
+    {
+    const hipStream_t s = sg;   // (the group stage's launches below)
     for (int k = 0; k < 5; ++k) {
       {
         ProfScope ps(s, K_BWD_SMALL);
@@ -1601,7 +1649,11 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     if (r.grad_x)
       CK(hipMemcpyAsync(r.grad_x + (size_t)g0 * xs, L.gx, (size_t)n * xs * 4, hipMemcpyDeviceToDevice, s));
     if (r.group_done) CK(r.group_done(r.ctx, g0, n, L.gx, s));
+    if (s != sg0) CK(hipEventRecord(evG[gi & 1], s));
+    }
+    if (pipe_mode == 4 && sg != s) CK(hipStreamWaitEvent(s, evG[gi & 1], 0));
   }
+  CK(join_g.join());
   if (r.grad_params) {
     hipLaunchKernelGGL(gacc_to_float_kernel, dim3(256), dim3(256), 0, s, L.gacc, r.grad_params,
                        PL.raw_total);

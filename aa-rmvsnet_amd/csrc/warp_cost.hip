@@ -632,7 +632,8 @@ constexpr int kOmegaTW = 16;   // the library's tile width
 // library instantiates ABL = 0): 1 no MFMAs, 2 no box DMA, 4 no box sampling, 8 no reference
 // loads, 16 sampling positions without the homography divisions (the own pixel), 32 no Y
 // image / gather (t1 from the accumulators), 64 no statistics atomics, 128 no B-fragment loads
-template <int ABL = 0, int TW = kOmegaTW>
+// BAL: sign-balanced accumulation, for the training sweep only: +9% time
+template <int ABL = 0, int TW = kOmegaTW, bool BAL = false>
 __global__ void __launch_bounds__(OmegaTile<TW>::NT) __attribute__((amdgpu_waves_per_eu(4)))
 omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restrict__ Rel,
                   const unsigned* __restrict__ xbound) {
@@ -789,6 +790,22 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
       hw[i] = r[0];
       lw[i] = r[1];
     }
+    // BAL: odd chunks accumulate the negated sum (accumulators and A negated), so the matrix
+    // cores' downward rounding alternates sign
+    if (BAL && (c & 1)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        hw[i] ^= 0x80008000u;
+        lw[i] ^= 0x80008000u;
+      }
+    }
+    if (BAL && c > 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc0[r] = -acc0[r];
+        acc1[r] = -acc1[r];
+      }
+    }
     const half8 A0 = __builtin_bit_cast(half8, u32x4{hw[0], hw[1], hw[2], hw[3]});
     const half8 A1 = __builtin_bit_cast(half8, u32x4{lw[0], lw[1], lw[2], lw[3]});
     half8 Bd, Bl, Bl2;
@@ -825,8 +842,8 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int px = (r & 3) + 8 * (r >> 2) + rb;
-      yimg[(64 * wave + px) * kMYStride + col] = acc0[r];
-      yimg[(64 * wave + 32 + px) * kMYStride + col] = acc1[r];
+      yimg[(64 * wave + px) * kMYStride + col] = BAL ? -acc0[r] : acc0[r];   // (BAL: chunk 3 left -sum)
+      yimg[(64 * wave + 32 + px) * kMYStride + col] = BAL ? -acc1[r] : acc1[r];
     }
   }
   __syncthreads();
@@ -1040,7 +1057,7 @@ hipError_t launch_cost_x_group(const CostArgs& ca, const SweepGeom& g, const Wor
 }
 
 hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Workspace& ws, int d0,
-                              int n, hipStream_t s) {
+                              int n, hipStream_t s, bool balanced) {
   PipeArgs a = pipe_args_c8(ca, g, ws);
   group_strides(a, ws, n);
   a.d_prev = -1;
@@ -1057,9 +1074,12 @@ hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Work
     const int ntiles = OmegaTile<kOmegaTW>::tiles(g.H, g.W);
     ProfScope ps(s, K_OMEGA_CONV);
     a.part_n = ntiles;
-    hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW>), dim3(ntiles * g.nsrc * n, 1, g.B),
-                       dim3(OmegaTile<kOmegaTW>::NT), 0, s,
-                       a, a.params, a.rel, ws.xbound);
+    if (balanced)
+      hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW, true>), dim3(ntiles * g.nsrc * n, 1, g.B),
+                         dim3(OmegaTile<kOmegaTW>::NT), 0, s, a, a.params, a.rel, ws.xbound);
+    else
+      hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW>), dim3(ntiles * g.nsrc * n, 1, g.B),
+                         dim3(OmegaTile<kOmegaTW>::NT), 0, s, a, a.params, a.rel, ws.xbound);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   {
@@ -1459,15 +1479,35 @@ __global__ void cbw_scale_kernel(const unsigned* __restrict__ gmax, const unsign
 
 // gsrc8 += the group's fixed-point sums (value 2^-k), which are cleared for the next group:
 // the groups are folded in their fixed (reverse plane) order
+// AARMVS_COH (diagnostic builds only, tools/bwd_nondet.py): the cost-slice backward's reads of
+// buffers written by earlier kernels as agent-scope atomic loads, its read-modify-writes as
+// agent-scope atomic loads and stores (L2-coherent across XCDs); the library is built with 0
+#ifndef AARMVS_COH
+#define AARMVS_COH 0
+#endif
+template <typename T>
+__device__ __forceinline__ T coh_ld(const T* p) {
+  if constexpr (AARMVS_COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <typename T>
+__device__ __forceinline__ void coh_st(T* p, T v) {
+  if constexpr (AARMVS_COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+__device__ __forceinline__ float4 coh_ld4(const float* p) {
+  if constexpr (AARMVS_COH) return make_float4(coh_ld(p), coh_ld(p + 1), coh_ld(p + 2), coh_ld(p + 3));
+  else return *reinterpret_cast<const float4*>(p);
+}
 __global__ void __launch_bounds__(256) cbw_fold_kernel(unsigned long long* __restrict__ g64,
                                                        float* __restrict__ gsrc8, size_t n,
                                                        const int* __restrict__ fxk) {
   const int k = *fxk;
   for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-    const long long q = (long long)g64[i];
+    const long long q = (long long)coh_ld(g64 + i);
     if (q != 0) {
-      gsrc8[i] += (float)ldexp((double)q, -k);
-      g64[i] = 0ull;
+      coh_st(gsrc8 + i, coh_ld(gsrc8 + i) + (float)ldexp((double)q, -k));
+      coh_st(g64 + i, 0ull);
     }
   }
 }
@@ -1610,8 +1650,9 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
   const int hi0 = tid, hi1 = tid + 256;
   auto halo = [&](int i, size_t kbv) {
     const int hy = i / 18, hx = i % 18, gy = ty0 - 1 + hy, gxx = tx0 - 1 + hx;
-    return (i < 18 * 18 && gy >= 0 && gy < H && gxx >= 0 && gxx < W) ? a.gt1[kbv * HW + gy * W + gxx]
-                                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    return (i < 18 * 18 && gy >= 0 && gy < H && gxx >= 0 && gxx < W)
+               ? coh_ld4(reinterpret_cast<const float*>(a.gt1 + kbv * HW + gy * W + gxx))
+               : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   float4 nh0, nh1, ngx0, ngx1, ns[4][2];
   float nw = 0.f;
@@ -1621,10 +1662,10 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
     nh0 = halo(hi0, kbv);
     nh1 = halo(hi1, kbv);
     if (in) {
-      nw = a.w[kbv * HW + p];
+      nw = coh_ld(a.w + kbv * HW + p);
       const float* gxp = gxb + (((size_t)k * pa.B + b) * HW + p) * kC;
-      ngx0 = *reinterpret_cast<const float4*>(gxp);
-      ngx1 = *reinterpret_cast<const float4*>(gxp + 4);
+      ngx0 = coh_ld4(gxp);
+      ngx1 = coh_ld4(gxp + 4);
       ntf = tap_f(m, pa.dvals[b * pa.D + a.d0 + k], x, y, H, W);
       const Box none{0, 0, 0, 0};
       const TapP t = tap_p(ntf, true, H, W, false, none, fbytes / 32u);
@@ -1694,31 +1735,30 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
       }
     }
     // grid_sample backward: file the pixel under its top-left tap's cell for the gather below;
-    // taps that are not gathered (in-image corners outside the box, every corner of a pixel not
-    // filed) are scattered with global atomics here
+    // taps that are never gathered (in-image corners outside the box, every corner of a pixel
+    // outside the cells) are scattered with fixed-point global atomics here.  Whether a filed
+    // pixel is gathered depends only on its cell's final count (read after the barrier), so the
+    // result does not depend on the order the LDS atomics were served in.
+    int kx = 0, ky = 0;
     if (in && !(AARMVS_CBF_ABL & 2) && tf.xf == tf.xf && tf.yf == tf.yf) {
-      const int kx = (int)fminf(fmaxf(tf.xf, -8.f), (float)W + 8.f);
-      const int ky = (int)fminf(fmaxf(tf.yf, -8.f), (float)H + 8.f);
+      kx = (int)fminf(fmaxf(tf.xf, -8.f), (float)W + 8.f);
+      ky = (int)fminf(fmaxf(tf.yf, -8.f), (float)H + 8.f);
       const int cx = kx - bxr.x0 + 1, cy = ky - bxr.y0 + 1;
-      bool filed = false;
       if (use_box && cx >= 0 && cx < cw && cy >= 0 && cy <= bxr.ny) {
         const int cell = cy * cw + cx;
         const int slot = atomicAdd(&cnt[cell], 1);
         mycell = cell;
-        if (slot < kFbSlots) {
-          lst[cell][slot] = (unsigned short)tid;
-          gwim[tid][0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
-          gwim[tid][1] = make_float4(gw[4], gw[5], gw[6], gw[7]);
-          wtim[tid] = make_float4(tf.wt[0], tf.wt[1], tf.wt[2], tf.wt[3]);
-          filed = true;
-        }
+        if (slot < kFbSlots) lst[cell][slot] = (unsigned short)tid;
+        gwim[tid][0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
+        gwim[tid][1] = make_float4(gw[4], gw[5], gw[6], gw[7]);
+        wtim[tid] = make_float4(tf.wt[0], tf.wt[1], tf.wt[2], tf.wt[3]);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int xi = kx + (q & 1), yi = ky + (q >> 1);
         if (xi < 0 || xi >= W || yi < 0 || yi >= H) continue;   // zero padding
         const bool inbox = xi >= bxr.x0 && xi < bxr.x0 + bxr.nx && yi >= bxr.y0 && yi < bxr.y0 + bxr.ny;
-        if (filed && inbox) continue;
+        if (mycell >= 0 && inbox) continue;
         unsigned long long* gp = a.gsrc64 + ((((size_t)v * pa.B + b) * 4 + c) * HW + (size_t)yi * W + xi) * 8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) atomicAdd(gp + j, to_fixed(tf.wt[q] * gw[j], fxk));
@@ -1740,7 +1780,25 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
           for (int j = 0; j < 4; ++j) wacc[co * 4 + j] = fmaf(g4[co], s4[j], wacc[co * 4 + j]);
       }
     }
-    // the gather: owned source pixel s takes corner q of the pixels filed under cell s - q
+    // a cell holding more than kFbSlots pixels is not gathered: its pixels scatter their in-box
+    // corners with the fixed-point atomics
+    if (mycell >= 0 && cnt[mycell] > kFbSlots) {
+      const float4 wq = wtim[tid], g0 = gwim[tid][0], g1 = gwim[tid][1];
+      const float wt4[4] = {wq.x, wq.y, wq.z, wq.w};
+      const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int xi = kx + (q & 1), yi = ky + (q >> 1);
+        if (xi < 0 || xi >= W || yi < 0 || yi >= H) continue;
+        const bool inbox = xi >= bxr.x0 && xi < bxr.x0 + bxr.nx && yi >= bxr.y0 && yi < bxr.y0 + bxr.ny;
+        if (!inbox) continue;
+        unsigned long long* gp = a.gsrc64 + ((((size_t)v * pa.B + b) * 4 + c) * HW + (size_t)yi * W + xi) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomicAdd(gp + j, to_fixed(wt4[q] * gv[j], fxk));
+      }
+    }
+    // the gather: owned source pixel s takes corner q of the pixels filed under cell s - q, in
+    // ascending tile-index order
     if (use_box && !(AARMVS_CBF_ABL & 2)) {
 #pragma unroll
       for (int j = 0; j < kFbOwn; ++j) {
@@ -1748,9 +1806,11 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int cell = obase[j] - (q >> 1) * cw - (q & 1);
-          const int n = min(cnt[cell], kFbSlots);
+          const int n = cnt[cell];
+          if (n > kFbSlots) continue;
+          const int l0 = lst[cell][0], l1 = lst[cell][1];
           for (int sl = 0; sl < n; ++sl) {
-            const int pp = lst[cell][sl];
+            const int pp = n == 1 ? l0 : (sl == 0 ? min(l0, l1) : max(l0, l1));
             const float4 wq = wtim[pp];
             const float w = q == 0 ? wq.x : q == 1 ? wq.y : q == 2 ? wq.z : wq.w;
             const float4 g0 = gwim[pp][0], g1 = gwim[pp][1];
@@ -1770,7 +1830,7 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
   if (in) {
     float* gr = a.grefv + ((size_t)v * pa.B + b) * kC * HW + p;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gr[(size_t)(8 * c + j) * HW] += gref[j];
+    for (int j = 0; j < 8; ++j) coh_st(gr + (size_t)(8 * c + j) * HW, coh_ld(gr + (size_t)(8 * c + j) * HW) + gref[j]);
   }
   __syncthreads();   // every gather of the last plane done: the scratch becomes the subset sums
   if (tid < kWgPairs * kWgSubs) {

@@ -1,6 +1,6 @@
 """Helper of tests/test_gpu_bptt.py::test_backward_pipeline_schedule_is_bit_exact: one recorded
 training sweep and its backward (aarmvs_sweep_backward) at a small geometry spanning two plane
-groups (D = 20: 16 + 4, odd and even planes), printing a SHA-256 of every gradient's bytes and saving the
+groups (D = 36: 16 + 16 + 4, odd and even planes, both group buffer sets), printing a SHA-256 of every gradient's bytes and saving the
 source-feature gradients to argv[1] (.npy: their scatter flushes overlapping boxes with fp32
 atomics, so they agree between runs to rounding only).  Run once per schedule
 (AARMVS_BWD_PIPE=0: both backward stages on one stream; default: the two-stream plane
@@ -19,7 +19,7 @@ import torch  # noqa: E402
 
 from aarmvs import ops, synthetic as syn  # noqa: E402
 
-B, N, H, W, D = 1, 3, 96, 128, 20
+B, N, H, W, D = 1, 3, 96, 128, 36
 sc = syn.scene(B, N, H, W, D, seed=3)
 P = {k: torch.from_numpy(v).cuda() for k, v in syn.sweep_weights(5).items()}
 sw = ops.DepthSweep(P, "cuda")

@@ -192,17 +192,18 @@ def test_backward_is_deterministic_in_the_parameter_gradients():
 
 
 def test_backward_pipeline_schedule_is_bit_exact(tmp_path):
-    """The backward's two-stream plane pipeline (stage A of plane d beside stage B of plane
-    d + 1, bptt.hip) against the one-stream schedule (AARMVS_BWD_PIPE=0), over two plane
-    groups (D = 20; the forward's cost volume digest too): dL/dref, dL/dx and every parameter
-    gradient bit for bit, dL/dsrc included (its scatter sums in fixed point); the schedule only
-    moves kernels between streams, so a missing dependency shows up as a differing digest (the
-    pipelined run is repeated)."""
+    """The backward's default stream schedule (bptt.hip, AARMVS_BWD_PIPE=3: the plane pipeline,
+    stage A of plane d beside stage B of plane d + 1) against the one-stream schedule (0), over
+    three plane groups (D = 36, both group buffer sets; the forward's cost volume digest too):
+    dL/dref, dL/dx, dL/dsrc and every parameter gradient bit for bit (the scatter sums in fixed
+    point, in an order fixed by construction); the schedule only moves kernels between
+    streams, so a missing dependency shows up as a differing digest (the default schedule is
+    run twice)."""
     import subprocess
     import sys
     helper = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bwd_digest.py")
     out = {}
-    for run, pipe in (("0", "0"), ("1", "1"), ("2", "1")):   # the pipelined schedule twice (races)
+    for run, pipe in (("0", "0"), ("1", "3"), ("2", "3")):   # the default twice (races)
         env = dict(os.environ, AARMVS_BWD_PIPE=pipe)
         f = str(tmp_path / f"src{run}.npy")
         r = subprocess.run([sys.executable, helper, f], env=env, capture_output=True, text=True, timeout=100)

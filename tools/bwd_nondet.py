@@ -30,12 +30,38 @@ def cost_layout():
     sizes = [("go", G * B * nsrc * HW * 4), ("wo", G * B * nsrc * HW * 4), ("gt1", G * B * nsrc * HW * 16),
              ("gsum", G * B * nsrc * 6 * 8), ("part", G * B * nsrc * pblk * 32 * 8),
              ("wpart", 4 * nsrc * B * nt * 288 * 4), ("wseg", 64 * 1152 * 8),
-             ("gsrc8", nsrc * B * 32 * HW * 4), ("grefv", nsrc * B * 32 * HW * 4)]
+             ("gsrc8", nsrc * B * 32 * HW * 4), ("grefv", nsrc * B * 32 * HW * 4),
+             ("gsrc64", nsrc * B * 32 * HW * 8), ("gmax", 256)]
     off, L = 0, {}
     for k, n in sizes:
         L[k] = (off, n)
         off = al(off + n)
     return L, off
+
+
+def where(a, b):
+    """Where run b differs from run 0: dL/dx per plane (count, max |diff|, pixels), dL/dref
+    per channel, dL/dsrc per view, and the parameter tensors that differ."""
+    x0, x1 = a["x"], b["x"]   # [D][B][H][W][32]
+    dx = (x0 != x1)
+    if dx.any():
+        planes = dx.reshape(dx.shape[0], -1).sum(1)
+        pl = [(int(i), int(planes[i]), float((x0[i] - x1[i]).abs().max())) for i in range(len(planes)) if planes[i]]
+        print(f"   x: {len(pl)} planes differ, d = {[p[0] for p in pl]}; top plane {pl[-1]}; "
+              f"max {max(p[2] for p in pl):.2e}", flush=True)
+        i = pl[0][0]
+        idx = dx[i].nonzero()[:8].tolist()
+        print("   x first plane diffs at [b,y,x,c]:", idx, flush=True)
+    for name in ("ref", "src"):
+        t0, t1 = a[name], b[name]
+        m = t0 != t1
+        if m.any():
+            nz = m.nonzero()
+            print(f"   {name}: n={int(m.sum())} max={float((t0 - t1).abs().max()):.3e} "
+                  f"first={nz[:6].tolist()}", flush=True)
+    ps = [k for k in a["params"] if not torch.equal(a["params"][k], b["params"][k])]
+    if ps:
+        print(f"   params differ: {len(ps)} tensors, e.g. {ps[:3]}", flush=True)
 
 
 def main():
@@ -73,6 +99,13 @@ def main():
             d["s:" + k] = hashlib.sha256(scratch[breg + o: breg + o + n].cpu().numpy().tobytes()).hexdigest()[:12]
         runs.append(d)
         print(r, " ".join(f"{k}={v}" for k, v in d.items()), flush=True)
+        cur = {"x": g_x.detach().cpu().clone(), "ref": g_ref.detach().cpu().clone(),
+               "src": torch.stack([t.detach().cpu() for t in g_src]),
+               "params": {k: v.detach().cpu().clone() for k, v in g_par.items()}}
+        if r == 0:
+            first = cur
+        else:
+            where(first, cur)
     for k in runs[0]:
         vals = sorted(set(r[k] for r in runs))
         print(f"{k:8s} {'VARIES' if len(vals) > 1 else 'same'} ({len(vals)} distinct)")
