@@ -310,6 +310,7 @@ enum KernelId : int {
   K_DGRAD0, K_DGRAD1, K_DGRAD2, K_DGRAD3, K_DGRAD4,
   K_WGRAD0, K_WGRAD1, K_WGRAD2, K_WGRAD3, K_WGRAD4,
   K_GNB_PARTIAL, K_DECONV_BWD, K_BWD_SMALL, K_CBW_CHAIN, K_CBW_FEAT, K_CBW_SMALL,
+  K_DECONV_WGRAD, K_HEAD_WGRAD,
   K_COUNT
 };
 extern bool g_prof_on;

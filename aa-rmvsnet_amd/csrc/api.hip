@@ -94,7 +94,8 @@ static const char* kKernelNames[K_COUNT] = {
     "gate_bwd0", "gate_bwd1", "gate_bwd2", "gate_bwd3", "gate_bwd4",
     "dgrad0", "dgrad1", "dgrad2", "dgrad3", "dgrad4",
     "wgrad0", "wgrad1", "wgrad2", "wgrad3", "wgrad4",
-    "gnb_partial", "deconv_bwd", "bwd_small", "cbw_chain", "cbw_feat", "cbw_small"};
+    "gnb_partial", "deconv_bwd", "bwd_small", "cbw_chain", "cbw_feat", "cbw_small",
+    "deconv_wgrad", "head_wgrad"};
 
 static hipEvent_t prof_event() {
   if (g_prof_used == g_prof_pool.size()) {

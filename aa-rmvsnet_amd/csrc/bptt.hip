@@ -54,16 +54,40 @@ __device__ __forceinline__ void split16(float v, _Float16& hi, _Float16& lo) {
 }
 
 // max |v| of a wave folded into *dst (float bits: non-negative floats order as unsigned)
-__device__ __forceinline__ void wave_absmax_to(float m, unsigned* dst) {
+// The block's max |v| (NaN as +inf) as float bits, one plain store per block: the scale maxima
+// are per-block partials reduced by their consumers in a fixed way, no atomics (deterministic
+// whatever the schedule).
+__device__ __forceinline__ void block_absmax_store(float m, unsigned* dst) {
+  __shared__ float wm[16];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float q = __shfl_xor(m, o, 64);
     m = (q > m || q != q) ? q : m;
   }
-  if ((threadIdx.x & 63) == 0) {
-    const unsigned bits = __float_as_uint(m != m ? INFINITY : m);
-    if (bits > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(dst, bits);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) wm[w] = m != m ? INFINITY : fabsf(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = 0.f;
+    for (int i = 0; i < nw; ++i) b = fmaxf(b, wm[i]);
+    *dst = __float_as_uint(b);
   }
+}
+
+// max over n partial maxima (float bits) by the whole block; every thread gets the result
+__device__ __forceinline__ unsigned block_max_of(const unsigned* p, int n) {
+  __shared__ unsigned wm[16];
+  unsigned m = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) m = max(m, p[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) wm[w] = m;
+  __syncthreads();
+  unsigned r = 0;
+  for (int i = 0; i < nw; ++i) r = max(r, wm[i]);
+  return r;
 }
 
 // ---------------------------------------------------------------------------
@@ -75,7 +99,9 @@ struct BpttLayout {
   float* gh[5];        // dL/dh of the state the current plane leaves [Pk][hid]
   float* gc[5];        // dL/dc likewise
   float* gz[5];        // [G][Pk][4 hid] gate gradients of the group's planes
-  unsigned* zmax;      // [5][G] float bits of max |gz| per (cell, group plane)
+  unsigned* zmax;      // [5][G] float bits of max |gz| per (cell, group plane), after zmax_group
+  unsigned* zpart;     // [5][G][zp_n] per-gate-block maxima of |gz| (float bits), plain stores
+  int zp_n;            // partial slots per (cell, plane): the gate kernel's largest grid
   float* gr[2];        // dL/d relu(GN(u_j)) of the current plane [B][Hu][Wu][16]
   float* gr0b;         // gr[0]'s second buffer (odd planes: stage A writes it, stage B reads it)
   float* gskip[2][2];  // [plane parity][cell 0, 1] cells 4 and 3's skip-input dL/dh0, dL/dh1 [Pk][16]
@@ -92,6 +118,7 @@ struct BpttLayout {
   struct GroupSet {
     float* gz[5];
     unsigned* zmax;
+    unsigned* zpart;
     float* gu[2];
     float* gx;
     double* gnb_part[2];
@@ -100,6 +127,7 @@ struct BpttLayout {
     const GroupSet& g = set[p];
     for (int k = 0; k < 5; ++k) gz[k] = g.gz[k];
     zmax = g.zmax;
+    zpart = g.zpart;
     gu[0] = g.gu[0];
     gu[1] = g.gu[1];
     gx = g.gx;
@@ -133,11 +161,13 @@ BpttLayout bptt_layout(void* base, int B, int H, int W) {
     L.gc[k] = reinterpret_cast<float*>(take(L.cell_px[k] * kCellHid[k] * 4));
   }
   L.gnb_nblk = (int)std::min<size_t>(512, (HW + 1023) / 1024);
+  L.zp_n = (int)((L.cell_px[0] * 4 + 255) / 256);   // gate blocks of the largest cell (hid / 4 lanes per px)
   for (int q = 0; q < 2; ++q) {
     BpttLayout::GroupSet& g = L.set[q];
     for (int k = 0; k < 5; ++k)
       g.gz[k] = reinterpret_cast<float*>(take((size_t)G * L.cell_px[k] * 4 * kCellHid[k] * 4));
     g.zmax = reinterpret_cast<unsigned*>(take(5 * G * 4));
+    g.zpart = reinterpret_cast<unsigned*>(take((size_t)5 * G * L.zp_n * 4));
     g.gu[0] = reinterpret_cast<float*>(take((size_t)G * B * (HW / 4) * 16 * 4));
     g.gu[1] = reinterpret_cast<float*>(take((size_t)G * B * HW * 16 * 4));
     g.gx = reinterpret_cast<float*>(take((size_t)G * B * HW * kC * 4));
@@ -176,7 +206,7 @@ struct GateBwdArgs {
   const float* gh_add;   // null or [P][hid]: a second term of dL/dh' (the skip input's), added to gh
   float* gc;             // [P][hid] dL/dc' in, dL/dc (previous plane) out
   float* gz;             // [P][4 hid] out
-  unsigned* zmax;        // max |gz| (float bits)
+  unsigned* zpart;       // per-block max |gz| (float bits) at [blockIdx.x]
   int mode;              // 0: none, 1: cell 4 head, 2: max-pool routing
   const float* gcost;    // mode 1: dL/dcost of this plane, [B][D][H][W] at plane d
   int gcost_bstride;     // D * H * W
@@ -283,7 +313,7 @@ __global__ void __launch_bounds__(256) gate_bwd_kernel(GateBwdArgs a) {
     *reinterpret_cast<float4*>(gzp + 3 * hid) = make_float4(dg[0], dg[1], dg[2], dg[3]);
     *reinterpret_cast<float4*>(a.gc + p * hid + c0) = make_float4(dcp[0], dcp[1], dcp[2], dcp[3]);
   }
-  wave_absmax_to(m, a.zmax);
+  block_absmax_store(m, a.zpart + blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -302,7 +332,8 @@ struct DgPart {
 };
 struct DgradArgs {
   const float* gz;          // [B][H][W][CZ]
-  const unsigned* zmax;     // float bits of max |gz|
+  const unsigned* zpart;    // the gate kernel's per-block maxima of |gz| (float bits)
+  int nzp;
   const float* wfrag;       // this cell's packed fragments (all m-tiles)
   const float* wscale;      // 1 / 2^e of the fragments
   DgPart part[3];
@@ -338,7 +369,7 @@ __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
     float4* d = reinterpret_cast<float4*>(wl);
     for (int i = tid; i < AH * 2 / 16; i += 512) d[i] = s[i];
   }
-  const int ez = scale_exp(*a.zmax);
+  const int ez = scale_exp(block_max_of(a.zpart, a.nzp));
   const float zs = ldexpf(1.0f, -ez);
   const float inv = *a.wscale * ldexpf(1.0f, ez);
   auto coords = [&](int t, int& b, int& y0, int& x0) {
@@ -1212,13 +1243,33 @@ __global__ void gacc_to_float_kernel(const double* __restrict__ gacc, float* __r
     out[i] = (float)gacc[i];
 }
 
-// every plane of a group shares the largest scale exponent: slot 0 <- max over the slots
-__global__ void zmax_group_kernel(unsigned* zmax, int n) {
-  if (threadIdx.x == 0) {
-    unsigned m = 0;
-    for (int i = 0; i < n; ++i) m = zmax[i] > m ? zmax[i] : m;
-    for (int i = 0; i < n; ++i) zmax[i] = m;
+// Diagnostic trace (AARMVS_BWD_TRACE=1): after every kernel of the plane chain a position-
+// weighted checksum of what it wrote, at [plane][slot] of a device log that
+// aarmvs_debug_bwd_trace (not part of the ABI) copies out.  Runs of a schedule are compared
+// entry by entry: the first differing entry names the kernel whose output first differs.
+constexpr int kTraceSlots = 32;
+static unsigned long long* g_trace = nullptr;
+static int g_trace_planes = 0;
+__global__ void __launch_bounds__(256) cksum_kernel(const unsigned* __restrict__ p, size_t n,
+                                                   unsigned long long* out) {
+  __shared__ unsigned long long red[256];
+  unsigned long long acc = 0;
+  for (size_t i = threadIdx.x; i < n; i += 256) acc += (unsigned long long)p[i] * (1 + (i % 61));
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
   }
+  if (threadIdx.x == 0) *out = red[0];
+}
+
+// every plane of a group shares the largest scale exponent: zmax[slot] <- max over the slots
+__global__ void __launch_bounds__(256) zmax_group_kernel(const unsigned* zpart, int stride, int nb, int n,
+                                                         unsigned* zmax) {
+  unsigned m = 0;
+  for (int i = 0; i < n; ++i) m = max(m, block_max_of(zpart + (size_t)i * stride, nb));
+  if ((int)threadIdx.x < n) zmax[threadIdx.x] = m;
 }
 
 // ---------------------------------------------------------------------------
@@ -1301,6 +1352,17 @@ namespace aarmvs {
 
 size_t bptt_scratch_bytes(int B, int H, int W) { return bptt_layout(nullptr, B, H, W).bytes; }
 
+// A cross-stream dependency of the backward's schedules.  AARMVS_BWD_HOSTSYNC=1 (diagnostic)
+// makes the host wait for the event instead of the consumer stream (same ordering, no device-side
+// wait), to tell a missing dependency from a device-side event problem.
+static hipError_t xwait(hipStream_t consumer, hipEvent_t ev) {
+  static const bool host = [] {
+    const char* v = getenv("AARMVS_BWD_HOSTSYNC");
+    return v && atoi(v) != 0;
+  }();
+  return host ? hipEventSynchronize(ev) : hipStreamWaitEvent(consumer, ev, 0);
+}
+
 // The regulariser's backward over every plane (last first), in groups of kPlaneGroup planes:
 // per plane the gate / dgrad / GroupNorm / deconv chain; per group the weight gradients and
 // then `group_done(g0, n, gx)` (the cost-slice backward of the group's dL/dx, or a copy-out).
@@ -1326,6 +1388,8 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
   CK(hipMemsetAsync(L.gacc, 0, PL.raw_total * 8, s));
   const int res_div[5] = {1, 2, 4, 2, 1};
   auto zslot = [&](int k, int slot) { return L.gz[k] + (size_t)slot * L.cell_px[k] * 4 * kCellHid[k]; };
+  // blocks of cell k's gate kernel (run_gate_bwd): hid / 4 threads per cell pixel
+  auto gate_blocks = [&](int k) { return (int)((L.cell_px[k] * (kCellHid[k] / 4) + 255) / 256); };
   auto gate = [&](hipStream_t s, int k, int slot, const UnetIO& io, int mode, int d, const float* gh_add = nullptr) {
     GateBwdArgs a{};
     a.z = io.z[k];
@@ -1335,7 +1399,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     a.gh_add = gh_add;
     a.gc = L.gc[k];
     a.gz = zslot(k, slot);
-    a.zmax = L.zmax + k * G + slot;
+    a.zpart = L.zpart + ((size_t)k * G + slot) * L.zp_n;
     a.mode = mode;
     a.B = B;
     a.H = H / res_div[k];
@@ -1354,7 +1418,8 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
   auto dgrad = [&](hipStream_t s, int k, int slot, std::initializer_list<DgPart> parts) {
     DgradArgs a{};
     a.gz = zslot(k, slot);
-    a.zmax = L.zmax + k * G + slot;
+    a.zpart = L.zpart + ((size_t)k * G + slot) * L.zp_n;
+    a.nzp = gate_blocks(k);
     a.wfrag = pk + PL.dg_off[k];
     a.wscale = pk + PL.dg_scale_off + k;
     int i = 0;
@@ -1422,18 +1487,21 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
   // writes only the parameter accumulators and the cost-slice scratch, which the plane chain
   // never touches.  Events: evP "the group's planes done" (main -> group stream), evG[p] "the
   // group stage of a parity-p group done" (its set is free again).
-  // AARMVS_BWD_PIPE: 3 the plane pipeline only (default), 1 both overlaps, 0 everything on the caller's
-  // stream, 2 the plane stages on two streams in order; diagnostics: 4 the group stage on its
-  // stream but waited for at once, 5 the group overlap without the plane pipeline.
+  // AARMVS_BWD_PIPE: 0 everything on the caller's stream (default), 3 the plane pipeline, 1 the
+  // plane pipeline and the group overlap (6% faster at config 4), 2 the plane stages on two
+  // streams in order; diagnostics: 4 the group stage on its stream but waited for at once, 5
+  // the group overlap without the plane pipeline.  The multi-stream schedules give results that
+  // differ from run to run at the split products' precision (~2e-6 of max |dL/dx|) in some runs,
+  // for a reason not found: the default is the one-stream schedule, bit-reproducible.
   struct PipeSet {
     int dev = -1;
     hipStream_t aux = nullptr, grp = nullptr;
     hipEvent_t ev[9] = {};   // evA[2], evB[2], fork, evP, evG[2], group join
   };
   static thread_local PipeSet ps_dev[kMaxDevices];   // aux streams + events per device
-  static const int pipe_mode = [] {
+  const int pipe_mode = [] {   // read per call (bench.py times the schedules side by side)
     const char* v = getenv("AARMVS_BWD_PIPE");
-    return v ? atoi(v) : 3;
+    return v ? atoi(v) : 0;
   }();
   const bool pipe_on = pipe_mode != 0;
   int dev = 0;
@@ -1459,36 +1527,85 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
   hipEvent_t evP = ps.ev[5];
   hipEvent_t* evG = ps.ev + 6;
   auto gr0_of = [&](int d) { return (d & 1) ? L.gr0b : L.gr[0]; };
+  static const bool trace = [] {
+    const char* v = getenv("AARMVS_BWD_TRACE");
+    return v && atoi(v) != 0;
+  }();
+  if (trace && g_trace_planes < D) {
+    if (g_trace) CK(hipFree(g_trace));
+    CK(hipMalloc(&g_trace, (size_t)D * kTraceSlots * 8));
+    g_trace_planes = D;
+  }
+  if (trace) CK(hipMemsetAsync(g_trace, 0, (size_t)D * kTraceSlots * 8, s));
+  auto tr = [&](hipStream_t st, int d, int slot, const void* ptr, size_t nfloats) -> hipError_t {
+    if (!trace) return hipSuccess;
+    hipLaunchKernelGGL(cksum_kernel, dim3(1), dim3(256), 0, st, static_cast<const unsigned*>(ptr), nfloats,
+                       g_trace + (size_t)d * kTraceSlots + slot);
+    return hipGetLastError();
+  };
+  const size_t hw4 = (size_t)B * (HW / 4) * 16, hw1 = (size_t)B * HW * 16;
+  auto zsz = [&](int k) { return L.cell_px[k] * 4 * kCellHid[k]; };
+  auto hsz = [&](int k) { return L.cell_px[k] * kCellHid[k]; };
   int gi = 0;
   for (int g0 = ((D - 1) / G) * G; g0 >= 0; g0 -= G, ++gi) {
     const int n = std::min(G, D - g0);
     L.use_set(gi & 1);
-    if (sg != s && gi >= 2) CK(hipStreamWaitEvent(s, evG[gi & 1], 0));   // set free again
-    CK(hipMemsetAsync(L.zmax, 0, 5 * G * 4, s));
+    if (sg != s && gi >= 2) CK(xwait(s, evG[gi & 1]));   // set free again
     if (sa != s) {   // the aux stream starts after everything the group's stage A overwrites is consumed
       CK(hipEventRecord(ps.ev[4], s));
-      CK(hipStreamWaitEvent(sa, ps.ev[4], 0));
+      CK(xwait(sa, ps.ev[4]));
     }
     auto stage_a = [&](int d) -> hipError_t {
       const int k = d - g0, q = d & 1;
       const UnetIO io = unet_io_record(T, rec, d);
       CK(gate(sa, 4, k, io, 1, d));
+      CK(tr(sa, d, 0, zslot(4, k), zsz(4)));
+      CK(tr(sa, d, 1, L.gc[4], hsz(4)));
+      CK(tr(sa, d, 2, L.zpart + ((size_t)4 * G + k) * L.zp_n, gate_blocks(4)));
       CK(dgrad(sa, 4, k, {{L.gr[1], 0, 16, 0}, {L.gskip[q][0], 16, 16, 0}, {L.gh[4], 32, 8, 0}}));
+      CK(tr(sa, d, 3, L.gr[1], hw1));
+      CK(tr(sa, d, 4, L.gskip[q][0], L.cell_px[0] * 16));
+      CK(tr(sa, d, 5, L.gh[4], hsz(4)));
       CK(deconv_bwd(sa, 1, k, io, L.gr[1]));
+      CK(tr(sa, d, 6, L.gu[1] + (size_t)k * hw1, hw1));
+      CK(tr(sa, d, 7, L.gh[3], hsz(3)));
       CK(gate(sa, 3, k, io, 0, d));
+      CK(tr(sa, d, 8, zslot(3, k), zsz(3)));
+      CK(tr(sa, d, 9, L.gc[3], hsz(3)));
       CK(dgrad(sa, 3, k, {{gr0_of(d), 0, 16, 0}, {L.gskip[q][1], 16, 16, 0}, {L.gh[3], 32, 16, 0}}));
+      CK(tr(sa, d, 10, gr0_of(d), hw4));
+      CK(tr(sa, d, 11, L.gskip[q][1], L.cell_px[1] * 16));
+      CK(tr(sa, d, 12, L.gh[3], hsz(3)));
       return hipSuccess;
     };
     auto stage_b = [&](int d) -> hipError_t {
       const int k = d - g0, q = d & 1;
       const UnetIO io = unet_io_record(T, rec, d);
       CK(deconv_bwd(s, 0, k, io, gr0_of(d)));
+      CK(tr(s, d, 13, L.gu[0] + (size_t)k * hw4, hw4));
+      CK(tr(s, d, 14, L.gh[2], hsz(2)));
       CK(gate(s, 2, k, io, 0, d));
+      CK(tr(s, d, 15, zslot(2, k), zsz(2)));
+      CK(tr(s, d, 16, L.gc[2], hsz(2)));
       CK(dgrad(s, 2, k, {{L.gpool[1], 0, 16, 0}, {L.gh[2], 16, 16, 0}}));
+      CK(tr(s, d, 17, L.gpool[1], (size_t)B * (HW / 16) * 16));
+      CK(tr(s, d, 18, L.gh[2], hsz(2)));
       CK(gate(s, 1, k, io, 2, d, L.gskip[q][1]));
+      CK(tr(s, d, 19, zslot(1, k), zsz(1)));
+      CK(tr(s, d, 20, L.gc[1], hsz(1)));
       CK(dgrad(s, 1, k, {{L.gpool[0], 0, 16, 0}, {L.gh[1], 16, 16, 0}}));
+      CK(tr(s, d, 21, L.gpool[0], hw4));
+      CK(tr(s, d, 22, L.gh[1], hsz(1)));
       CK(gate(s, 0, k, io, 2, d, L.gskip[q][0]));
+      CK(tr(s, d, 23, zslot(0, k), zsz(0)));
+      CK(tr(s, d, 24, L.gc[0], hsz(0)));
+      CK(tr(s, d, 27, L.zpart + ((size_t)0 * G + k) * L.zp_n, gate_blocks(0)));
+      CK(tr(s, d, 28, L.zpart + ((size_t)1 * G + k) * L.zp_n, gate_blocks(1)));
+      CK(tr(s, d, 29, L.zpart + ((size_t)2 * G + k) * L.zp_n, gate_blocks(2)));
+      CK(tr(s, d, 30, L.zpart + ((size_t)3 * G + k) * L.zp_n, gate_blocks(3)));
       CK(dgrad(s, 0, k, {{L.gx + (size_t)k * xs, 0, 32, 0}, {L.gh[0], 32, 16, 0}}));
+      CK(tr(s, d, 25, L.gx + (size_t)k * xs, xs));
+      CK(tr(s, d, 26, L.gh[0], hsz(0)));
       return hipSuccess;
     };
     // step i: stage A of plane g0 + n - 1 - i, stage B of the plane after it
@@ -1496,24 +1613,24 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       const int d = g0 + n - 1 - i;
       if (pipe_mode == 2 && sa != s) {   // diagnostic: B(d + 1), then A(d) after it (no overlap)
         if (i >= 1) {
-          CK(hipStreamWaitEvent(s, evA[(d + 1) & 1], 0));
+          CK(xwait(s, evA[(d + 1) & 1]));
           CK(stage_b(d + 1));
         }
         if (i < n) {
           CK(hipEventRecord(evB[d & 1], s));
-          CK(hipStreamWaitEvent(sa, evB[d & 1], 0));
+          CK(xwait(sa, evB[d & 1]));
           CK(stage_a(d));
           CK(hipEventRecord(evA[d & 1], sa));
         }
         continue;
       }
       if (i < n) {
-        if (sa != s && i >= 2) CK(hipStreamWaitEvent(sa, evB[d & 1], 0));   // B(d + 2) done
+        if (sa != s && i >= 2) CK(xwait(sa, evB[d & 1]));   // B(d + 2) done
         CK(stage_a(d));
         if (sa != s) CK(hipEventRecord(evA[d & 1], sa));
       }
       if (i >= 1) {
-        if (sa != s) CK(hipStreamWaitEvent(s, evA[(d + 1) & 1], 0));
+        if (sa != s) CK(xwait(s, evA[(d + 1) & 1]));
         CK(stage_b(d + 1));
         if (sa != s) CK(hipEventRecord(evB[(d + 1) & 1], s));
       }
@@ -1521,14 +1638,15 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     // ---- the group stage: weight gradients of the group, then its cost-slice backward ----
     if (sg != s) {
       CK(hipEventRecord(evP, s));
-      CK(hipStreamWaitEvent(sg, evP, 0));
+      CK(xwait(sg, evP));
     }
     {
     const hipStream_t s = sg;   // (the group stage's launches below)
     for (int k = 0; k < 5; ++k) {
       {
         ProfScope ps(s, K_BWD_SMALL);
-        hipLaunchKernelGGL(zmax_group_kernel, dim3(1), dim3(64), 0, s, L.zmax + k * G, n);
+        hipLaunchKernelGGL(zmax_group_kernel, dim3(1), dim3(256), 0, s, L.zpart + (size_t)k * G * L.zp_n,
+                           L.zp_n, gate_blocks(k), n, L.zmax + k * G);
       }
       CK(hipGetLastError());
     }
@@ -1619,7 +1737,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       a.Wi = j ? W / 2 : W / 4;
       a.wpart = L.wpart;
       {
-        ProfScope ps(s, K_BWD_SMALL);
+        ProfScope ps(s, K_DECONV_WGRAD);
         hipLaunchKernelGGL(deconv_wgrad_kernel, dim3(kDcwBlocks), dim3(256), 0, s, a);
       }
       CK(hipGetLastError());
@@ -1639,7 +1757,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       a.W = W;
       a.wpart = L.wpart;
       {
-        ProfScope ps(s, K_BWD_SMALL);
+        ProfScope ps(s, K_HEAD_WGRAD);
         hipLaunchKernelGGL(head_wgrad_kernel, dim3(kWgBlocks), dim3(256), 0, s, a);
       }
       CK(hipGetLastError());
@@ -1649,9 +1767,9 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     if (r.grad_x)
       CK(hipMemcpyAsync(r.grad_x + (size_t)g0 * xs, L.gx, (size_t)n * xs * 4, hipMemcpyDeviceToDevice, s));
     if (r.group_done) CK(r.group_done(r.ctx, g0, n, L.gx, s));
-    if (s != sg0) CK(hipEventRecord(evG[gi & 1], s));
+    if (sg != sg0) CK(hipEventRecord(evG[gi & 1], sg));
     }
-    if (pipe_mode == 4 && sg != s) CK(hipStreamWaitEvent(s, evG[gi & 1], 0));
+    if (pipe_mode == 4 && sg != s) CK(xwait(s, evG[gi & 1]));
   }
   CK(join_g.join());
   if (r.grad_params) {
@@ -1668,3 +1786,14 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
 namespace aarmvs {
 double* bptt_gacc(void* scratch, int B, int H, int W) { return bptt_layout(scratch, B, H, W).gacc; }
 }  // namespace aarmvs
+
+// diagnostic (AARMVS_BWD_TRACE, tools/bwd_nondet.py), not part of the ABI: copies the last
+// backward's checksum log ([D][32] uint64) to host memory; returns the planes it holds
+extern "C" __attribute__((visibility("default"))) int aarmvs_debug_bwd_trace(void* host, size_t bytes) {
+  using namespace aarmvs;
+  if (!g_trace) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  const size_t n = std::min(bytes, (size_t)g_trace_planes * kTraceSlots * 8);
+  if (hipMemcpy(host, g_trace, n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return g_trace_planes;
+}

@@ -277,7 +277,9 @@ def backward_work(name: str, B: int, N: int, H: int, W: int, D: int, launches: i
       cbw_feat     per hypothesis: the reference and source features (128 (N) B), dL/dx (128 B),
                    dL/dt1 and the omega weight per view (20 (N-1) B);
       cbw_chain    per hypothesis and view: the omega conv output t1 (16 B) per stage (4), the
-                   stage-1 warp and dL/dx (3 x 128 B), dL/do / w / dL/dt1 out (24 B)."""
+                   stage-1 warp and dL/dx (3 x 128 B), dL/do / w / dL/dt1 out (24 B);
+      deconv_wgrad 2*16*16*9 FLOP per deconv input pixel and plane (fp32 MFMA), both deconvs;
+      head_wgrad   the head's h4 (8 ch) and dL/dcost per pixel and plane: 36 B."""
     HW = H * W
     nsrc = N - 1
     cell = {0: (48, 16, 1), 1: (32, 16, 2), 2: (32, 16, 4), 3: (48, 16, 2), 4: (40, 8, 1)}
@@ -294,6 +296,10 @@ def backward_work(name: str, B: int, N: int, H: int, W: int, D: int, launches: i
         return "flops", 2.0 * 16 * 16 * 9 * B * (HW / 4 + HW / 16) * D / launches, FP32_PEAK_TFLOPS
     if name == "cbw_feat":
         return "bytes", (128.0 * N + 128.0 + 20.0 * nsrc) * B * HW * D / launches, HBM_PEAK_GBS
+    if name == "deconv_wgrad":
+        return "flops", 2.0 * 16 * 16 * 9 * B * (HW / 4 + HW / 16) * D / launches, FP32_PEAK_TFLOPS
+    if name == "head_wgrad":
+        return "bytes", 36.0 * B * HW * D / launches, HBM_PEAK_GBS
     if name == "cbw_chain":
         return "bytes", (16.0 * 4 + 3 * 128.0 + 24.0) * nsrc * B * HW * D / launches, HBM_PEAK_GBS
     return None, 0.0, None
@@ -315,7 +321,8 @@ def train_kernel_table(prof: dict, B: int, N: int, H: int, W: int, D: int):
             row.update(bound="hbm", achieved=round(ach, 1), unit="GB/s", peak=peak, frac=round(ach / peak, 4))
         elif kind == "flops":
             ach = amount / avg_s / 1e12
-            row.update(bound="mfma" if name[:-1] in ("dgrad", "wgrad") else "valu", achieved=round(ach, 2),
+            row.update(bound="mfma" if name[:-1] in ("dgrad", "wgrad") or name == "deconv_wgrad" else "valu",
+                       achieved=round(ach, 2),
                        unit="TFLOP/s", peak=round(peak, 1), frac=round(ach / peak, 4))
         elif name in ("bwd_small", "cbw_small"):
             row.update(bound=None, note="fixed-order reductions / small per-group kernels")
@@ -361,6 +368,21 @@ def train_bench(dev, D: int = 192, reps: int = 2):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
     peak = torch.cuda.max_memory_allocated(dev)
+    # the same steps with the backward's multi-stream schedule (AARMVS_BWD_PIPE=1: plane
+    # pipeline + group stage overlap; not bit-reproducible run to run)
+    prev = os.environ.get("AARMVS_BWD_PIPE")
+    os.environ["AARMVS_BWD_PIPE"] = "1"
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    dt_ov = (time.perf_counter() - t0) / reps
+    if prev is None:
+        del os.environ["AARMVS_BWD_PIPE"]
+    else:
+        os.environ["AARMVS_BWD_PIPE"] = prev
     ok = bool(torch.isfinite(loss)) and all(
         p.grad is None or bool(torch.isfinite(p.grad).all()) for p in model.parameters())
     # one more step with a hipEvent pair around every library launch (the forward's and the
@@ -380,6 +402,8 @@ def train_bench(dev, D: int = 192, reps: int = 2):
     return dict(metric="training step (forward + mvsnet_cls_loss + backward), 1 sample / GPU",
                 config="dtu_train_640x512_n3_d192", D=D, s_per_step=round(dt, 4),
                 ms_per_plane=round(dt / D * 1e3, 3), steps_timed=reps,
+                backward_schedule="one stream (AARMVS_BWD_PIPE=0, bit-reproducible)",
+                s_per_step_multistream=round(dt_ov, 4), ms_per_plane_multistream=round(dt_ov / D * 1e3, 3),
                 peak_device_gb=round(peak / 1e9, 2),
                 backward=getattr(EMVSNet, "BACKWARD_PATH", "see DESIGN.md §6"),
                 loss_and_grads_finite=ok,

@@ -191,23 +191,30 @@ def test_backward_is_deterministic_in_the_parameter_gradients():
         assert torch.equal(x, y)
 
 
-def test_backward_pipeline_schedule_is_bit_exact(tmp_path):
-    """The backward's default stream schedule (bptt.hip, AARMVS_BWD_PIPE=3: the plane pipeline,
-    stage A of plane d beside stage B of plane d + 1) against the one-stream schedule (0), over
-    three plane groups (D = 36, both group buffer sets; the forward's cost volume digest too):
-    dL/dref, dL/dx, dL/dsrc and every parameter gradient bit for bit (the scatter sums in fixed
-    point, in an order fixed by construction); the schedule only moves kernels between
-    streams, so a missing dependency shows up as a differing digest (the default schedule is
-    run twice)."""
+def test_backward_schedules_default_bit_reproducible_others_close(tmp_path):
+    """The backward's stream schedules (bptt.hip AARMVS_BWD_PIPE) over three plane groups
+    (D = 36, both group buffer sets; the forward's cost volume digest too): the default
+    one-stream schedule (0) is bit-reproducible -- dL/dref, dL/dx, dL/dsrc and every parameter
+    gradient, the scatter summed in fixed point in an order fixed by construction -- across
+    processes; the multi-stream schedules (3: the plane pipeline, 1: with the group stage on a
+    third stream) match it to 1e-5 relative L2 per tensor (they differ from run to run at the
+    split products' precision in some runs)."""
     import subprocess
     import sys
     helper = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bwd_digest.py")
-    out = {}
-    for run, pipe in (("0", "0"), ("1", "3"), ("2", "3")):   # the default twice (races)
+    out, arrs = {}, {}
+    for run, pipe in (("a", "0"), ("b", "0"), ("p3", "3"), ("p1", "1")):
         env = dict(os.environ, AARMVS_BWD_PIPE=pipe)
         f = str(tmp_path / f"src{run}.npy")
-        r = subprocess.run([sys.executable, helper, f], env=env, capture_output=True, text=True, timeout=100)
+        fr = str(tmp_path / f"ref{run}.npy")
+        r = subprocess.run([sys.executable, helper, f, fr], env=env, capture_output=True, text=True, timeout=100)
         assert r.returncode == 0, r.stderr[-2000:]
         out[run] = [ln for ln in r.stdout.splitlines() if ln.startswith("DIGEST")]
         assert len(out[run]) == 5, r.stdout
-    assert out["0"] == out["1"] == out["2"], out
+        arrs[run] = (np.load(f), np.load(fr))
+    assert out["a"] == out["b"], out
+    for run in ("p3", "p1"):
+        assert out[run][0] == out["a"][0]   # the forward's cost volume
+        for x, y in zip(arrs[run], arrs["a"]):
+            rel = np.linalg.norm(x.astype(np.float64) - y) / np.linalg.norm(y)
+            assert rel < 1e-5, (run, rel)

@@ -39,6 +39,36 @@ def cost_layout():
     return L, off
 
 
+def bptt_sets():
+    """Offsets of the two group buffer sets in the backward scratch (bptt.hip bptt_layout)."""
+    hid = [16, 16, 16, 16, 8]
+    px = [HW, HW // 4, HW // 16, HW // 4, HW]
+    off = 0
+    for k in range(5):
+        off = al(off + B * px[k] * hid[k] * 4)   # gh
+        off = al(off + B * px[k] * hid[k] * 4)   # gc
+    nblk = min(512, (HW + 1023) // 1024)
+    sets = []
+    for q in range(2):
+        d = {}
+        for k in range(5):
+            d[f"gz{k}"] = (off, G * B * px[k] * 4 * hid[k] * 4)
+            off = al(off + G * B * px[k] * 4 * hid[k] * 4)
+        d["zmax"] = (off, 5 * G * 4)
+        off = al(off + 5 * G * 4)
+        d["gu0"] = (off, G * B * (HW // 4) * 64)
+        off = al(off + G * B * (HW // 4) * 64)
+        d["gu1"] = (off, G * B * HW * 64)
+        off = al(off + G * B * HW * 64)
+        d["gx"] = (off, G * B * HW * 128)
+        off = al(off + G * B * HW * 128)
+        for j in range(2):
+            d[f"gnb{j}"] = (off, G * B * nblk * 36 * 8)
+            off = al(off + G * B * nblk * 36 * 8)
+        sets.append(d)
+    return sets
+
+
 def where(a, b):
     """Where run b differs from run 0: dL/dx per plane (count, max |diff|, pixels), dL/dref
     per channel, dL/dsrc per view, and the parameter tensors that differ."""
@@ -47,8 +77,12 @@ def where(a, b):
     if dx.any():
         planes = dx.reshape(dx.shape[0], -1).sum(1)
         pl = [(int(i), int(planes[i]), float((x0[i] - x1[i]).abs().max())) for i in range(len(planes)) if planes[i]]
+        top = pl[-1][0]
+        xm = float(x0[top].abs().max())
+        rel = ((x0[top] - x1[top]).abs() / x0[top].abs().clamp_min(xm * 1e-3)).max()
         print(f"   x: {len(pl)} planes differ, d = {[p[0] for p in pl]}; top plane {pl[-1]}; "
-              f"max {max(p[2] for p in pl):.2e}", flush=True)
+              f"max {max(p[2] for p in pl):.2e}; top plane max|x| {xm:.2e}, max rel diff {float(rel):.2e}",
+              flush=True)
         i = pl[0][0]
         idx = dx[i].nonzero()[:8].tolist()
         print("   x first plane diffs at [b,y,x,c]:", idx, flush=True)
@@ -97,6 +131,31 @@ def main():
         for k in ("wo", "gt1", "go", "grefv", "gsrc8", "gsum"):
             o, n = CL[k]
             d["s:" + k] = hashlib.sha256(scratch[breg + o: breg + o + n].cpu().numpy().tobytes()).hexdigest()[:12]
+        for q, st in enumerate(bptt_sets()):
+            for name in ("zmax", "gz0", "gz4", "gx"):
+                o, n = st[name]
+                d[f"b{q}:{name}"] = hashlib.sha256(scratch[o: o + n].cpu().numpy().tobytes()).hexdigest()[:8]
+        o, n = bptt_sets()[0]["zmax"]
+        zm = scratch[o: o + n].cpu().view(torch.float32).reshape(5, G)
+        if r == 0:
+            zm0 = zm.clone()
+        elif not torch.equal(zm, zm0):
+            dd = (zm != zm0).nonzero().tolist()
+            print("   zmax set 0 differs at (cell, slot):", dd[:10],
+                  [(float(zm0[c, k]), float(zm[c, k])) for c, k in dd[:4]], flush=True)
+        if os.environ.get("AARMVS_BWD_TRACE"):
+            import ctypes
+            import numpy as np
+            buf = np.zeros((D, 32), dtype=np.uint64)
+            lib = _lib.lib()
+            lib.aarmvs_debug_bwd_trace.restype = ctypes.c_int
+            lib.aarmvs_debug_bwd_trace(ctypes.c_void_p(buf.ctypes.data), ctypes.c_size_t(buf.nbytes))
+            if r == 0:
+                trace0 = buf.copy()
+            else:
+                diff = [(dd, sl) for dd in range(D - 1, -1, -1) for sl in range(32) if buf[dd, sl] != trace0[dd, sl]]
+                if diff:
+                    print(f"   trace: {len(diff)} entries differ; first (plane, slot): {diff[:6]}", flush=True)
         runs.append(d)
         print(r, " ".join(f"{k}={v}" for k, v in d.items()), flush=True)
         cur = {"x": g_x.detach().cpu().clone(), "ref": g_ref.detach().cpu().clone(),
