@@ -58,7 +58,9 @@ __host__ __device__ constexpr int dg_mt_halves(int k) { return dg_chunks(k) * 9 
 struct ParamLayout {
   size_t raw_off[P_COUNT];
   size_t pk_off[P_COUNT];   // packed offsets (floats), 64-float aligned
-  size_t h3_off[5];         // split-fp16 cell weights (hi then lo halves), in floats
+  size_t h3_off[5];         // split-fp16 cell weights (hi then lo halves), in floats; taps with
+                            // (tap + chunk) odd negated (the training cells' sign balance)
+  size_t h3p_off[5];        // the same, every tap positive (the inference cells)
   size_t h3_scale_off;      // 5 floats: 1 / (power-of-two weight scale) per cell
   size_t ow0t_off;          // omega conv3x3 weights as [tap][ci][co] (1,152 floats)
   size_t owb_off;           // omega conv3x3 off-centre taps as split-fp16 MFMA B fragments [chunk][2][64 lanes][8]

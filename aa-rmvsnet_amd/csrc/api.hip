@@ -38,6 +38,10 @@ const ParamLayout& param_layout() {
       l.h3_off[k] = pk;
       pk += ((size_t)cell_a_halves(k) + 63) / 64 * 64;   // 2 x halves = halves floats
     }
+    for (int k = 0; k < 5; ++k) {
+      l.h3p_off[k] = pk;
+      pk += ((size_t)cell_a_halves(k) + 63) / 64 * 64;
+    }
     l.h3_scale_off = pk;
     pk += 64;
     l.ow0t_off = pk;
@@ -251,6 +255,8 @@ __global__ void __launch_bounds__(256) pack_cell_h3_kernel(const float* __restri
   const int halves = cell_a_halves(k);
   _Float16* hi = reinterpret_cast<_Float16*>(pk + L.h3_off[k]);
   _Float16* lo = hi + halves;
+  _Float16* hip = reinterpret_cast<_Float16*>(pk + L.h3p_off[k]);
+  _Float16* lop = hip + halves;
   for (int i = threadIdx.x; i < halves; i += blockDim.x) {
     const int j = i & 7, l = (i >> 3) & 63, rest = i >> 9;   // [chunk][tap][mt][lane][j]
     const int mt = rest % mt_n, tap = (rest / mt_n) % 9, c = rest / (mt_n * 9);
@@ -258,11 +264,13 @@ __global__ void __launch_bounds__(256) pack_cell_h3_kernel(const float* __restri
     const int co = (r >> 3) * hid + 8 * mt + (r & 7);
     const int ci = 16 * c + 8 * h + j;
     // taps with (tap + chunk) odd negated: the cells' sign-balanced accumulation (convlstm.hip)
-    const float sg = ((tap + c) & 1) ? -1.0f : 1.0f;
-    const float v = ci < cin ? w[(co * cin + ci) * 9 + tap] * sc * sg : 0.f;
-    const _Float16 vh = (_Float16)v;
-    hi[i] = vh;
-    lo[i] = (_Float16)(v - (float)vh);
+    const bool neg = ((tap + c) & 1) != 0;
+    const float v = ci < cin ? w[(co * cin + ci) * 9 + tap] * sc : 0.f;
+    const _Float16 vh = (_Float16)v, vl = (_Float16)(v - (float)vh);
+    hip[i] = vh;
+    lop[i] = vl;
+    hi[i] = neg ? -vh : vh;   // (fp16 negation is exact: the balanced copy is the same split)
+    lo[i] = neg ? -vl : vl;
   }
 }
 

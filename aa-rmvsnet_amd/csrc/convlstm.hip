@@ -321,7 +321,7 @@ struct H3PixStager {
 // Before the MFMAs of chunk CH: bring part 0's partial sums (cell 0's x, cells 3 and 4's
 // GroupNorm+ReLU part, staged x 2^-e) to the h parts' scale 2^kHScaleExp (CH is the first chunk
 // past part 0); the epilogue undoes 2^kHScaleExp with the weight scale.
-template <class C, int KIND, int CH>
+template <class C, int KIND, int CH, bool BAL>
 __device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], floatx16 (&accn)[C::MT][C::RW],
                                                float xr) {
   if constexpr ((KIND == 0 || C::D::MODE[0] == SRC_GNRELU) && CH > 0 && C::chunk_part(CH) != 0 &&
@@ -331,7 +331,7 @@ __device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], fl
 #pragma unroll
       for (int r = 0; r < C::RW; ++r) {
         acc[m][r] *= xr;
-        accn[m][r] *= xr;
+        if constexpr (BAL) accn[m][r] *= xr;
       }
   }
 }
@@ -346,8 +346,10 @@ __device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], fl
 // chain drifts downwards, a bias that long cancelling gradient sums amplify.
 // Taps with (tap + chunk) odd carry negated weights (pack_cell_h3_kernel) and accumulate into
 // accn; the result is acc - accn, whose two drifts cancel (tools/microbench/mfma_chain.cpp:
-// -0.164 -> +0.001 ulp over 108 MFMAs).
-template <class C, int CH, bool PIPE = false>
+// -0.164 -> +0.001 ulp over 108 MFMAs).  BAL: the training cells only (their record is what
+// the BPTT differentiates); the inference cells accumulate every tap into acc with the
+// positive fragments (pack_cell_h3_kernel's second copy): 32 fewer accumulator registers.
+template <class C, int CH, bool PIPE = false, bool BAL = true>
 __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], floatx16 (&accn)[C::MT][C::RW],
                                               const char* wl_hi, const char* wl_lo, const char* in_hi,
                                               const char* in_lo, int wave, int lane) {
@@ -379,7 +381,7 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], flo
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
-          floatx16& d = ((tap + CH) & 1) ? accn[m][r] : acc[m][r];
+          floatx16& d = (BAL && ((tap + CH) & 1)) ? accn[m][r] : acc[m][r];
           d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s][m], bh[s][r], d, 0, 0, 0);
           d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s][m], bl[s][r], d, 0, 0, 0);
           d = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s][m], bh[s][r], d, 0, 0, 0);
@@ -404,7 +406,7 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], flo
         const half8 al = *reinterpret_cast<const half8*>(wl_lo + aoff);
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
-          floatx16& d = ((tap + CH) & 1) ? accn[m][r] : acc[m][r];
+          floatx16& d = (BAL && ((tap + CH) & 1)) ? accn[m][r] : acc[m][r];
           d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[r], d, 0, 0, 0);
           d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[r], d, 0, 0, 0);
           d = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[r], d, 0, 0, 0);
@@ -571,8 +573,8 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
         st.template load<0>(a, nb, ny0, nx0, tid);
       }
       if (CH == 0) cell_c_load<C>(a, b, yw, x0 + col, hi, cst);
-      xguard_rescale<C, KIND, CH>(acc, accn, xr);
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0>(acc, accn, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
+      xguard_rescale<C, KIND, CH, PRECISE>(acc, accn, xr);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE>(acc, accn, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
     };
     chunk(std::integral_constant<int, 0>{});
     if constexpr (NCHK > 1) chunk(std::integral_constant<int, 1>{});
@@ -580,7 +582,8 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int r = 0; r < RW; ++r) acc[m][r] -= accn[m][r];
+      for (int r = 0; r < RW; ++r)
+        if constexpr (PRECISE) acc[m][r] -= accn[m][r];
     cell_epilogue<C, ABL, PRECISE>(a, acc, cst, inv_scale, b, yw, x0 + col, hi);
   }
 }
@@ -669,8 +672,8 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
       constexpr int AC = A_NEXT ? CH + 2 - NCHK : CH + 2;
       const char* cur = inb + 2 * par * PB;
       char* oth = inb + 2 * (par ^ 1) * PB;
-      xguard_rescale<C, KIND, CH>(acc, accn, xr);
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0>(acc, accn, wl_hi, wl_lo, cur, cur + PB, wave, lane);
+      xguard_rescale<C, KIND, CH, PRECISE>(acc, accn, xr);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE>(acc, accn, wl_hi, wl_lo, cur, cur + PB, wave, lane);
       if (!(ABL & 2)) {
         if (!F_NEXT || next < ntiles) st.template store<F>(oth, oth + PB, gn, tid, 0, W);
         if (!A_NEXT)
@@ -682,7 +685,8 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-          for (int r = 0; r < RW; ++r) acc[m][r] -= accn[m][r];
+          for (int r = 0; r < RW; ++r)
+            if constexpr (PRECISE) acc[m][r] -= accn[m][r];
         cell_epilogue<C, ABL, PRECISE>(a, acc, cst, inv_scale, b, yw, x, hi);
       }
       __syncthreads();   // buffer `oth` staged; buffer `cur` free for the step after next
@@ -1238,7 +1242,9 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a.c = io.c_new[k];
     a.c_in = io.c_prev[k];
     a.z_out = io.z[k];
-    a.wpk = params + L.h3_off[k];   // split-fp16 A fragments
+    // split-fp16 A fragments: sign-balanced (odd taps negated) for the training cells,
+    // positive for the inference cells
+    a.wpk = params + (io.z[k] ? L.h3_off[k] : L.h3p_off[k]);
     a.bias = params + L.pk_off[P_C0B + 2 * k];
     a.B = B;
     a.H = H / scale;

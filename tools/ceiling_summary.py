@@ -38,9 +38,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--out")
+    ap.add_argument("--kernels", default="omega_conv,cost_x,omega_stats1,omega_stats2,lstm_cell0,lstm_cell4")
     args = ap.parse_args()
-    P = {p: load(os.path.join(args.dir, p)) for p in ("sq_time", "sq_mix", "tex", "l2", "fetch", "write")}
-    kernels = ["omega_conv", "cost_x", "omega_stats1", "omega_stats2", "lstm_cell0", "lstm_cell4"]
+    passes = ["sq_time", "sq_mix", "tex", "l2", "fetch", "write"]
+    if os.path.isdir(os.path.join(args.dir, "f64")):
+        passes.append("f64")
+    P = {p: load(os.path.join(args.dir, p)) for p in passes}
+    kernels = args.kernels.split(",")
     res = {}
     for k in kernels:
         g = lambda p, c: P[p].get(k, {}).get(c)  # noqa: E731
@@ -74,6 +78,15 @@ def main():
             r["l2_req"] = req
             r["l2_hit_frac"] = g("l2", "TCC_HIT_sum") / req
             r["l2_to_hbm_rdreq"] = g("l2", "TCC_EA0_RDREQ_sum")
+        if "f64" in P and waves:
+            for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                      "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_TRANS_F32"):
+                v = g("f64", c)
+                if v is not None:
+                    r[c.lower().replace("sq_insts_valu_", "per_wave_")] = v / waves
+            av, gt = g("f64", "SQ_ACTIVE_INST_VALU"), g("f64", "GRBM_GUI_ACTIVE")
+            if av is not None and wc:
+                r["valu_issue_frac"] = av / wc
         f, w = g("fetch", "FETCH_SIZE"), g("write", "WRITE_SIZE")
         if f is not None and w is not None:
             r["hbm_bytes_per_launch"] = (2 * f + w) * 1024

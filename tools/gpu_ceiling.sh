@@ -22,3 +22,7 @@ run tex TA_BUSY_avr TA_TOTAL_WAVEFRONTS_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_T
 run l2 TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum TCC_EA0_RDREQ_sum
 run fetch FETCH_SIZE
 run write WRITE_SIZE
+# (CEIL_F64=1) VALU fp64 / transcendental instruction counts and VALU issue
+if [ "${CEIL_F64:-0}" = "1" ]; then
+  run f64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VALU SQ_WAVES GRBM_GUI_ACTIVE
+fi

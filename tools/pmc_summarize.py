@@ -16,7 +16,7 @@ from collections import defaultdict
 
 SHORT = [("cost_x_kernel", "cost_x"), ("omega_conv_kernel", "omega_conv"), ("omega_mfma_kernel", "omega_conv"),
          ("omega_stats_kernel<1>", "omega_stats1"),
-         ("omega_stats_kernel<2>", "omega_stats2"), ("deconv_mfma_kernel", "deconv"), ("deconv_px2_kernel", "deconv"), ("deconv_px_kernel", "deconv"), ("deconv_kernel", "deconv"), ("head_wta", "head_wta"), ("nchw_to_c8", "to_c8")]
+         ("omega_stats_kernel<2>", "omega_stats2"), ("deconv_mfma_kernel", "deconv"), ("deconv_px2_kernel", "deconv"), ("deconv_px_kernel", "deconv"), ("deconv_kernel", "deconv"), ("head_wta", "head_wta"), ("nchw_to_c8", "to_c8"), ("fusion_filter_kernel", "fusion")]
 
 
 CELL = re.compile(r"lstm_cell_h3(?:db)?_kernel<(\d),")
