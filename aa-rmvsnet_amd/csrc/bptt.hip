@@ -1195,7 +1195,10 @@ __global__ void __launch_bounds__(256) deconv_wgrad_kernel(DcwArgs a) {
 }
 
 // conv_0 (head) weight / bias gradient over a group: gW[ci][tap] = sum gcost[p] h4[p + off][ci],
-// gb = sum gcost.  Thread per pixel, 73 sums, block reduce, one partial per block.
+// gb = sum gcost.  Thread per pixel (32-bit index arithmetic: the caller checks the group's
+// pixel count), 73 sums, block reduce, one partial of kHwPart floats per block.
+constexpr int kHwBlocks = 1024, kHwPart = 80;
+static_assert((size_t)kHwBlocks * kHwPart <= (size_t)kWgBlocks * kWgPartMax, "head partials fit wpart");
 struct HwArgs {
   const float* gcost;   // [B][D][H][W]
   const float* h4;      // record: h4' of plane d0 (state slab d0 + 1) + k * hstride
@@ -1209,12 +1212,12 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(HwArgs a) {
   float s[73];
 #pragma unroll
   for (int i = 0; i < 73; ++i) s[i] = 0.f;
-  const size_t HW = (size_t)a.H * a.W;
-  const size_t n = (size_t)a.nplanes * a.B * HW;
-  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < n; t += (size_t)gridDim.x * 256) {
-    const size_t p = t % HW;
-    const int b = (int)((t / HW) % a.B), k = (int)(t / (HW * a.B));
-    const int x = (int)(p % a.W), y = (int)(p / a.W);
+  const uint32_t HW = (uint32_t)a.H * (uint32_t)a.W, W = (uint32_t)a.W;
+  const uint32_t n = (uint32_t)a.nplanes * (uint32_t)a.B * HW;
+  for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < n; t += gridDim.x * 256u) {
+    const uint32_t kb = t / HW, p = t - kb * HW;
+    const int b = (int)(kb % (uint32_t)a.B), k = (int)(kb / (uint32_t)a.B);
+    const int y = (int)(p / W), x = (int)(p - (uint32_t)y * W);
     const float g = a.gcost[((size_t)b * a.D + a.d0 + k) * HW + p];
     const float* hb = a.h4 + (size_t)k * a.hstride + (size_t)b * HW * 8;
 #pragma unroll
@@ -1232,7 +1235,7 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(HwArgs a) {
   }
   block_sum<73>(s, red);
   if (threadIdx.x == 0) {
-    float* wp = a.wpart + (size_t)blockIdx.x * kWgPartMax;
+    float* wp = a.wpart + (size_t)blockIdx.x * kHwPart;
 #pragma unroll
     for (int i = 0; i < 73; ++i) wp[i] = s[i];
   }
@@ -1758,10 +1761,11 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       a.wpart = L.wpart;
       {
         ProfScope ps(s, K_HEAD_WGRAD);
-        hipLaunchKernelGGL(head_wgrad_kernel, dim3(kWgBlocks), dim3(256), 0, s, a);
+        if ((size_t)n * B * H * W >= (1ull << 31)) return hipErrorInvalidValue;   // 32-bit indices
+        hipLaunchKernelGGL(head_wgrad_kernel, dim3(kHwBlocks), dim3(256), 0, s, a);
       }
       CK(hipGetLastError());
-      CK(reduce_partials(L.wpart, kWgBlocks, (int)kWgPartMax, 73, 0, 0, 73, 72, L.rseg,
+      CK(reduce_partials(L.wpart, kHwBlocks, kHwPart, 73, 0, 0, 73, 72, L.rseg,
                          L.gacc + PL.raw_off[P_HW], L.gacc + PL.raw_off[P_HB], s));
     }
     if (r.grad_x)
