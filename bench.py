@@ -334,6 +334,37 @@ def train_kernel_table(prof: dict, B: int, N: int, H: int, W: int, D: int):
     return rows
 
 
+def ceiling_limits():
+    """What binds the cost-slice kernels besides HBM, from the committed rocprofv3 counter passes
+    (tools/gpu_ceiling.sh -> tools/ceiling_summary.py, one 16-plane group at the headline): the
+    fraction of wave cycles issuing / dependency-stalled / parked for omega_conv (issue- and
+    latency-bound) and the texture-unit (TA, TD) busy fractions and L1 hit rate for cost_x
+    (bound by its gathers through the vector L1)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    for name in ("r04_ceiling_pmc.json", "r03_ceiling_pmc.json"):
+        path = os.path.join(here, "profiles", name)
+        if not os.path.exists(path):
+            continue
+        with open(path) as fh:
+            d = json.load(fh)
+        if not (d.get("omega_conv") or d.get("cost_x")):
+            continue
+        out = {"source": "profiles/" + name}
+        om, cx = d.get("omega_conv") or {}, d.get("cost_x") or {}
+        if om:
+            out["omega_conv"] = {k: om[k] for k in ("issue_frac", "dep_stall_frac", "parked_frac", "per_wave_valu")
+                                 if k in om}
+            out["omega_conv"]["bound"] = "issue/latency"
+        if cx:
+            l1 = 1.0 - cx["tcp_to_l2_read_req"] / cx["tcp_accesses"] if cx.get("tcp_accesses") else None
+            out["cost_x"] = {k: cx[k] for k in ("ta_busy_frac", "td_busy_frac", "issue_frac", "parked_frac")
+                             if k in cx}
+            out["cost_x"]["l1_hit_frac"] = round(l1, 4) if l1 is not None else None
+            out["cost_x"]["bound"] = "L1 gather (TD)"
+        return out
+    return None
+
+
 def train_bench(dev, D: int = 192, reps: int = 2):
     """Training-step time at config 4 as stated (BASELINE configs[3]: 640x512, N=3, D=192, one
     sample per GPU; train.py:288-307): the drop-in EMVSNet train forward (FeatNet + the HIP
@@ -566,6 +597,9 @@ def main():
             roofline["warp_aggregation"] = dict(kernels=group, achieved=round(ach, 1), unit="GB/s",
                                                 peak=HBM_PEAK_GBS, frac=round(ach / HBM_PEAK_GBS, 4),
                                                 us_per_plane=round(ms / planes * 1e3, 2))
+        lim = ceiling_limits()
+        if lim:
+            roofline["limits"] = lim
 
     cpu = None
     parity = None
