@@ -1147,16 +1147,28 @@ __global__ void __launch_bounds__(256) deconv_wgrad_kernel(DcwArgs a) {
     const int b = t % a.B, k = t / a.B;
     const int x0 = rx * 64;
     __syncthreads();
+    // staging: one float4 (4 channels of a pixel) per load
     const float* hp = a.h + (size_t)k * a.hstride + ((size_t)b * a.Hi + iy) * a.Wi * 16;
-    for (int e = tid; e < 64 * 16; e += 256) {
-      const int px = e >> 4, c = e & 15;
-      hs[px][c] = x0 + px < a.Wi ? hp[(size_t)(x0 + px) * 16 + c] : 0.f;
+    {
+      const int px = tid >> 2, c4 = (tid & 3) * 4;   // 64 px x 4 quads = 256 threads
+      const float4 v = x0 + px < a.Wi ? *reinterpret_cast<const float4*>(hp + (size_t)(x0 + px) * 16 + c4)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      hs[px][c4] = v.x;
+      hs[px][c4 + 1] = v.y;
+      hs[px][c4 + 2] = v.z;
+      hs[px][c4 + 3] = v.w;
     }
     const float* gp = a.gu + ((size_t)k * a.B + b) * Ho * Wo * 16;
-    for (int e = tid; e < 3 * 130 * 16; e += 256) {
-      const int c = e & 15, cc = (e >> 4) % 130, rr = (e >> 4) / 130;
+    for (int e = tid; e < 3 * 130 * 4; e += 256) {
+      const int c4 = (e & 3) * 4, pc = e >> 2, rr = pc / 130, cc = pc - rr * 130;
       const int oy = 2 * iy - 1 + rr, ox = 2 * x0 - 1 + cc;
-      gs[rr][cc][c] = (oy >= 0 && oy < Ho && ox >= 0 && ox < Wo) ? gp[((size_t)oy * Wo + ox) * 16 + c] : 0.f;
+      const float4 v = (oy >= 0 && oy < Ho && ox >= 0 && ox < Wo)
+                           ? *reinterpret_cast<const float4*>(gp + ((size_t)oy * Wo + ox) * 16 + c4)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      gs[rr][cc][c4] = v.x;
+      gs[rr][cc][c4 + 1] = v.y;
+      gs[rr][cc][c4 + 2] = v.z;
+      gs[rr][cc][c4 + 3] = v.w;
     }
     __syncthreads();
 #pragma unroll

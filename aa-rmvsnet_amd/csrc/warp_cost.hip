@@ -1575,11 +1575,16 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
   __shared__ int bad;
   const PipeArgs& pa = a.p;
   const int tid = threadIdx.x, b = blockIdx.z;
-  const int v = blockIdx.y >> 2, c = blockIdx.y & 3;
+  // one block per (tile, view, chunk), chunk fastest, XCD-aware (xcd_tile): the 4 nsrc blocks
+  // of a tile, which read the same dL/dx (and per view the same dL/dt1 halo) lines, and the
+  // neighbouring tiles, which share source taps, run together on one XCD's L2
+  const int seq = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = seq / (4 * pa.nsrc), vc = seq - tile * (4 * pa.nsrc);
+  const int v = vc >> 2, c = vc & 3;
   const int fxk = *a.fxk;
   const int H = pa.H, W = pa.W, HW = H * W, nsrc = pa.nsrc;
   const int tiles_x = (W + kFbT - 1) / kFbT;
-  const int tx0 = (blockIdx.x % tiles_x) * kFbT, ty0 = (blockIdx.x / tiles_x) * kFbT;
+  const int tx0 = (tile % tiles_x) * kFbT, ty0 = (tile / tiles_x) * kFbT;
   const int lx = tid & 15, ly = tid >> 4;
   const int x = tx0 + lx, y = ty0 + ly;
   const bool in = x < W && y < H;
@@ -1850,7 +1855,8 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
         if (own[j][ch] != 0.f) atomicAdd(gp + ch, to_fixed(own[j][ch], fxk));
     }
   }
-  const size_t blk = (((size_t)c * nsrc + v) * pa.B + b) * gridDim.x + blockIdx.x;
+  const int ntiles = tiles_x * ((H + kFbT - 1) / kFbT);
+  const size_t blk = (((size_t)c * nsrc + v) * pa.B + b) * ntiles + tile;
   float* wp = a.wpart + blk * 288;
   for (int i = tid; i < 288; i += 256) {   // i = (co * 8 + j) * 9 + tap
     const int tap = i % 9, j = (i / 9) % 8, co = i / 72;
@@ -2101,7 +2107,7 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   fa.n = n;
   {
     ProfScope ps(s, K_CBW_FEAT);
-    hipLaunchKernelGGL(cbw_feat_kernel, dim3(L.ntiles16, 4 * a->nsrc, a->B), dim3(256), 0, s, fa,
+    hipLaunchKernelGGL(cbw_feat_kernel, dim3(L.ntiles16 * 4 * a->nsrc, 1, a->B), dim3(256), 0, s, fa,
                        ba.p.params, ba.p.rel);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -16,7 +16,12 @@ from collections import defaultdict
 
 SHORT = [("cost_x_kernel", "cost_x"), ("omega_conv_kernel", "omega_conv"), ("omega_mfma_kernel", "omega_conv"),
          ("omega_stats_kernel<1>", "omega_stats1"),
-         ("omega_stats_kernel<2>", "omega_stats2"), ("deconv_mfma_kernel", "deconv"), ("deconv_px2_kernel", "deconv"), ("deconv_px_kernel", "deconv"), ("deconv_kernel", "deconv"), ("head_wta", "head_wta"), ("nchw_to_c8", "to_c8"), ("fusion_filter_kernel", "fusion")]
+         ("omega_stats_kernel<2>", "omega_stats2"), ("deconv_mfma_kernel", "deconv"), ("deconv_px2_kernel", "deconv"), ("deconv_px_kernel", "deconv"), ("deconv_kernel", "deconv"), ("head_wta", "head_wta"), ("nchw_to_c8", "to_c8"), ("fusion_filter_kernel", "fusion"),
+         ("cbw_feat_kernel", "cbw_feat"), ("dgrad_kernel<64>", "dgrad64"), ("dgrad_kernel<32>", "dgrad32"),
+         ("wgrad2_kernel<64, 3>", "wgrad64x3"), ("wgrad2_kernel<64, 2>", "wgrad64x2"),
+         ("wgrad2_kernel<32, 3>", "wgrad32x3"), ("gate_bwd_kernel", "gate_bwd"), ("cbw_chain_kernel", "cbw_chain"),
+         ("deconv_wgrad_kernel", "deconv_wgrad"), ("head_wgrad_kernel", "head_wgrad"),
+         ("deconv_bwd_kernel", "deconv_bwd")]
 
 
 CELL = re.compile(r"lstm_cell_h3(?:db)?_kernel<(\d),")
