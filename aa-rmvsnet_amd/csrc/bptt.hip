@@ -378,8 +378,10 @@ __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
     y0 = (rem / tiles_x) * kDgTH;
     x0 = (rem % tiles_x) * kDgTW;
   };
-  float4 pv[NI][2];   // the prefetched chunk: item j = (half hh, haloed pixel p) of e = tid + 512 j
-  auto load = [&](int t, int c) {
+  // two prefetched chunks in flight (register buffers by chunk parity): chunk i + 2's loads are
+  // issued when chunk i is staged, so a chunk's global latency spans two chunks' MFMAs
+  float4 pv[2][NI][2];   // [buffer][item j = (half hh, haloed pixel p) of e = tid + 512 j]
+  auto load = [&](int t, int c, int buf) {
     int b, y0, x0;
     coords(t, b, y0, x0);
     const float* gzb = a.gz + (size_t)b * a.H * a.W * CZ;
@@ -389,22 +391,22 @@ __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
       const int hh = e >= kDgNPIX ? 1 : 0, p = e - hh * kDgNPIX;
       const int row = p / kDgW2, cc = p - row * kDgW2;
       const int gy = y0 - 1 + row, gx = x0 - 1 + cc;
-      pv[j][0] = pv[j][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      pv[buf][j][0] = pv[buf][j][1] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (e < 2 * kDgNPIX && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
         const float4* s = reinterpret_cast<const float4*>(gzb + ((size_t)gy * a.W + gx) * CZ + 16 * c + 8 * hh);
-        pv[j][0] = s[0];
-        pv[j][1] = s[1];
+        pv[buf][j][0] = s[0];
+        pv[buf][j][1] = s[1];
       }
     }
   };
-  auto store = [&]() {
+  auto store = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int e = tid + 512 * j;
       if (e >= 2 * kDgNPIX) continue;
       const int hh = e >= kDgNPIX ? 1 : 0, p = e - hh * kDgNPIX;
-      const float v[8] = {pv[j][0].x, pv[j][0].y, pv[j][0].z, pv[j][0].w,
-                          pv[j][1].x, pv[j][1].y, pv[j][1].z, pv[j][1].w};
+      const float4 q0 = pv[buf][j][0], q1 = pv[buf][j][1];
+      const float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
       bhalf8 hv, lv;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -418,7 +420,8 @@ __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
     }
   };
   const int col = lane & 31, h = lane >> 5;
-  load(tile, 0);
+  load(tile, 0, 0);
+  load(tile, 1, 1);   // (NCHK >= 2)
   for (; tile < ntiles; tile += gridDim.x) {
     int b, y0, x0;
     coords(tile, b, y0, x0);
@@ -432,12 +435,12 @@ __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
     auto chunk = [&](int c, auto PAR) {
       constexpr int CP = decltype(PAR)::value;   // c & 1
       __syncthreads();   // previous chunk's fragment reads done (fragments visible the first time)
-      store();
+      store(CP);
       __syncthreads();
-      if (c + 1 < NCHK)
-        load(tile, c + 1);
+      if (c + 2 < NCHK)
+        load(tile, c + 2, CP);
       else if (next < ntiles)
-        load(next, 0);
+        load(next, c + 2 - NCHK, CP);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int p = (wave + tap / 3) * kDgW2 + col + tap % 3;
