@@ -131,6 +131,16 @@ constexpr int kMaxParts = 3;
 // (TH rows of NT x 32 pixels; one wave per row).
 template <int KIND>
 struct CellDef;
+// (A/B builds only: the staging variant of cells 3 and 4; the library uses the defaults)
+#ifndef AARMVS_C3DB
+#define AARMVS_C3DB 0
+#endif
+#ifndef AARMVS_C4DB
+#define AARMVS_C4DB 0
+#endif
+#ifndef AARMVS_C4PIPE
+#define AARMVS_C4PIPE 0
+#endif
 template <>
 struct CellDef<0> {   // [x, h0] @ H
   static constexpr int NP = 2, CH[kMaxParts] = {32, 16, 0};
@@ -154,7 +164,7 @@ struct CellDef<3> {   // [gnrelu(u0), h1', h3] @ H/2
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 16};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16;
-  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 0, H3PIPE = 1;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = AARMVS_C3DB, H3PIPE = 1;
   static constexpr int MIN_WAVES = 1;
 };
 template <>
@@ -162,7 +172,7 @@ struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 8};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 8;
-  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 0, H3PIPE = 0;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = AARMVS_C4DB, H3PIPE = AARMVS_C4PIPE;
   // <= 128 VGPRs: two 512-thread blocks per CU (the sign-balanced accumulator pair took the
   // compiler's choice to 130, one block per CU: 160 -> 202 us per plane at the headline)
   static constexpr int MIN_WAVES = 4;
