@@ -601,7 +601,8 @@ struct DcbArgs {
 };
 
 __global__ void __launch_bounds__(256) deconv_bwd_kernel(DcbArgs a) {
-  __shared__ float4 wsh[9 * 16 * 4];   // [tap][co][ci / 4]
+  __shared__ float4 wsh[9 * 16 * 4];   // [tap][co & 3][co >> 2][ci / 4]: the 4 lanes of a quad (co >> 2)
+                                       // read 4 distinct float4s in distinct banks
   __shared__ float coef[4][16];        // y = u a + b; xhat = (u - mean) rstd
   __shared__ float gco[2][2];          // per group: S1 / n, S2 / n
   __shared__ double gred[4][256];
@@ -625,7 +626,8 @@ __global__ void __launch_bounds__(256) deconv_bwd_kernel(DcbArgs a) {
   const int Ho = 2 * a.Hi, Wo = 2 * a.Wi;
   for (int i = tid; i < 9 * 16 * 16; i += 256) {
     const int ci = i & 15, co = (i >> 4) & 15, tap = i >> 8;
-    reinterpret_cast<float*>(wsh)[(tap * 16 + co) * 16 + ci] = a.w[(ci * 16 + co) * 9 + tap];
+    reinterpret_cast<float*>(wsh)[((((tap * 4 + (co & 3)) * 4 + (co >> 2)) * 4) + (ci >> 2)) * 4 + (ci & 3)] =
+        a.w[(ci * 16 + co) * 9 + tap];
   }
   if (tid < 16) {
     const int c = tid, g = c >> 3;
@@ -678,7 +680,7 @@ __global__ void __launch_bounds__(256) deconv_bwd_kernel(DcbArgs a) {
       const float g = gu[i];
 #pragma unroll
       for (int c4 = 0; c4 < 4; ++c4) {
-        const float4 wv = wsh[(tap * 16 + 4 * q + i) * 4 + c4];
+        const float4 wv = wsh[((tap * 4 + i) * 4 + q) * 4 + c4];
         acc[4 * c4 + 0] = fmaf(g, wv.x, acc[4 * c4 + 0]);
         acc[4 * c4 + 1] = fmaf(g, wv.y, acc[4 * c4 + 1]);
         acc[4 * c4 + 2] = fmaf(g, wv.z, acc[4 * c4 + 2]);
