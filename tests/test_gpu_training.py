@@ -179,6 +179,22 @@ def test_ddp_world2_gradients_equal_hand_averaged():
         assert "DDP_OK" in out, out[-3000:]
 
 
+def test_ddp_rccl_one_rank_gradients_equal_local():
+    """The RCCL (`nccl` backend) process group with DDP over the HIP training path: one rank
+    (RCCL refuses two ranks on one GPU), DDP's gradient all-reduce over RCCL leaves the
+    gradients bit-identical to a plain backward of the same sample."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), DDP_BACKEND="nccl")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ddp_worker.py")], env=env,
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "DDP_OK" in r.stdout, r.stdout[-3000:]
+
+
 def _train_args(tmp_path, numdepth, extra=()):
     from aarmvs import train_ddp
     mini = os.path.join(ROOT, "tests", "golden", "dtu_mini")
