@@ -171,4 +171,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if os.environ.get("NONDET_STREAM") == "1":   # the library called on a created (non-null) stream
+        with torch.cuda.stream(torch.cuda.Stream()):
+            main()
+    else:
+        main()
