@@ -196,8 +196,7 @@ def fusion_bench(H: int, W: int, nsrc: int, dev, cpu_leg: bool, reps: int = 10):
     depth + confidence + one depth read per source view + three masks + the float64
     average), and the CPU oracle on a 2-source-view sample of the same maps."""
     from aarmvs import fusion
-    from oracle import fusion_oracle as fo
-    depths, cams, conf = fo.synthetic_views(H, W, nsrc, seed=7)
+    depths, cams, conf = syn.fusion_views(H, W, nsrc, seed=7)
     t = [torch.from_numpy(d).to(dev) for d in depths]
     c = torch.from_numpy(conf).to(dev)
     run = lambda: fusion.filter_depth_core(t[0], c, cams[0], t[1:], cams[1:], 0.35)  # noqa: E731
@@ -218,6 +217,7 @@ def fusion_bench(H: int, W: int, nsrc: int, dev, cpu_leg: bool, reps: int = 10):
                peak_gbs=HBM_PEAK_GBS, frac=round(ach / HBM_PEAK_GBS, 4),
                geo_mask_mean=round(float(out[1].float().mean()), 4))
     if cpu_leg:
+        from oracle import fusion_oracle as fo
         k = 2
         t0 = time.perf_counter()
         fo.filter_depth_core(depths[0], conf, cams[0], depths[1:1 + k], cams[1:1 + k], 0.35)

@@ -134,45 +134,6 @@ def filter_depth_core(ref_depth, confidence, ref_cam, src_depths, src_cams, phot
     return photo_mask, geo_mask, final_mask, depth_est_averaged
 
 
-def synthetic_views(H, W, nsrc, seed=0):
-    """Seeded depth maps + DTU-like cameras of one scene (a tilted plane with bumps, seen
-    from nsrc + 1 cameras on an arc), for parity tests and the fusion bench."""
-    rng = np.random.default_rng(seed)
-    f = np.float32(1.2 * W)
-    K = np.array([[f, 0, W / 2], [0, f, H / 2], [0, 0, 1]], np.float32)
-    cams = []
-    for v in range(nsrc + 1):
-        th = 0.03 * (v - nsrc / 2)
-        R = np.array([[np.cos(th), 0, np.sin(th)], [0, 1, 0], [-np.sin(th), 0, np.cos(th)]])
-        t = np.array([-30.0 * (v - nsrc / 2), 2.0 * v, 0.0])
-        E = np.eye(4)
-        E[:3, :3] = R
-        E[:3, 3] = t
-        cams.append((K.copy(), E.astype(np.float32)))
-    # world surface: z = 600 + 0.05 x + bumps, sampled per camera by ray casting on a grid
-    ys, xs = np.mgrid[0:H, 0:W].astype(np.float64)
-    depths = []
-    for K_, E_ in cams:
-        Ki = np.linalg.inv(K_.astype(np.float64))
-        rays = Ki @ np.stack([xs.ravel(), ys.ravel(), np.ones(H * W)])
-        # camera -> world: X_w = R^T (X_c - t); surface z_w = 600 + 0.05 x_w
-        R = E_[:3, :3].astype(np.float64)
-        t = E_[:3, 3].astype(np.float64)
-        o = -R.T @ t
-        dvec = R.T @ rays
-        lam = (600.0 + 0.05 * o[0] - o[2]) / (dvec[2] - 0.05 * dvec[0])
-        pw = o[:, None] + dvec * lam
-        bump = 4.0 * np.sin(pw[0] / 37.0) * np.cos(pw[1] / 23.0)
-        depth = (lam * (1.0 + bump / 600.0)).reshape(H, W)
-        noise = rng.normal(0, 0.3, (H, W))
-        hole = rng.random((H, W)) < 0.02
-        d = (depth + noise).astype(np.float32)
-        d[hole] = 0.0
-        depths.append(d)
-    conf = rng.random((H, W)).astype(np.float32)
-    return depths, cams, conf
-
-
 def filter_depth_scan(pair_data, images, cam_texts, depth_ests, confidences, photo_threshold):
     """fusion.py:135-273 on in-memory inputs: pair_data [(ref, [src...])], images {view: float32
     [H,W,3] in [0,1]}, cam_texts {view: cam.txt text}, depth_ests / confidences {view: float32

@@ -168,7 +168,7 @@ for k in ["gz4", "gr1", "gu1", "gz3", "gr0", "gu0", "gz2", "gpool1", "gz1", "gpo
         e = g - ref
         print(f"  {k:7s} {tag:5s} L2 {np.linalg.norm(e) / nr:.3e}  bias {float((e * ref).sum()) / nr ** 2:+.3e}")
 
-# projection of the last plane's dL/dx error on K = dx/dtheta (tools/diag_gx_corr.py)
+# projection of the last plane's dL/dx error on K = dx/dtheta (tests/diag_gx_corr.py)
 rels = [orc.relative_projection(proj[:, v], proj[:, 0]) for v in range(1, N)]
 P64 = {k: v.double() for k, v in P.items()}
 fd = feats.double()

@@ -2,8 +2,8 @@
 dx_d/dtheta> is linear in dL/dx, so an error e_d in dL/dx changes it by sum_d <e_d, K_d> with
 K_d = dx_d/dtheta (forward-mode AD of the oracle's cost slice in float64).  Splits that change
 by plane, channel, batch element and pixel position for the HIP dL/dx (gpurun_out/<dump>.npz
-from tools/diag_gx_dump.py) and for float32 CPU autograd, both against float64.
-usage: python tools/diag_gx_corr.py gpurun_out/gx_dump_r04c.npz [param]"""
+from tests/diag_gx_dump.py) and for float32 CPU autograd, both against float64.
+usage: python tests/diag_gx_corr.py gpurun_out/gx_dump_r04c.npz [param]"""
 import os
 import sys
 

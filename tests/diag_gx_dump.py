@@ -1,6 +1,6 @@
 """GPU half of the dL/dx error bisection: runs test_gpu_bptt's backward at one shape and saves
 the HIP dL/dx per plane ([D,B,32,H,W]) and the recorded cost volume, dL/dcost and the record's cost slices and states, for the CPU-side analysis
-in tools/diag_gx_corr.py (which needs no GPU)."""
+in tests/diag_gx_corr.py (which needs no GPU)."""
 import os
 import sys
 

@@ -1,12 +1,12 @@
 """CPU-side split of the HIP dL/dx error (no GPU) into what the backward's arithmetic adds and
-what the forward's recorded values add: from tools/diag_gx_dump.py's dump (the GPU's record:
+what the forward's recorded values add: from tests/diag_gx_dump.py's dump (the GPU's record:
 cost slices and every plane's regulariser state, its dL/dcost and its dL/dx), the float64 BPTT
 is run plane by plane AT THE GPU'S RECORDED STATES (local autograd of one oracle unet_step per
 plane, gradients chained backward) -> gx_hyb.  Then
    e_bwd = gx_gpu - gx_hyb    (the HIP backward's arithmetic)
    e_fwd = gx_hyb - gx64      (the HIP forward's values, float64 backward)
-are projected on K_d = dx_d/dtheta (tools/diag_gx_corr.py) for an omega parameter theta.
-usage: python tools/diag_gx_hybrid.py gpurun_out/<dump>.npz [param]"""
+are projected on K_d = dx_d/dtheta (tests/diag_gx_corr.py) for an omega parameter theta.
+usage: python tests/diag_gx_hybrid.py gpurun_out/<dump>.npz [param]"""
 import os
 import sys
 

@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "aa-rmvsnet_amd"))
 
 from oracle import fusion_oracle as fo  # noqa: E402
-from aarmvs import fusion  # noqa: E402
+from aarmvs import fusion, synthetic as syn  # noqa: E402
 
 
 def test_remap_known_answers():
@@ -38,7 +38,7 @@ def test_remap_known_answers():
 
 
 def test_filter_core_on_a_consistent_scene():
-    depths, cams, conf = fo.synthetic_views(48, 64, 4, seed=3)
+    depths, cams, conf = syn.fusion_views(48, 64, 4, seed=3)
     photo, geo, final, avg = fo.filter_depth_core(depths[0], conf, cams[0], depths[1:], cams[1:], 0.35)
     assert photo.dtype == bool and geo.dtype == bool and avg.dtype == np.float64
     np.testing.assert_array_equal(final, photo & geo)
@@ -75,7 +75,7 @@ def test_pfm_cam_pair_roundtrip(tmp_path):
 
 
 def test_camera_pack_layout():
-    _, cams, _ = fo.synthetic_views(8, 8, 3)
+    _, cams, _ = syn.fusion_views(8, 8, 3)
     p = fusion.pack_cameras(cams[0], cams[1:])
     assert p.dtype == np.float32 and p.size == 18 + 42 * 3
     np.testing.assert_array_equal(p[:9], np.linalg.inv(cams[0][0]).ravel())
@@ -109,7 +109,7 @@ def test_numpy_matmul_is_an_fma_chain():
                                            (300, 400, 10, 3)])
 def test_gpu_filter_matches_oracle(H, W, nsrc, seed):
     import torch
-    depths, cams, conf = fo.synthetic_views(H, W, nsrc, seed=seed)
+    depths, cams, conf = syn.fusion_views(H, W, nsrc, seed=seed)
     photo, geo, final, avg = fo.filter_depth_core(depths[0], conf, cams[0], depths[1:], cams[1:], 0.35)
     dev = torch.device("cuda")
     t = [torch.from_numpy(d).to(dev) for d in depths]
@@ -128,7 +128,7 @@ def test_gpu_filter_matches_oracle(H, W, nsrc, seed):
 def test_gpu_filter_rejects_bad_input():
     import torch
     from aarmvs._lib import AarmvsError
-    depths, cams, conf = fo.synthetic_views(16, 16, 2)
+    depths, cams, conf = syn.fusion_views(16, 16, 2)
     with pytest.raises(AarmvsError):
         fusion.filter_depth_core(torch.from_numpy(depths[0]), torch.from_numpy(conf), cams[0],
                                  [torch.from_numpy(d) for d in depths[1:]], cams[1:], 0.35)
@@ -152,7 +152,7 @@ def _write_scan(root, H, W, nsrc, pad):
     """A scan folder in the DTU layout: pair.txt, cams/, images/ (pad extra rows top and
     bottom: the driver's crop), depth_est_0/ and confidence_0/ PFMs."""
     from PIL import Image
-    depths, cams, conf = fo.synthetic_views(H, W, nsrc, seed=11)
+    depths, cams, conf = syn.fusion_views(H, W, nsrc, seed=11)
     n = nsrc + 1
     scan, out = root / "scan1", root / "out"
     for d in ("cams", "images"):
