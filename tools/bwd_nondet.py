@@ -56,6 +56,9 @@ def bptt_sets():
             off = al(off + G * B * px[k] * 4 * hid[k] * 4)
         d["zmax"] = (off, 5 * G * 4)
         off = al(off + 5 * G * 4)
+        zp_n = (B * px[0] * 4 + 255) // 256   # bptt.hip: the largest gate grid
+        d["zpart"] = (off, 5 * G * zp_n * 4)
+        off = al(off + 5 * G * zp_n * 4)
         d["gu0"] = (off, G * B * (HW // 4) * 64)
         off = al(off + G * B * (HW // 4) * 64)
         d["gu1"] = (off, G * B * HW * 64)
