@@ -97,8 +97,9 @@ SIGNATURES = {
     "aarmvs_pack_params": (c_int, [c_void_p, c_void_p, c_void_p]),
     "aarmvs_homo_warp": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                  c_void_p, c_void_p]),
+    "aarmvs_homo_warp_backward_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "aarmvs_homo_warp_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                                          c_void_p, c_void_p]),
+                                          c_void_p, c_void_p, c_void_p]),
     "aarmvs_sweep_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "aarmvs_sweep": (c_int, [ctypes.POINTER(SweepArgs), c_void_p]),
     "aarmvs_train_record_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),

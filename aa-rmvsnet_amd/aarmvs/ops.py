@@ -110,15 +110,21 @@ def homo_warp(src_fea: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor) -> 
 @_on_tensor_device
 def homo_warp_backward(grad_out: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor,
                        src_shape) -> torch.Tensor:
-    """d loss / d src_fea of homo_warp: bilinear scatter-add of grad_out (fp32 atomics)."""
+    """d loss / d src_fea of homo_warp: bilinear scatter-add of grad_out, summed in 64-bit fixed
+    point (bit-reproducible, aarmvs_homo_warp_backward)."""
     _require_device(grad_out)
     g = grad_out.contiguous()
     B, C, H, W = src_shape
     rel_d = rel.reshape(B, 12).to(g.device, torch.float32).contiguous()
     dep = depth.reshape(B).to(g.device, torch.float32).contiguous()
     grad_src = torch.zeros(B, C, H, W, device=g.device)
+    n = lib().aarmvs_homo_warp_backward_workspace_bytes(B, C, H, W)
+    if n == 0:
+        raise AarmvsError(f"aarmvs: homo_warp_backward geometry B={B} C={C} H={H} W={W} (B <= 64)")
+    ws = torch.empty(n, dtype=torch.uint8, device=g.device)
     check(lib().aarmvs_homo_warp_backward(g.data_ptr(), rel_d.data_ptr(), dep.data_ptr(), B, C, H,
-                                          W, grad_src.data_ptr(), _stream()), "homo_warp_backward")
+                                          W, grad_src.data_ptr(), ws.data_ptr(), _stream()),
+          "homo_warp_backward")
     return grad_src
 
 
@@ -251,11 +257,17 @@ class _EvidentialEpilogue(torch.autograd.Function):
         if B != 1 or C != 4 or any(tuple(h.shape) != (1, 4, D, H, W) for h in heads):
             raise ValueError(f"evidential epilogue: heads must be [1, 4, D, H, W], got "
                              f"{[tuple(h.shape) for h in heads]}")
+        dev = heads[0].device
+        if any(h.device != dev for h in heads):
+            raise AarmvsError("aarmvs: evidential epilogue heads must be on one device")
+        if not dv.is_cuda or dv.device != dev:
+            raise AarmvsError(f"aarmvs: evidential epilogue depth values must be on {dev} "
+                              f"(got {dv.device}); the kernel reads them in place")
         dvc = dv.reshape(-1).float().contiguous()
         if dvc.numel() != D:
             raise ValueError(f"evidential epilogue: {dvc.numel()} depth values for D = {D}")
-        ev = torch.empty(4, H, W, device=heads[0].device)
-        pc = torch.empty(1, D, H, W, device=heads[0].device)
+        ev = torch.empty(4, H, W, device=dev, dtype=torch.float32)
+        pc = torch.empty(1, D, H, W, device=dev, dtype=torch.float32)
         check(lib().aarmvs_evidential_epilogue(_ptr3(heads), dvc.data_ptr(), D, H * W, ev.data_ptr(),
                                                pc.data_ptr(), _stream()), "evidential_epilogue")
         ctx.save_for_backward(dvc, *heads)
@@ -268,6 +280,11 @@ class _EvidentialEpilogue(torch.autograd.Function):
         D, H, W = heads[0].shape[2:]
         g_ev = g_ev.contiguous() if g_ev is not None else None
         g_pc = g_pc.contiguous() if g_pc is not None else None
+        for gt in (g_ev, g_pc):
+            if gt is not None:
+                _require_device(gt)
+                if gt.device != heads[0].device:
+                    raise AarmvsError("aarmvs: evidential epilogue gradients on another device")
         gh = [torch.empty_like(h) for h in heads]
         check(lib().aarmvs_evidential_epilogue_backward(_ptr3(heads), dvc.data_ptr(), D, H * W,
                                                         _ptr(g_ev), _ptr(g_pc), _ptr3(gh), _stream()),

@@ -129,8 +129,9 @@ struct SweepGeom {
 hipError_t launch_pack_params(const float* raw, float* packed, hipStream_t s);
 hipError_t launch_homo_warp(const float* src, const float* rel, const float* depth, int B, int C,
                             int H, int W, float* out, hipStream_t s);
-hipError_t launch_homo_warp_bwd(const float* gout, const float* rel, const float* depth, int B,
-                                int C, int H, int W, float* gsrc, hipStream_t s);
+size_t homo_warp_bwd_workspace_bytes(int B, int C, int H, int W);
+hipError_t launch_homo_warp_bwd(const float* gout, const float* rel, const float* depth, int B, int C, int H,
+                                int W, float* gsrc, void* workspace, hipStream_t s);
 
 struct CostArgs {
   const float* ref;

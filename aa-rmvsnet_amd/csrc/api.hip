@@ -495,13 +495,19 @@ int aarmvs_homo_warp(const float* src_fea, const float* rel_proj, const float* d
   return e == hipSuccess ? AARMVS_OK : hip_fail(e, "homo_warp");
 }
 
+size_t aarmvs_homo_warp_backward_workspace_bytes(int B, int C, int H, int W) {
+  if (B < 1 || B > 64 || C < 1 || H < 2 || W < 2) return 0;
+  return homo_warp_bwd_workspace_bytes(B, C, H, W);
+}
+
 int aarmvs_homo_warp_backward(const float* grad_out, const float* rel_proj, const float* depth,
-                              int B, int C, int H, int W, float* grad_src, hipStream_t stream) {
-  if (!grad_out || !rel_proj || !depth || !grad_src)
+                              int B, int C, int H, int W, float* grad_src, void* workspace,
+                              hipStream_t stream) {
+  if (!grad_out || !rel_proj || !depth || !grad_src || !workspace)
     return fail(AARMVS_ERR_INVALID, "homo_warp_backward: null pointer");
-  if (B < 1 || C < 1 || H < 2 || W < 2)
-    return fail(AARMVS_ERR_INVALID, "homo_warp_backward: need B>=1, C>=1, H>=2, W>=2");
-  hipError_t e = launch_homo_warp_bwd(grad_out, rel_proj, depth, B, C, H, W, grad_src, stream);
+  if (B < 1 || B > 64 || C < 1 || H < 2 || W < 2)
+    return fail(AARMVS_ERR_INVALID, "homo_warp_backward: need 1<=B<=64, C>=1, H>=2, W>=2");
+  hipError_t e = launch_homo_warp_bwd(grad_out, rel_proj, depth, B, C, H, W, grad_src, workspace, stream);
   return e == hipSuccess ? AARMVS_OK : hip_fail(e, "homo_warp_backward");
 }
 

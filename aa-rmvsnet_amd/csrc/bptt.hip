@@ -1507,12 +1507,13 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
   // writes only the parameter accumulators and the cost-slice scratch, which the plane chain
   // never touches.  Events: evP "the group's planes done" (main -> group stream), evG[p] "the
   // group stage of a parity-p group done" (its set is free again).
-  // AARMVS_BWD_PIPE: 0 everything on the caller's stream (default), 3 the plane pipeline, 1 the
-  // plane pipeline and the group overlap (6% faster at config 4), 2 the plane stages on two
-  // streams in order; diagnostics: 4 the group stage on its stream but waited for at once, 5
-  // the group overlap without the plane pipeline.  The multi-stream schedules give results that
-  // differ from run to run at the split products' precision (~2e-6 of max |dL/dx|) in some runs,
-  // for a reason not found: the default is the one-stream schedule, bit-reproducible.
+  // AARMVS_BWD_PIPE: 1 the plane pipeline and the group overlap (default), 0 everything on the
+  // caller's stream, 3 the plane pipeline alone, 2 the plane stages on two streams in order;
+  // diagnostics: 4 the group stage on its stream but waited for at once, 5 the group overlap
+  // without the plane pipeline.  Every schedule gives bit-identical gradients (every reduction
+  // has a fixed order; tests/test_gpu_bptt.py::test_backward_schedules_are_bit_identical).  Until
+  // round 5 the multi-stream ones did not: packed-fp32 device code (since disabled in the
+  // Makefile) gave results that depended on what ran beside it.
   struct PipeSet {
     int dev = -1;
     hipStream_t aux = nullptr, grp = nullptr;
@@ -1521,7 +1522,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
   static thread_local PipeSet ps_dev[kMaxDevices];   // aux streams + events per device
   const int pipe_mode = [] {   // read per call (bench.py times the schedules side by side)
     const char* v = getenv("AARMVS_BWD_PIPE");
-    return v ? atoi(v) : 0;
+    return v ? atoi(v) : 1;
   }();
   const bool pipe_on = pipe_mode != 0;
   int dev = 0;

@@ -57,11 +57,13 @@ __device__ __forceinline__ float fast_tanh(float x) {
 }
 __device__ __forceinline__ float exp_u(float x) {
   const float e = __builtin_amdgcn_exp2f(x * 1.44269502f);
-  return fmaf(e, x * 1.3349758e-8f, e);   // x (log2e - fp32(log2e)) ln 2
+  const float c = fmaf(e, x * 1.3349758e-8f, e);   // x (log2e - fp32(log2e)) ln 2
+  // no correction at e = 0, inf or NaN (x = -inf would give fmaf(0, -inf, 0) = NaN)
+  return (e > 0.0f && e < INFINITY) ? c : e;
 }
-__device__ __forceinline__ float rcp_nr(float d) {   // 1 / d for d >= 1 (d = inf -> 0)
+__device__ __forceinline__ float rcp_nr(float d) {   // 1 / d for d >= 1 (d = inf -> 0, NaN -> NaN)
   const float r = __builtin_amdgcn_rcpf(d);
-  return d < INFINITY ? fmaf(fmaf(-d, r, 1.0f), r, r) : 0.0f;
+  return d < INFINITY ? fmaf(fmaf(-d, r, 1.0f), r, r) : (d != d ? d : 0.0f);
 }
 __device__ __forceinline__ float precise_sigmoid(float x) { return rcp_nr(1.0f + exp_u(-x)); }
 __device__ __forceinline__ float precise_tanh(float x) {

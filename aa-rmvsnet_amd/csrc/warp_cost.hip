@@ -111,40 +111,102 @@ hipError_t launch_homo_warp(const float* src, const float* rel, const float* dep
 }
 
 // ---------------------------------------------------------------------------
-// Backward of the warp w.r.t. the source features (aarmvs_homo_warp_backward):
-// grid_sample's bilinear backward as a scatter-add of the output gradient into the
-// four taps (no-return fp32 atomics; out-of-range taps receive nothing).
+// Backward of the warp w.r.t. the source features (aarmvs_homo_warp_backward, the gradient of
+// grid_sample at module.py:36): a scatter-add of the output gradient into the four bilinear
+// taps, many reference pixels into one source pixel.  fp32 atomics would make each sum depend on
+// the order the atomics are served in, so the sums are formed in 64-bit fixed point instead
+// (integer adds are associative: bit-reproducible), as the sweep's own dL/dsrc (cbw_feat):
+//   1. warp_bwd_max: max |grad_out| per batch element (float bits, order-independent max);
+//   2. warp_bwd_scatter: each contribution wt * g scaled by 2^k_b (exact) and rounded to an
+//      integer, k_b such that any source pixel's total (<= HW max|g|: the bilinear weights of
+//      one reference pixel sum to <= 1) stays below 2^61; quantum 2^-k_b ~ HW max|g| 2^-62;
+//   3. warp_bwd_fold: grad_src += (float)(sum 2^-k_b), one rounding.
+// Workspace: [B] exponents' source words + [B][C][HW] int64 accumulators (zeroed here).
 // ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) warp_bwd_max_kernel(const float* __restrict__ gout, size_t n_per_b,
+                                                           unsigned* __restrict__ gmax) {
+  const int b = blockIdx.y;
+  const float* g = gout + (size_t)b * n_per_b;
+  float m = 0.f;
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n_per_b; i += (size_t)gridDim.x * 256) {
+    const float v = fabsf(g[i]);
+    m = (v > m || v != v) ? (v != v ? INFINITY : v) : m;
+  }
+  const int w = wave_reduce_i32(__float_as_int(m), 0, [](int x, int y) { return x > y ? x : y; });
+  if ((threadIdx.x & 63) == 0 && (unsigned)w > __hip_atomic_load(gmax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(gmax + b, (unsigned)w);
+}
+
+__device__ __forceinline__ int warp_bwd_exp(unsigned maxbits, int HW) {
+  const double tot = (double)__uint_as_float(maxbits) * (double)HW;
+  if (!(tot > 0.0) || !(tot < 1e300)) return 0;
+  const int k = 61 - ilogb(tot) - 1;
+  return k > 120 ? 120 : (k < -120 ? -120 : k);
+}
+
 __global__ void __launch_bounds__(256) homo_warp_bwd_kernel(const float* __restrict__ gout,
                                                             const float* __restrict__ rel,
                                                             const float* __restrict__ depth,
+                                                            const unsigned* __restrict__ gmax,
                                                             int C, int H, int W,
-                                                            float* __restrict__ gsrc) {
+                                                            unsigned long long* __restrict__ acc) {
   const int b = blockIdx.y;
   const int HW = H * W;
   const float* m = rel + 12 * b;
   const float dep = depth[b];
+  const int k = warp_bwd_exp(gmax[b], HW);
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
     float ix, iy;
     sample_pos(m, dep, (float)(p % W), (float)(p / W), H, W, ix, iy);
     const Taps t = make_taps(ix, iy, H, W);
     const float* g = gout + (size_t)b * C * HW + p;
-    float* s = gsrc + (size_t)b * C * HW;
+    unsigned long long* s = acc + (size_t)b * C * HW;
     for (int c = 0; c < C; ++c) {
       const float gv = g[(size_t)c * HW];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (t.ok[k]) atomicAdd(s + (size_t)c * HW + t.idx[k], t.wt[k] * gv);
+      for (int q = 0; q < 4; ++q)
+        if (t.ok[q]) {
+          const long long f = (long long)rint(ldexp((double)(t.wt[q] * gv), k));
+          if (f != 0) atomicAdd(s + (size_t)c * HW + t.idx[q], (unsigned long long)f);
+        }
     }
   }
 }
 
+__global__ void __launch_bounds__(256) warp_bwd_fold_kernel(const unsigned long long* __restrict__ acc,
+                                                            const unsigned* __restrict__ gmax, size_t n_per_b,
+                                                            int HW, float* __restrict__ gsrc) {
+  const int b = blockIdx.y;
+  const int k = warp_bwd_exp(gmax[b], HW);
+  const unsigned long long* a = acc + (size_t)b * n_per_b;
+  float* o = gsrc + (size_t)b * n_per_b;
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n_per_b; i += (size_t)gridDim.x * 256) {
+    const long long q = (long long)a[i];
+    if (q != 0) o[i] += (float)ldexp((double)q, -k);
+  }
+}
+
+size_t homo_warp_bwd_workspace_bytes(int B, int C, int H, int W) {
+  return 256 + (size_t)B * C * H * W * 8;
+}
+
 hipError_t launch_homo_warp_bwd(const float* gout, const float* rel, const float* depth, int B,
-                                int C, int H, int W, float* gsrc, hipStream_t s) {
+                                int C, int H, int W, float* gsrc, void* workspace, hipStream_t s) {
   const int HW = H * W;
-  dim3 grid((unsigned)std::min((HW + 255) / 256, 4096), (unsigned)B);
+  const size_t nb = (size_t)C * HW;
+  if (B > 64) return hipErrorInvalidValue;   // the maxima fit the 256-B header
+  unsigned* gmax = static_cast<unsigned*>(workspace);
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + 256);
   ProfScope ps(s, K_WARP);
-  hipLaunchKernelGGL(homo_warp_bwd_kernel, grid, dim3(256), 0, s, gout, rel, depth, C, H, W, gsrc);
+  hipError_t e = hipMemsetAsync(workspace, 0, homo_warp_bwd_workspace_bytes(B, C, H, W), s);
+  if (e != hipSuccess) return e;
+  const unsigned gb = (unsigned)std::min<size_t>((nb + 255) / 256, 1024);
+  hipLaunchKernelGGL(warp_bwd_max_kernel, dim3(gb, B), dim3(256), 0, s, gout, nb, gmax);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  dim3 grid((unsigned)std::min((HW + 255) / 256, 4096), (unsigned)B);
+  hipLaunchKernelGGL(homo_warp_bwd_kernel, grid, dim3(256), 0, s, gout, rel, depth, gmax, C, H, W, acc);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(warp_bwd_fold_kernel, dim3(gb, B), dim3(256), 0, s, acc, gmax, nb, HW, gsrc);
   return hipGetLastError();
 }
 
@@ -1813,6 +1875,8 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
           const int cell = obase[j] - (q >> 1) * cw - (q & 1);
           const int n = cnt[cell];
           if (n > kFbSlots) continue;
+          // ascending tile index by min / max: written for exactly two slots
+          static_assert(kFbSlots == 2, "the fixed-order gather below sorts two slots");
           const int l0 = lst[cell][0], l1 = lst[cell][1];
           for (int sl = 0; sl < n; ++sl) {
             const int pp = n == 1 ? l0 : (sl == 0 ? min(l0, l1) : max(l0, l1));

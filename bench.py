@@ -399,10 +399,10 @@ def train_bench(dev, D: int = 192, reps: int = 2):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
     peak = torch.cuda.max_memory_allocated(dev)
-    # the same steps with the backward's multi-stream schedule (AARMVS_BWD_PIPE=1: plane
-    # pipeline + group stage overlap; not bit-reproducible run to run)
+    # the same steps with the backward on one stream (AARMVS_BWD_PIPE=0; the default schedule 1
+    # overlaps the plane pipeline and the group stage, bit-identical to it)
     prev = os.environ.get("AARMVS_BWD_PIPE")
-    os.environ["AARMVS_BWD_PIPE"] = "1"
+    os.environ["AARMVS_BWD_PIPE"] = "0"
     step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -433,8 +433,9 @@ def train_bench(dev, D: int = 192, reps: int = 2):
     return dict(metric="training step (forward + mvsnet_cls_loss + backward), 1 sample / GPU",
                 config="dtu_train_640x512_n3_d192", D=D, s_per_step=round(dt, 4),
                 ms_per_plane=round(dt / D * 1e3, 3), steps_timed=reps,
-                backward_schedule="one stream (AARMVS_BWD_PIPE=0, bit-reproducible)",
-                s_per_step_multistream=round(dt_ov, 4), ms_per_plane_multistream=round(dt_ov / D * 1e3, 3),
+                backward_schedule="plane pipeline + group-stage overlap on three streams (AARMVS_BWD_PIPE=1, "
+                                  "default; bit-identical to one stream)",
+                s_per_step_one_stream=round(dt_ov, 4), ms_per_plane_one_stream=round(dt_ov / D * 1e3, 3),
                 peak_device_gb=round(peak / 1e9, 2),
                 backward=getattr(EMVSNet, "BACKWARD_PATH", "see DESIGN.md §6"),
                 loss_and_grads_finite=ok,

@@ -73,11 +73,16 @@ int aarmvs_homo_warp(const float* src_fea, const float* rel_proj, const float* d
                      int B, int C, int H, int W, float* out, hipStream_t stream);
 
 /* Backward of aarmvs_homo_warp w.r.t. src_fea (the grid carries no gradient,
- * module.py:15): grad_src += bilinear scatter of grad_out.  grad_src must be
- * zero-initialised by the caller; accumulation uses fp32 atomics (order-dependent
- * rounding). */
+ * module.py:15; grid_sample's backward at module.py:36): grad_src += bilinear
+ * scatter of grad_out.  grad_src must be initialised by the caller (zeros for the
+ * plain gradient).  The scatter sums are formed in 64-bit fixed point (exponent from
+ * max |grad_out|), so the result is bit-reproducible whatever the order the GPU
+ * serves the contributions in.  workspace: aarmvs_homo_warp_backward_workspace_bytes
+ * (caller-owned, device memory; B <= 64). */
+size_t aarmvs_homo_warp_backward_workspace_bytes(int B, int C, int H, int W);
 int aarmvs_homo_warp_backward(const float* grad_out, const float* rel_proj, const float* depth,
-                              int B, int C, int H, int W, float* grad_src, hipStream_t stream);
+                              int B, int C, int H, int W, float* grad_src, void* workspace,
+                              hipStream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Whole depth sweep (drmvsnet.py:273-291 train / :306-342 eval).

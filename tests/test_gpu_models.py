@@ -126,6 +126,12 @@ def test_homo_warping_depthwise_forward_backward():
     orc.homo_warp(src_c, rel, dep).backward(gout)
     ref_g = src_c.grad.numpy()
     np.testing.assert_allclose(src.grad.cpu().numpy(), ref_g, atol=1e-4 * np.abs(ref_g).max())
+    # the scatter is summed in fixed point: a second backward is bit-identical
+    g1 = src.grad.detach().clone()
+    src.grad = None
+    out2 = homo_warping_depthwise(src, proj[:, 1].to(DEV), proj[:, 0].to(DEV), dep.to(DEV))
+    out2.backward(gout.to(DEV))
+    assert torch.equal(src.grad, g1)
 
 
 def test_training_backward_matches_cpu_autograd():

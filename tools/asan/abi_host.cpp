@@ -76,8 +76,12 @@ int main() {
   CHECK(aarmvs_pack_params(nullptr, dummy, nullptr) == AARMVS_ERR_INVALID && has_error());
   CHECK(aarmvs_homo_warp(nullptr, dummy, dummy, 1, 32, 8, 8, dummy, nullptr) == AARMVS_ERR_INVALID);
   CHECK(aarmvs_homo_warp(dummy, dummy, dummy, 1, 32, 1, 8, dummy, nullptr) == AARMVS_ERR_INVALID);
-  CHECK(aarmvs_homo_warp_backward(dummy, dummy, dummy, 0, 32, 8, 8, dummy, nullptr) ==
+  CHECK(aarmvs_homo_warp_backward(dummy, dummy, dummy, 0, 32, 8, 8, dummy, dummy, nullptr) ==
         AARMVS_ERR_INVALID);
+  CHECK(aarmvs_homo_warp_backward(dummy, dummy, dummy, 1, 32, 8, 8, dummy, nullptr, nullptr) ==
+        AARMVS_ERR_INVALID);   // no workspace
+  CHECK(aarmvs_homo_warp_backward_workspace_bytes(1, 32, 8, 8) == 256 + 32 * 64 * 8);
+  CHECK(aarmvs_homo_warp_backward_workspace_bytes(65, 32, 8, 8) == 0);
   CHECK(aarmvs_sweep(nullptr, nullptr) == AARMVS_ERR_INVALID);
   aarmvs_sweep_args a;
   std::memset(&a, 0, sizeof(a));
