@@ -147,7 +147,14 @@ def omega_weight(sq: torch.Tensor, P: dict, fast: bool = False) -> torch.Tensor:
     t = F.conv2d(t, P[k + "1.stem.1.weight"], P[k + "1.stem.1.bias"])
     t = group_norm(t, 1, P[k + "1.stem.2.weight"], P[k + "1.stem.2.bias"], fast=fast)
     r = F.relu(t + a)                                                # ResnetBlockGn :262-263
-    return torch.sigmoid(F.conv2d(r, P[k + "2.weight"], P[k + "2.bias"]))
+    z = F.conv2d(r, P[k + "2.weight"], P[k + "2.bias"])
+    if LOGIT_HOOK is not None:   # tests: the pre-sigmoid logits (their gradients are the bias's terms)
+        LOGIT_HOOK(z)
+    return torch.sigmoid(z)
+
+
+# test hook: called with every omega logit tensor (the input of the final sigmoid) if set
+LOGIT_HOOK = None
 
 
 def cost_slice(ref_fea, src_feas, rels, depth, P, fast: bool = False) -> torch.Tensor:

@@ -102,11 +102,41 @@ def test_recorded_forward_matches_eval_sweep_and_holds_the_tensors():
     np.testing.assert_allclose(z0.cpu().numpy(), zref, atol=2e-5 * np.abs(zref).max(), rtol=0)
 
 
+# float32 CPU autograd's error depends on its reduction order, which ATen picks by thread count:
+# e.g. omega.reweight_network.2.bias of shape (2, 4, 24, 40, 5), a sum with heavy cancellation,
+# is 5.0e-7 off float64 with 1 thread and 2.0e-5 with 2-8.  The float32 reference
+# error is therefore the max over these fixed thread counts -- a fixed function of the inputs,
+# not of the host's core count.
+F32_THREADS = (1, 2, 4, 8)
+
+
 def bound(name, e_cpu32):
     """Every tensor: within 2e-5 relative L2 of float64, or twice float32 CPU autograd's own
-    error against it (the omega network's former 15x exemption was the forward cells' fp16 lo
-    parts going subnormal, fixed by their staging scales: DESIGN.md §7)."""
+    error against it, the latter taken as the max over the reduction orders of F32_THREADS
+    (the omega network's former 15x exemption was the forward cells' fp16 lo parts going
+    subnormal, fixed by their staging scales: DESIGN.md §7)."""
     return max(2e-5, 2.0 * e_cpu32)
+
+
+def _f32_spread(feats, proj, dv, P, R, g64):
+    """{tensor: max over F32_THREADS of float32 autograd's relative L2 error vs float64};
+    keys 'features', 'x' and the parameter names.  g64 = _oracle_grads(..., float64)."""
+    _, gf64, gp64, gx64 = g64
+    prev = torch.get_num_threads()
+    worst = {}
+    try:
+        for n in F32_THREADS:
+            torch.set_num_threads(n)
+            _, gf32, gp32, gx32 = _oracle_grads(feats, proj, dv, P, R, torch.float32)
+            e = {"features": rel_l2(gf32.numpy(), gf64.numpy()),
+                 "x": rel_l2(np.stack([g.numpy() for g in gx32]), np.stack([g.numpy() for g in gx64]))}
+            for k in gp64:
+                e[k] = rel_l2(gp32[k].numpy(), gp64[k].numpy())
+            for k, v in e.items():
+                worst[k] = max(worst.get(k, 0.0), v)
+    finally:
+        torch.set_num_threads(prev)
+    return worst
 
 
 def _oracle_grads(feats, proj, dv, P, R, dtype):
@@ -133,13 +163,24 @@ def _oracle_grads(feats, proj, dv, P, R, dtype):
 @pytest.mark.parametrize("shape", [(1, 3, 32, 48, 6), (2, 4, 24, 40, 5), (1, 3, 16, 24, 18)])
 def test_backward_matches_float64_autograd(shape):
     """Whole backward (regulariser + cost slice) vs float64 CPU autograd; shape 3 spans two
-    16-plane groups (the group boundary of the weight gradients and the cost-slice pass)."""
+    16-plane groups (the group boundary of the weight gradients and the cost-slice pass).
+    Bounds (fixed functions of the inputs): every tensor within max(2e-5, 2 x float32 CPU
+    autograd's error) relative L2 of float64, float32's error the max over the reduction orders
+    of F32_THREADS; the omega logits' bias (a sum over every logit's gradient with 1100-3200x
+    cancellation) within half a unit roundoff of its terms' magnitude sum."""
     B, N, H, W, D = shape
     sc, P, feats, proj, dv, sw, args = _setup(B, N, H, W, D, 11 + D, 6)
     cost, rec, rel = _record_forward(sw, args, B, H, W, D)
     R = torch.randn(B, D, H, W, generator=torch.Generator().manual_seed(5))
-    prob64, gf64, gp64, gx64 = _oracle_grads(feats, proj, dv, P, R, torch.float64)
-    _, gf32, gp32, gx32 = _oracle_grads(feats, proj, dv, P, R, torch.float32)
+    from oracle import sweep_oracle as orc
+    tsum = [0.0]   # sum over (b, view, plane, pixel) of |dL/d omega logit|: the bias's terms
+    orc.LOGIT_HOOK = lambda z: z.register_hook(lambda g: tsum.__setitem__(0, tsum[0] + float(g.abs().sum())))
+    try:
+        g64 = _oracle_grads(feats, proj, dv, P, R, torch.float64)
+    finally:
+        orc.LOGIT_HOOK = None
+    prob64, gf64, gp64, gx64 = g64
+    e32 = _f32_spread(feats, proj, dv, P, R, g64)
     prob = torch.softmax(cost, dim=1)
     np.testing.assert_allclose(prob.cpu().numpy(), prob64.numpy(), atol=1e-5)
     # dL/dcost of sum(R * softmax(cost))
@@ -150,25 +191,31 @@ def test_backward_matches_float64_autograd(shape):
     _, _, gp_r, gx = sw.backward(ref, srcs, rel, dv, rec, gcost, regulariser_only=True, want_grad_x=True)
     gx = gx.permute(0, 1, 4, 2, 3).cpu().numpy()   # [D,B,32,H,W]
     # (GPU error, float32 CPU autograd's error), both against float64
-    errs = {"x": (rel_l2(gx, np.stack([g.numpy() for g in gx64])),
-                  rel_l2(np.stack([g.numpy() for g in gx32]), np.stack([g.numpy() for g in gx64])))}
+    errs = {"x": (rel_l2(gx, np.stack([g.numpy() for g in gx64])), e32["x"])}
     for k, g in gp_r.items():
         if k.startswith("cost_regularization.") and k != "cost_regularization.conv_0.bias":
-            errs[k] = (rel_l2(g.cpu().numpy(), gp64[k].numpy()), rel_l2(gp32[k].numpy(), gp64[k].numpy()))
+            errs[k] = (rel_l2(g.cpu().numpy(), gp64[k].numpy()), e32[k])
         elif k.startswith("omega."):
             assert float(g.abs().max()) == 0.0, k
     # everything
     g_ref, g_src, gp, _ = sw.backward(ref, srcs, rel, dv, rec, gcost)
     gfeat = torch.stack([g_ref] + g_src).cpu().numpy()
-    errs["features"] = (rel_l2(gfeat, gf64.numpy()), rel_l2(gf32.numpy(), gf64.numpy()))
+    errs["features"] = (rel_l2(gfeat, gf64.numpy()), e32["features"])
     for k, g in gp.items():
         if k != "cost_regularization.conv_0.bias":   # true gradient 0 (softmax over D)
-            errs["all:" + k] = (rel_l2(g.cpu().numpy(), gp64[k].numpy()),
-                                rel_l2(gp32[k].numpy(), gp64[k].numpy()))
-    print("\nrelative L2 vs float64 (gpu, cpu float32):")
+            errs["all:" + k] = (rel_l2(g.cpu().numpy(), gp64[k].numpy()), e32[k])
+    print(f"\nrelative L2 vs float64 (gpu, cpu float32 max over threads {F32_THREADS}):")
     for k, (e, c) in errs.items():
         print(f"  {k:52s} {e:.3e} {c:.3e}")
-    bad = {k: e for k, e in errs.items() if not e[0] <= bound(k, e[1])}
+    # omega.reweight_network.2.bias is the sum of every omega logit's gradient, 1100-3200x
+    # cancelling over pixels x views x planes: its error follows the terms' magnitude, not the
+    # sum's.  Bound: |error| <= u sum|terms| / 2 (u = 2^-24; float32 autograd of these shapes
+    # sits at 0.003-0.11 u sum|terms| over F32_THREADS' reduction orders).
+    kb = "all:omega.reweight_network.2.bias"
+    ab = abs(float(gp["omega.reweight_network.2.bias"]) - float(gp64["omega.reweight_network.2.bias"]))
+    print(f"  {kb} |error| / (u sum|terms|) = {ab / (2.0 ** -24 * tsum[0]):.3f}")
+    assert ab <= 0.5 * 2.0 ** -24 * tsum[0], (ab, tsum[0])
+    bad = {k: e for k, e in errs.items() if k != kb and not e[0] <= bound(k, e[1])}
     assert not bad, bad
     assert abs(float(gp["cost_regularization.conv_0.bias"])) <= 1e-5 * float(gcost.abs().sum())
 

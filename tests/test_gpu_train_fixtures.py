@@ -70,4 +70,4 @@ def test_training_gradients_match_reference_fixture(name):
     assert not bad, bad
     # conv_0.bias (true gradient 0): a float32 residue no larger than the reference's scale
     scale = float(np.abs(fix["params"]["cost_regularization.conv_0.weight"]).max())
-    assert abs(float(gpar[tf.ZERO_GRAD])) <= 1e-3 * scale
+    assert abs(float(np.asarray(gpar[tf.ZERO_GRAD]).reshape(-1)[0])) <= 1e-3 * scale

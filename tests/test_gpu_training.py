@@ -30,6 +30,9 @@ def _gpu():
     torch.set_num_threads(min(16, os.cpu_count() or 1))
 
 
+F32_THREADS = (4, 8, 16)   # reduction orders of the float32 reference (full frame: >= 4 threads)
+
+
 def _model(D, H, W, wseed):
     from models import EMVSNet
     m = EMVSNet(disparity_level=D, image_scale=1.0, max_h=H, max_w=W, return_depth=False)
@@ -68,8 +71,9 @@ def test_config4_full_frame_training_backward_matches_cpu_autograd():
     """640x512, N=3 (configs[3]) over the first 4 of D=192's hypotheses, every gradient
     anchored to float64 CPU autograd of the oracle: per tensor, the GPU's relative L2 error
     against float64 must be at most twice the float32 CPU autograd's (the reference's own
-    arithmetic) error against float64, plus 1e-6 for tensors where float32 is exact to
-    round-off (the split-fp16 products' ~2^-22)."""
+    arithmetic) error against float64 -- the max over the reduction orders ATen uses at
+    F32_THREADS threads -- plus 1e-6 for tensors where float32 is exact to round-off (the
+    split-fp16 products' ~2^-22)."""
     B, N, H, W, D = 1, 3, 512, 640, 4
     sc = syn.scene(B, N, H, W, 192, seed=404)
     dv = torch.from_numpy(sc["depth_values"][:, :D].copy())
@@ -78,22 +82,35 @@ def test_config4_full_frame_training_backward_matches_cpu_autograd():
     feats = torch.from_numpy(sc["features"])
     proj = torch.from_numpy(sc["proj_matrices"])
     R = torch.randn(B, D, H, W, generator=torch.Generator().manual_seed(3))
-    prob32, gf32, gp32 = _oracle_grads(feats, proj, dv, P_cpu, R, torch.float32)
     prob64, gf64, gp64 = _oracle_grads(feats, proj, dv, P_cpu, R, torch.float64)
+    # float32's error depends on ATen's reduction order, i.e. its thread count: the reference
+    # error is the max over F32_THREADS (a fixed function of the inputs, not of the host)
+    e32, gb32 = {}, 0.0
+    prev = torch.get_num_threads()
+    try:
+        for n in F32_THREADS:
+            torch.set_num_threads(n)
+            _, gf32, gp32 = _oracle_grads(feats, proj, dv, P_cpu, R, torch.float32)
+            cand = {"features": _rel_err(np.moveaxis(gf32.numpy(), 0, 1), np.moveaxis(gf64.numpy(), 0, 1))}
+            cand.update({k: _rel_err(gp32[k].numpy(), gp64[k].numpy()) for k in gp64})
+            for k, v in cand.items():
+                e32[k] = max(e32.get(k, 0.0), v)
+            gb32 = max(gb32, gp32["cost_regularization.conv_0.bias"].abs().max().item())
+    finally:
+        torch.set_num_threads(prev)
 
     imgs = torch.from_numpy(np.moveaxis(sc["features"], 0, 1).copy()).to(DEV).requires_grad_(True)
     prob, _, _ = m(imgs, proj.to(DEV), dv.to(DEV))
     np.testing.assert_allclose(prob.detach().cpu().numpy(), prob64.numpy(), atol=1e-5)
     (prob * R.to(DEV)).sum().backward()
     report = {}
-    checks = [("features", imgs.grad.cpu().numpy(), np.moveaxis(gf32.numpy(), 0, 1),
-               np.moveaxis(gf64.numpy(), 0, 1))]
+    checks = [("features", imgs.grad.cpu().numpy(), np.moveaxis(gf64.numpy(), 0, 1))]
     for k, p in m.named_parameters():
         if k in P_cpu and k != "cost_regularization.conv_0.bias":   # true gradient 0 (softmax)
-            checks.append((k, p.grad.cpu().numpy(), gp32[k].numpy(), gp64[k].numpy()))
+            checks.append((k, p.grad.cpu().numpy(), gp64[k].numpy()))
     bad = []
-    for k, g_gpu, g32, g64 in checks:
-        e_gpu, e_cpu = _rel_err(g_gpu, g64), _rel_err(g32, g64)
+    for k, g_gpu, g64 in checks:
+        e_gpu, e_cpu = _rel_err(g_gpu, g64), e32[k]
         report[k] = (e_gpu, e_cpu)
         lim = 2.0 * e_cpu + 1e-6
         if not e_gpu <= lim:
@@ -104,7 +121,7 @@ def test_config4_full_frame_training_backward_matches_cpu_autograd():
     assert not bad, bad
     # the conv_0 bias: its float64 gradient is ~0; the GPU's must be as small as float32's
     gb = m.cost_regularization.conv_0.bias.grad.abs().max().item()
-    assert gb <= 2.0 * gp32["cost_regularization.conv_0.bias"].abs().max().item() + 1e-6
+    assert gb <= 2.0 * gb32 + 1e-6
 
 
 def test_second_backward_through_freed_graph_raises():
