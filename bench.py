@@ -443,6 +443,149 @@ def train_bench(dev, D: int = 192, reps: int = 2):
                 library_ms_per_step=round(lib_ms, 2), kernels=kern)
 
 
+def train_cpu_baseline(planes: int = 6):
+    """CPU leg of the training mode: float32 autograd of the oracle (the reference's own ATen
+    arithmetic) through `planes` planes of config 4's 640x512, N=3 sweep plus the softmax loss,
+    on this host's cores; scaled to one D=192 sample (the sweep's cost is uniform per plane)."""
+    from oracle import sweep_oracle as orc
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(max(1, min(threads, os.cpu_count() or 1)))
+    B, N, H, W, D = 1, 3, 512, 640, 192
+    sc = syn.scene(B, N, H, W, D, seed=0)
+    feats = torch.from_numpy(sc["features"]).requires_grad_(True)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    dv = torch.from_numpy(sc["depth_values"][:, :planes].copy())
+    P = {k: torch.from_numpy(v).requires_grad_(True) for k, v in syn.sweep_weights(1).items()}
+    rels = [orc.relative_projection(proj[:, v], proj[:, 0]) for v in range(1, N)]
+    t0 = time.perf_counter()
+    state = orc.init_state(B, H, W)
+    costs = []
+    for d in range(planes):
+        x = orc.cost_slice(feats[0], [feats[v] for v in range(1, N)], rels, dv[:, d], P, fast=True)
+        cost, state = orc.unet_step(x, state, P)
+        costs.append(cost)
+    prob = torch.softmax(torch.stack(costs, 1).squeeze(2), dim=1)
+    (-(prob.clamp_min(1e-12).log()[:, 0]).mean()).backward()
+    dt = time.perf_counter() - t0
+    s_per_sample = dt / planes * D
+    return dict(value=round(1.0 / s_per_sample, 6), unit="training samples/s", cores=torch.get_num_threads(),
+                kind="port", cpu=cpu_model(), s_per_plane=round(dt / planes, 3),
+                sample=f"oracle/sweep_oracle.py float32 autograd, forward + backward of {planes} planes of "
+                       f"640x512, N=3 (no FeatNet), {dt:.1f} s, scaled x{D // planes} to one D={D} sample; "
+                       f"torch CPU threads={torch.get_num_threads()}, CPU: {cpu_model()}")
+
+
+def train_main(args, rank: int, world: int, dev) -> None:
+    """``--train``: BASELINE configs[3] as a data-parallel training step (train.py:172 wraps the
+    model for all GPUs, train.py:288-307 is the step): one 640x512, N=3, D=192 sample per rank
+    through the drop-in models.EMVSNet (FeatNet in PyTorch, the HIP sweep and its HIP backward),
+    mvsnet_cls_loss, DDP's gradient all-reduce over RCCL (gloo in a shared-GPU rehearsal) and
+    Adam.  value = samples of all ranks / max-over-ranks wall time of the K timed steps; the
+    all-reduce is timed on its own (the DDP bucket's size, 20 repetitions) to give its share."""
+    from models.drmvsnet import EMVSNet, mvsnet_cls_loss
+    B, N, H, W, D = 1, 3, 512, 640, args.train_planes
+    g = torch.Generator(device="cpu").manual_seed(rank)
+    imgs = torch.randn(B, N, 3, H, W, generator=g).to(dev)
+    sc = syn.scene(B, N, H, W, D, seed=rank)
+    proj = torch.from_numpy(sc["proj_matrices"]).to(dev)
+    dv = torch.from_numpy(sc["depth_values"]).to(dev)
+    depth_gt = dv[:, D // 2].reshape(B, 1, 1).expand(B, H, W).contiguous()
+    mask = torch.ones(B, H, W, device=dev)
+    torch.manual_seed(0)   # one initial model on every rank (DDP also broadcasts rank 0's)
+    core = EMVSNet(D, image_scale=1.0, max_h=H, max_w=W, evidential=False).to(dev).train()
+    model = core
+    if world > 1:
+        nccl = torch.distributed.get_backend() == "nccl"
+        model = torch.nn.parallel.DistributedDataParallel(core, device_ids=[dev.index] if nccl else None)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        prob, _, _ = model(imgs, proj, dv)
+        loss = mvsnet_cls_loss(prob, depth_gt, mask, dv)[0]
+        loss.backward()
+        opt.step()
+        return loss
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    ok = bool(torch.isfinite(loss)) and all(p.grad is None or bool(torch.isfinite(p.grad).all())
+                                            for p in core.parameters())
+    nparam = sum(p.numel() for p in core.parameters() if p.requires_grad)
+    ar_ms = 0.0
+    if world > 1:   # the gradient all-reduce alone: one flat bucket of every trained parameter
+        flat = torch.zeros(nparam, device=dev if torch.distributed.get_backend() == "nccl" else "cpu")
+        for _ in range(3):
+            torch.distributed.all_reduce(flat)
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(20):
+            torch.distributed.all_reduce(flat)
+        barrier()
+        ar_ms = max_over_ranks((time.perf_counter() - t1) / 20 * 1e3, dev)
+    cpu = train_cpu_baseline() if (rank == 0 and world == 1 and not args.no_cpu) else None
+    # the training backward's dominant kernel over one profiled step (one stream, hipEvents)
+    roofline, kern = None, None
+    if rank == 0 and not args.no_kernel_timing:
+        sw = core._sweep(dev)
+        sw.overlap = False
+        ops.profile_enable(True)
+        ops.profile_reset()
+        step()
+        torch.cuda.synchronize()
+        prof = ops.profile_read()
+        ops.profile_enable(False)
+        sw.overlap = True
+        kern = train_kernel_table(prof, B, N, H, W, D)
+        cand = {k: v for k, v in kern.items() if v.get("bound") in ("hbm", "mfma", "valu")}
+        if cand:
+            dom = max(cand, key=lambda k: cand[k]["share"])
+            r = cand[dom]
+            roofline = dict(kernel=dom, bound=r["bound"], achieved=r["achieved"],
+                            peak=r.get("peak", HBM_PEAK_GBS), unit=r["unit"], frac=r["frac"], traffic=None,
+                            avg_us=r["avg_us"], timing="separate profiled step, one stream, hipEvents per launch")
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        line = {
+            "metric": "training samples/sec (config 4 DDP step: EMVSNet forward + mvsnet_cls_loss + backward "
+                      "+ gradient all-reduce + Adam)",
+            "value": round(world * args.steps / elapsed, 4),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32-class split-fp16 (3 products; weight gradients 4) on the sweep, fp32 elsewhere",
+            "data": "synthetic images ~N(0,1), SURVEY 8d cameras, random-init weights",
+            "config": {"workload": "dtu_train_640x512_n3_d192", "views": N, "H": H, "W": W, "D": D,
+                       "global_batch": B * world, "parallelism": f"ddp x{world}"},
+            "hyp_per_s": round(world * args.steps * B * H * W * D / elapsed, 1),
+            "allreduce": dict(params=nparam, bytes=nparam * 4, ms=round(ar_ms, 4),
+                              share_of_step=round(ar_ms / ms, 5) if world > 1 else 0.0,
+                              backend=torch.distributed.get_backend() if world > 1 else None,
+                              note="timed alone; DDP overlaps it with the backward"),
+            "loss_and_grads_finite": ok,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "train_kernels": kern,
+        }
+        print(json.dumps(line), flush=True)
+
+
 def spawn_ranks(n: int) -> int:
     """``--gpus N`` without a launcher: start N rank processes (one per GPU, the torchrun
     environment set by hand) from this parent, which never initialises the GPU
@@ -504,6 +647,9 @@ def main():
                     help="depth planes of the training step (BASELINE configs[3]: 192)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end EMVSNet.forward figure (FeatNet + sweep)")
+    ap.add_argument("--train", action="store_true",
+                    help="measure config 4's DDP training step (one sample per rank) instead of the "
+                         "inference sweep; --train-planes sets D")
     ap.add_argument("--planes", type=int, default=0,
                     help="profiling aid: sweep only the first P depth planes (0 = all D); "
                          "per-launch figures are unchanged, the headline value is not comparable")
@@ -519,6 +665,11 @@ def main():
     dev = torch.device("cuda", local_device_index(local))
     torch.cuda.set_device(dev)
     init_process_group(dev)
+    if args.train:
+        train_main(args, rank, world, dev)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
 
     cfg = dict(CONFIGS[args.config])
     if args.planes:
@@ -601,6 +752,11 @@ def main():
         lim = ceiling_limits()
         if lim:
             roofline["limits"] = lim
+            # what binds the dominant kernel by its counters (the HBM ratio stays in frac):
+            # omega_conv issue/latency, cost_x the vector-L1 gather path
+            if dom in lim and lim[dom].get("bound"):
+                roofline["roofline_model"] = r["bound"]
+                roofline["bound"] = lim[dom]["bound"]
 
     cpu = None
     parity = None
@@ -640,13 +796,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (cells, deconvs, omega conv: 3x f16-split MFMA, lo*lo dropped; "
-                     "fp32 accumulate)",
+            "dtype": "fp32-class split-fp16 (3 products: cells, deconvs, omega conv on f16 MFMA, lo*lo "
+                     "dropped, fp32 accumulate; fp32 elsewhere)",
             "data": "synthetic (seeded numpy features ~N(0,1), SURVEY 8d cameras, "
                     + ("random-init weights)" if args.random_weights else "model_dtu_v2 weights)"),
             "config": {"workload": args.config, "ref_views_per_gpu": B, "views": N, "H": H, "W": W,
                        "D": D, "global_batch": B * world, "parallelism": f"ref-view shard x{world}"},
             "roofline": roofline,
+            "warp_aggregation": (roofline or {}).get("warp_aggregation"),
             "cpu_baseline": cpu,
             "parity": parity,
             "fusion": fusion_res,

@@ -52,3 +52,24 @@ def test_bench_refuses_to_oversubscribe_one_gpu():
         pytest.skip("two or more GPUs visible: --gpus 2 is a real two-GPU run here")
     r = _bench(["--gpus", "2"] + SMALL)
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+
+
+TRAIN = ["--train", "--train-planes", "4", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-kernel-timing"]
+
+
+def test_bench_train_mode_one_and_two_ranks():
+    """``--train`` (config 4's DDP step, train.py:172, 288-307): one JSON line per run with
+    n_gpus = N, samples/s = N x steps over the max-over-ranks time, finite loss and gradients,
+    and (N > 1) the gradient all-reduce timed beside it."""
+    one = _bench(["--gpus", "1"] + TRAIN)
+    assert one.returncode == 0, one.stderr[-3000:]
+    two = _bench(["--gpus", "2"] + TRAIN, {"AARMVS_SHARED_GPU": "1"}, timeout=600)
+    assert two.returncode == 0, two.stderr[-3000:]
+    l1, l2 = _line(one.stdout), _line(two.stdout)
+    for ln, n in ((l1, 1), (l2, 2)):
+        assert ln["n_gpus"] == n and ln["unit"] == "samples/s"
+        assert ln["config"]["global_batch"] == n and ln["config"]["parallelism"] == f"ddp x{n}"
+        assert ln["loss_and_grads_finite"]
+        assert abs(ln["value"] * ln["ms_per_step"] / 1e3 - n) < 1e-2 * n
+    assert l2["allreduce"]["params"] == l1["allreduce"]["params"] > 0
+    assert l2["allreduce"]["ms"] > 0 and l2["allreduce"]["backend"] == "gloo"
