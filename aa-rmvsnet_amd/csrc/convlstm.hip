@@ -359,7 +359,7 @@ __device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], fl
 // -0.164 -> +0.001 ulp over 108 MFMAs).  BAL: the training cells only (their record is what
 // the BPTT differentiates); the inference cells accumulate every tap into acc with the
 // positive fragments (pack_cell_h3_kernel's second copy): 32 fewer accumulator registers.
-template <class C, int CH, bool PIPE = false, bool BAL = true>
+template <class C, int CH, bool PIPE = false, bool BAL = true, int ONCE = 0>
 __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], floatx16 (&accn)[C::MT][C::RW],
                                               const char* wl_hi, const char* wl_lo, const char* in_hi,
                                               const char* in_lo, int wave, int lane) {
@@ -368,11 +368,20 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], flo
   if constexpr (PIPE) {
     half8 bh[2][RW], bl[2][RW], ah[2][MT], al[2][MT];
     auto fetch = [&](int tap, int s) {
+      if ((ONCE & 2) && tap > 0) {   // microbenchmark ablation: B fragments of tap 0 only
+#pragma unroll
+        for (int r = 0; r < RW; ++r) bh[s][r] = bh[s ^ 1][r], bl[s][r] = bl[s ^ 1][r];
+      } else
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
         const int boff = h3_pix((wave * RW + r + tap / 3) * C::W2 + col + tap % 3, h);
         bh[s][r] = *reinterpret_cast<const half8*>(in_hi + boff);
         bl[s][r] = *reinterpret_cast<const half8*>(in_lo + boff);
+      }
+      if ((ONCE & 1) && tap > 0) {   // microbenchmark ablation: A fragments of tap 0 only
+#pragma unroll
+        for (int m = 0; m < MT; ++m) ah[s][m] = ah[s ^ 1][m], al[s][m] = al[s ^ 1][m];
+        return;
       }
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
@@ -505,7 +514,7 @@ __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 
 
 // Single-buffered kernel.  PIPE: software-pipelined fragment reads (h3_mfma_chunk).  ABL:
 // ablation bits for the microbenchmark only (1 no MFMA, 2 no staging loads/stores, 4 no
-// gate math)
+// gate math, 8 / 16 the A / B fragments read for tap 0 only)
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
           int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false>
 __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(CellDef<KIND>::MIN_WAVES))) lstm_cell_h3_kernel(
@@ -584,7 +593,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
       }
       if (CH == 0) cell_c_load<C>(a, b, yw, x0 + col, hi, cst);
       xguard_rescale<C, KIND, CH, PRECISE>(acc, accn, xr);
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE>(acc, accn, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE, (ABL >> 3) & 3>(acc, accn, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
     };
     chunk(std::integral_constant<int, 0>{});
     if constexpr (NCHK > 1) chunk(std::integral_constant<int, 1>{});
@@ -683,7 +692,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
       const char* cur = inb + 2 * par * PB;
       char* oth = inb + 2 * (par ^ 1) * PB;
       xguard_rescale<C, KIND, CH, PRECISE>(acc, accn, xr);
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE>(acc, accn, wl_hi, wl_lo, cur, cur + PB, wave, lane);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE, (ABL >> 3) & 3>(acc, accn, wl_hi, wl_lo, cur, cur + PB, wave, lane);
       if (!(ABL & 2)) {
         if (!F_NEXT || next < ntiles) st.template store<F>(oth, oth + PB, gn, tid, 0, W);
         if (!A_NEXT)

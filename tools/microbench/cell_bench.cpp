@@ -135,6 +135,11 @@ int main() {
   run("cell4 h3 RW2 W4 DB0", [&] { return run_cell_h3<4, 2, 4, 0, 0, 0>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
   run("cell3 h3 RW2 W8 DB0", [&] { return run_cell_h3<3, 2, 8, 0, 0, 1>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
   run("cell1 h3 RW2 W8 DB0", [&] { return run_cell_h3<1, 2, 8, 0, 0, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+  run("cell0 h3 DB1 A once (8)", [&] { return run_cell_h3<0, 1, 8, 8, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 DB1 B once (16)", [&] { return run_cell_h3<0, 1, 8, 16, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 DB1 A+B once (24)", [&] { return run_cell_h3<0, 1, 8, 24, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 DB1 MFMA only, A once (14)", [&] { return run_cell_h3<0, 1, 8, 14, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+  run("cell0 h3 DB1 MFMA only, A+B once (30)", [&] { return run_cell_h3<0, 1, 8, 30, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 no MFMA (1)", [&] { return run_cell_h3<0, 1, 8, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 no staging (2)", [&] { return run_cell_h3<0, 1, 8, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
   run("cell0 h3 MFMA only (6)", [&] { return run_cell_h3<0, 1, 8, 6>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
