@@ -1908,15 +1908,28 @@ __global__ void __launch_bounds__(256, AARMVS_CBF_MINB) cbw_feat_kernel(CbfArgs 
   }
   __syncthreads();
   if (use_box && !(AARMVS_CBF_ABL & 8)) {   // flush the owned box pixels (8 channels each)
+    // through LDS (sq4's 8 KB, free after the last plane) so that consecutive lanes add to
+    // consecutive channels: a wave-wide atomic covers 8 pixels x 64 B instead of 64 pixels'
+    // separate lines
     unsigned long long* gb = a.gsrc64 + (((size_t)v * pa.B + b) * 4 + c) * HW * 8;
+    float* fl = reinterpret_cast<float*>(sq4);
+    const int nbox = bxr.nx * bxr.ny;
 #pragma unroll
     for (int j = 0; j < kFbOwn; ++j) {
-      if (obase[j] < 0) continue;
-      const int i = tid + 256 * j, ry = i / bxr.nx, rx = i - ry * bxr.nx;
-      unsigned long long* gp = gb + ((size_t)(bxr.y0 + ry) * W + bxr.x0 + rx) * 8;
+      if (256 * j >= nbox) break;   // block-uniform
+      if (j > 0) __syncthreads();   // the previous round's reads done
+      *reinterpret_cast<float4*>(fl + 8 * tid) = make_float4(own[j][0], own[j][1], own[j][2], own[j][3]);
+      *reinterpret_cast<float4*>(fl + 8 * tid + 4) = make_float4(own[j][4], own[j][5], own[j][6], own[j][7]);
+      __syncthreads();
 #pragma unroll
-      for (int ch = 0; ch < 8; ++ch)
-        if (own[j][ch] != 0.f) atomicAdd(gp + ch, to_fixed(own[j][ch], fxk));
+      for (int k = 0; k < 8; ++k) {
+        const int e = tid + 256 * k, i = (e >> 3) + 256 * j, ch = e & 7;
+        const float val = fl[e];
+        if (i < nbox && val != 0.f) {
+          const int ry = i / bxr.nx, rx = i - ry * bxr.nx;
+          atomicAdd(gb + ((size_t)(bxr.y0 + ry) * W + bxr.x0 + rx) * 8 + ch, to_fixed(val, fxk));
+        }
+      }
     }
   }
   const int ntiles = tiles_x * ((H + kFbT - 1) / kFbT);

@@ -36,5 +36,8 @@ for _ in range(3):
 e1.record()
 torch.cuda.synchronize()
 chk = float(out[0].double().abs().sum()) + sum(float(x.double().abs().sum()) for x in out[1])
+import hashlib  # noqa: E402
+dig = hashlib.sha256(b"".join(t.detach().cpu().contiguous().numpy().tobytes()
+                              for t in [out[0], *out[1], *[out[2][k] for k in sorted(out[2])]])).hexdigest()[:12]
 print(f"{os.environ.get('AARMVS_LIB', 'in-tree')}: backward {e0.elapsed_time(e1) / 3:8.2f} ms "
-      f"({D} planes) |g_feat| {chk:.6e}", flush=True)
+      f"({D} planes) |g_feat| {chk:.6e} digest {dig}", flush=True)
