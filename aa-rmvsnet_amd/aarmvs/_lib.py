@@ -130,6 +130,9 @@ SIGNATURES = {
     "aarmvs_evidential_epilogue_backward": (c_int, [ctypes.POINTER(c_void_p), c_void_p, c_int, c_int,
                                                     c_void_p, c_void_p, ctypes.POINTER(c_void_p),
                                                     c_void_p]),
+    "aarmvs_deform_sample": (c_int, [c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p, c_void_p]),
+    "aarmvs_deform_sample_backward": (c_int, [c_void_p, c_void_p, c_void_p] + [c_int] * 8
+                                      + [c_void_p] * 5),
     "aarmvs_profile_enable": (None, [c_int]),
     "aarmvs_profile_reset": (None, []),
     "aarmvs_profile_kernel_count": (c_int, []),

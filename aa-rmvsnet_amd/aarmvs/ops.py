@@ -292,6 +292,60 @@ class _EvidentialEpilogue(torch.autograd.Function):
         return (None, *gh)
 
 
+class _DeformSample(torch.autograd.Function):
+    """The sampling half of DeformConv2d (aarmvs_deform_sample, the reference's
+    models/module.py:160-219): x NHWC [B,H,W,32], offset [B,18,h,w], mask [B,9,h,w] or None ->
+    val [B,h*w,9*32], the A operand of the (tap, channel) contraction; differentiable in x,
+    offset and mask."""
+
+    @staticmethod
+    def forward(ctx, x_nhwc, offset, mask, stride, pad):
+        x_nhwc, offset = x_nhwc.contiguous(), offset.contiguous()
+        mask = mask.contiguous() if mask is not None else None
+        ts = [x_nhwc, offset] + ([mask] if mask is not None else [])
+        _require_device(*ts)
+        if any(t.device != x_nhwc.device for t in ts):
+            raise AarmvsError("aarmvs: deform_sample tensors must be on one device")
+        B, H, W, C = x_nhwc.shape
+        h, w = offset.shape[2:]
+        if tuple(offset.shape) != (B, 18, h, w) or (mask is not None and tuple(mask.shape) != (B, 9, h, w)):
+            raise ValueError(f"deform_sample: offset / mask shapes {tuple(offset.shape)} / "
+                             f"{None if mask is None else tuple(mask.shape)} for x {tuple(x_nhwc.shape)}")
+        val = torch.empty(B, h * w, 9 * C, device=x_nhwc.device, dtype=torch.float32)
+        check(lib().aarmvs_deform_sample(x_nhwc.data_ptr(), offset.data_ptr(), _ptr(mask), B, C, H, W,
+                                         h, w, stride, pad, val.data_ptr(), _stream()), "deform_sample")
+        ctx.save_for_backward(x_nhwc, offset, mask)
+        ctx.geom = (stride, pad)
+        return val
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g_val):
+        x_nhwc, offset, mask = ctx.saved_tensors
+        stride, pad = ctx.geom
+        g_val = g_val.contiguous()
+        _require_device(g_val)
+        if g_val.device != x_nhwc.device:
+            raise AarmvsError("aarmvs: deform_sample gradient on another device")
+        B, H, W, C = x_nhwc.shape
+        h, w = offset.shape[2:]
+        gx = torch.zeros_like(x_nhwc)
+        goff = torch.empty_like(offset)
+        gm = torch.empty_like(mask) if mask is not None else None
+        check(lib().aarmvs_deform_sample_backward(x_nhwc.data_ptr(), offset.data_ptr(), _ptr(mask), B, C,
+                                                  H, W, h, w, stride, pad, g_val.data_ptr(),
+                                                  gx.data_ptr(), goff.data_ptr(), _ptr(gm), _stream()),
+              "deform_sample_backward")
+        return gx, goff, gm, None, None
+
+
+@_on_tensor_device
+def deform_sample(x_nhwc: torch.Tensor, offset: torch.Tensor, mask: torch.Tensor | None, stride: int = 1,
+                  pad: int = 1) -> torch.Tensor:
+    """val [B, h*w, 9*C] of DeformConv2d's sampling (C == 32), differentiable (see _DeformSample)."""
+    return _DeformSample.apply(x_nhwc, offset, mask, int(stride), int(pad))
+
+
 @_on_tensor_device
 def evidential_epilogue(h0: torch.Tensor, h1: torch.Tensor, h2: torch.Tensor, depth_values: torch.Tensor):
     """(evidential [4,H,W], prob_combine [1,D,H,W]) from classif0/1/2's outputs [1,4,D,H,W]

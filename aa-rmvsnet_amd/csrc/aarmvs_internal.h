@@ -207,6 +207,20 @@ hipError_t launch_softmax_depth(const float* cost, float* prob, int B, int D, in
 hipError_t launch_evidential(const float* const head[3], const float* dv, int D, int HW, float* ev,
                              float* pc, const float* g_ev, const float* g_pc, float* const g_head[3],
                              hipStream_t s);
+// the sampling half of FeatNet's deformable conv (deform.hip): val from x (forward), or dL/dx,
+// dL/d offset, dL/d m from dL/d val (backward)
+struct DfArgs {
+  const float* x;        // [B][H][W][C]
+  const float* off;      // [B][18][h][w]
+  const float* m;        // [B][9][h][w] or null (no modulation)
+  int B, H, W, h, w, stride, pad;
+  float* val;            // [B][h w][9][C]
+  const float* gval;     // backward: dL/d val
+  float* gx;             // backward: dL/d x, NHWC, accumulated
+  float* goff;           // backward: dL/d offset
+  float* gm;             // backward: dL/d m (null if m is null)
+};
+hipError_t launch_deform_sample(const DfArgs& a, bool bwd, hipStream_t s);
 // GroupNorm of NCHW [B][C][HW] fp32 (group_norm.hip): mean_rstd [B][G][2]; gamma / beta may
 // be null (1 / 0); scratch of gn_scratch_bytes(B, C, HW); bwd also writes s1 = sum dy xhat and
 // s2 = sum dy per (b, c) (the per-sample dgamma / dbeta terms)
@@ -313,7 +327,7 @@ enum KernelId : int {
   K_DGRAD0, K_DGRAD1, K_DGRAD2, K_DGRAD3, K_DGRAD4,
   K_WGRAD0, K_WGRAD1, K_WGRAD2, K_WGRAD3, K_WGRAD4,
   K_GNB_PARTIAL, K_DECONV_BWD, K_BWD_SMALL, K_CBW_CHAIN, K_CBW_FEAT, K_CBW_SMALL,
-  K_DECONV_WGRAD, K_HEAD_WGRAD,
+  K_DECONV_WGRAD, K_HEAD_WGRAD, K_DEFORM,
   K_COUNT
 };
 extern bool g_prof_on;

@@ -99,7 +99,7 @@ static const char* kKernelNames[K_COUNT] = {
     "dgrad0", "dgrad1", "dgrad2", "dgrad3", "dgrad4",
     "wgrad0", "wgrad1", "wgrad2", "wgrad3", "wgrad4",
     "gnb_partial", "deconv_bwd", "bwd_small", "cbw_chain", "cbw_feat", "cbw_small",
-    "deconv_wgrad", "head_wgrad"};
+    "deconv_wgrad", "head_wgrad", "deform_sample"};
 
 static hipEvent_t prof_event() {
   if (g_prof_used == g_prof_pool.size()) {
@@ -937,6 +937,60 @@ int aarmvs_evidential_epilogue_backward(const float* const head[3], const float*
   hipError_t e = launch_evidential(head, depth_values, D, HW, nullptr, nullptr, grad_evidential,
                                    grad_prob_combine, grad_head, stream);
   return e == hipSuccess ? AARMVS_OK : hip_fail(e, "evidential_epilogue_backward");
+}
+
+static int deform_check(const char* who, const float* x, const float* offset, int B, int C, int H,
+                        int W, int h, int w, int stride, int pad) {
+  if (!x || !offset) return fail(AARMVS_ERR_INVALID, std::string(who) + ": null pointer");
+  if (C != AARMVS_DEFORM_C)
+    return fail(AARMVS_ERR_INVALID, std::string(who) + ": C must be 32 (FeatNet's deformable convs)");
+  if (B < 1 || H < 1 || W < 1 || h < 1 || w < 1 || stride < 1 || pad < 0)
+    return fail(AARMVS_ERR_INVALID, std::string(who) + ": bad geometry");
+  return AARMVS_OK;
+}
+
+static DfArgs deform_args(const float* x, const float* offset, const float* mask, int B, int H,
+                          int W, int h, int w, int stride, int pad) {
+  DfArgs a{};
+  a.x = x;
+  a.off = offset;
+  a.m = mask;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.h = h;
+  a.w = w;
+  a.stride = stride;
+  a.pad = pad;
+  return a;
+}
+
+int aarmvs_deform_sample(const float* x_nhwc, const float* offset, const float* mask, int B, int C,
+                         int H, int W, int h, int w, int stride, int pad, float* val,
+                         hipStream_t stream) {
+  if (int rc = deform_check("deform_sample", x_nhwc, offset, B, C, H, W, h, w, stride, pad)) return rc;
+  if (!val) return fail(AARMVS_ERR_INVALID, "deform_sample: null pointer");
+  DfArgs a = deform_args(x_nhwc, offset, mask, B, H, W, h, w, stride, pad);
+  a.val = val;
+  hipError_t e = launch_deform_sample(a, false, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "deform_sample");
+}
+
+int aarmvs_deform_sample_backward(const float* x_nhwc, const float* offset, const float* mask, int B,
+                                  int C, int H, int W, int h, int w, int stride, int pad,
+                                  const float* grad_val, float* grad_x_nhwc, float* grad_offset,
+                                  float* grad_mask, hipStream_t stream) {
+  if (int rc = deform_check("deform_sample_backward", x_nhwc, offset, B, C, H, W, h, w, stride, pad))
+    return rc;
+  if (!grad_val || !grad_x_nhwc || !grad_offset || (mask && !grad_mask))
+    return fail(AARMVS_ERR_INVALID, "deform_sample_backward: null pointer");
+  DfArgs a = deform_args(x_nhwc, offset, mask, B, H, W, h, w, stride, pad);
+  a.gval = grad_val;
+  a.gx = grad_x_nhwc;
+  a.goff = grad_offset;
+  a.gm = mask ? grad_mask : nullptr;
+  hipError_t e = launch_deform_sample(a, true, stream);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "deform_sample_backward");
 }
 
 }  // extern "C"

@@ -147,6 +147,8 @@ class DeformConv2d(nn.Module):
             nn.init.constant_(self.m_conv.weight, 0)
 
     def forward(self, x):
+        if x.is_cuda and self.kernel_size == 3 and x.shape[1] == 32 and x.dtype == torch.float32:
+            return self._forward_hip(x)
         ks = self.kernel_size
         n_taps = ks * ks
         offset = self.p_conv(x)                                   # [B, 2n, h, w]
@@ -165,11 +167,13 @@ class DeformConv2d(nn.Module):
         r0c, r1c = r0.clamp(0, Hp - 1), (r0 + 1).clamp(0, Hp - 1)
         c0c, c1c = c0.clamp(0, Wp - 1), (c0 + 1).clamp(0, Wp - 1)
         pr, pc = pr.clamp(0, Hp - 1), pc.clamp(0, Wp - 1)
-        flat = xp.reshape(B, xp.shape[1], Hp * Wp)
-
-        def tap(ri, ci):
-            idx = (ri.long() * Wp + ci.long()).reshape(B, 1, -1).expand(-1, flat.shape[1], -1)
-            return flat.gather(2, idx).view(B, flat.shape[1], h, w, n_taps)
+        C = xp.shape[1]
+        # channels-last rows: one gather of the four corners' 32-channel rows (the backward
+        # is one scatter-add of contiguous rows, not 4 x C strided planes)
+        rows_cl = xp.permute(0, 2, 3, 1).reshape(B, Hp * Wp, C)
+        idx = torch.stack([r0c * Wp + c0c, r1c * Wp + c1c, r0c * Wp + c1c, r1c * Wp + c0c], 1)
+        idx = idx.long().reshape(B, -1, 1).expand(-1, -1, C)              # [B, 4 h w n, C]
+        taps = rows_cl.gather(1, idx).view(B, 4, h * w * n_taps, C)
 
         # corner weights: (lt) (1+(r0-p))(1+(c0-p)), (rb) (1-(r1-p))(1-(c1-p)),
         # (lb) rows r0 / cols c1, (rt) rows r1 / cols c0
@@ -177,15 +181,36 @@ class DeformConv2d(nn.Module):
         g_rb = (1 - (r1c - pr)) * (1 - (c1c - pc))
         g_lb = (1 + (r0c - pr)) * (1 - (c1c - pc))
         g_rt = (1 - (r1c - pr)) * (1 + (c0c - pc))
-        val = (g_lt.unsqueeze(1) * tap(r0c, c0c) + g_rb.unsqueeze(1) * tap(r1c, c1c)
-               + g_lb.unsqueeze(1) * tap(r0c, c1c) + g_rt.unsqueeze(1) * tap(r1c, c0c))
+        g = torch.stack([g_lt, g_rb, g_lb, g_rt], 1).reshape(B, 4, h * w * n_taps, 1)
+        val = g[:, 0] * taps[:, 0] + g[:, 1] * taps[:, 1] + g[:, 2] * taps[:, 2] + g[:, 3] * taps[:, 3]
         if self.modulation:
-            val = val * torch.sigmoid(self.m_conv(x)).permute(0, 2, 3, 1).unsqueeze(1)
-        wgt = self.conv.weight.reshape(self.conv.out_channels, -1, n_taps)
-        out = torch.einsum("bchwn,ocn->bohw", val, wgt)
+            m = torch.sigmoid(self.m_conv(x)).permute(0, 2, 3, 1).reshape(B, h * w * n_taps, 1)
+            val = val * m
+        # sum_{c,n} W[o,c,n] val[c,n] as one GEMM over (n, c)
+        wgt = self.conv.weight.reshape(self.conv.out_channels, C, n_taps).permute(2, 1, 0)
+        out = val.view(B, h * w, n_taps * C) @ wgt.reshape(n_taps * C, -1)   # [B, h w, O]
+        out = out.view(B, h, w, -1).permute(0, 3, 1, 2)
         if self.conv.bias is not None:
             out = out + self.conv.bias.view(1, -1, 1, 1)
-        return out
+        return out.contiguous()
+
+
+    def _forward_hip(self, x):
+        """The same operator on the GPU: the sampling (with modulation) as one HIP kernel
+        (aarmvs_deform_sample, forward and backward), the contraction with the weights as one
+        GEMM over (tap, channel)."""
+        from aarmvs import ops
+        offset = self.p_conv(x)
+        B, C, _, _ = x.shape
+        h, w = offset.shape[2:]
+        m = torch.sigmoid(self.m_conv(x)) if self.modulation else None
+        val = ops.deform_sample(x.permute(0, 2, 3, 1).contiguous(), offset, m, self.stride, self.padding)
+        wgt = self.conv.weight.reshape(self.conv.out_channels, C, 9).permute(2, 1, 0)
+        out = val @ wgt.reshape(9 * C, -1)                                     # [B, h w, O]
+        out = out.view(B, h, w, -1).permute(0, 3, 1, 2)
+        if self.conv.bias is not None:
+            out = out + self.conv.bias.view(1, -1, 1, 1)
+        return out.contiguous()
 
 
 def deformconvgnrelu(in_channels, out_channels, kernel_size=3, stride=1, dilation=1, bias=True,

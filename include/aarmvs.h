@@ -301,6 +301,29 @@ int aarmvs_evidential_epilogue_backward(const float* const head[3], const float*
                                         hipStream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * The sampling half of FeatNet's modulated deformable convolution (models/module.py:105-236,
+ * DeformConv2d.forward; used by IntraViewAAModule, drmvsnet.py:7-24): for output pixel (i, j)
+ * and tap n of the 3x3 kernel, the bilinear sample of the zero-padded input at
+ * (i*stride + 1 + n/3 - 1 + offset[n], j*stride + 1 + n%3 - 1 + offset[9 + n]) with the
+ * reference's clamping and corner weights (:160-214), times mask[n] (the sigmoid of m_conv,
+ * :216-219; NULL: no modulation).  x_nhwc [B][H][W][C] (C == 32), offset [B][18][h][w], mask
+ * [B][9][h][w], val [B][h*w][9][C]: the A operand of the conv over (tap, channel) (:230-234),
+ * which the caller multiplies by the weights [9*C][outc].  The forward's val equals the
+ * reference's sampled tensor op for op in fp32.  The backward takes dL/d val and ADDS dL/dx
+ * into grad_x_nhwc (atomically: zero it first), and writes dL/d offset [B][18][h][w] and
+ * dL/d mask [B][9][h][w] (NULL when mask is NULL); like the reference's gather backward, dL/dx's
+ * summation order is not fixed.
+ * ------------------------------------------------------------------------- */
+#define AARMVS_DEFORM_C 32
+int aarmvs_deform_sample(const float* x_nhwc, const float* offset, const float* mask, int B, int C,
+                         int H, int W, int h, int w, int stride, int pad, float* val,
+                         hipStream_t stream);
+int aarmvs_deform_sample_backward(const float* x_nhwc, const float* offset, const float* mask, int B,
+                                  int C, int H, int W, int h, int w, int stride, int pad,
+                                  const float* grad_val, float* grad_x_nhwc, float* grad_offset,
+                                  float* grad_mask, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Opt-in per-kernel timing (a diagnostic, not part of the reference interface).
  * When enabled, every launch made by the entry points above is bracketed by
  * hipEvents on its stream; aarmvs_profile_read synchronises on the recorded

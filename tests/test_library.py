@@ -34,6 +34,26 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == set(declared_functions())
 
 
+def declared_arity():
+    """{function: number of parameters} from the prototypes in include/aarmvs.h."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(aarmvs_[a-z_0-9]+)\s*\(([^;{]*?)\)\s*;", text):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_ctypes_signatures_match_the_header_arity():
+    """Every ctypes binding passes as many arguments as the C prototype takes (a short
+    argtypes list makes ctypes refuse the call only when it runs -- on the GPU box)."""
+    from aarmvs import _lib
+    arity = declared_arity()
+    assert set(arity) == set(_lib.SIGNATURES)
+    for name, (_, argtypes) in _lib.SIGNATURES.items():
+        assert len(argtypes) == arity[name], (name, len(argtypes), arity[name])
+
+
 def test_host_only_queries():
     from aarmvs import lib
     L = lib()
