@@ -260,7 +260,7 @@ def e2e_bench(N: int, H: int, W: int, D: int, B: int, dev, reps: int = 2):
     del feats, out, model
     return dict(metric="end-to-end depth-hypotheses/s (EMVSNet.forward: FeatNet + sweep)",
                 value=round(B * H * W * D / dt, 1), s_per_step=round(dt, 4),
-                featnet_s=round(ft, 4), featnet="PyTorch (MIOpen) fp32, out of the §8 scope",
+                featnet_s=round(ft, 4), featnet="PyTorch (MIOpen) fp32 convs + the HIP deformable-conv sampling (aarmvs_deform_sample); outside the §8 scope",
                 images=f"[{B},{N},3,{H},{W}] ~N(0,1)", depth_finite=ok)
 
 
