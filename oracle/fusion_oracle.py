@@ -78,7 +78,8 @@ def reproject_with_depth(depth_ref, intrinsics_ref, extrinsics_ref, depth_src, i
                                 np.vstack((xyz_src, np.ones_like(x_ref))))[:3]
     depth_reprojected = xyz_reprojected[2].reshape([height, width]).astype(np.float32)
     K_xyz_reprojected = np.matmul(intrinsics_ref, xyz_reprojected)
-    xy_reprojected = K_xyz_reprojected[:2] / K_xyz_reprojected[2:3]
+    with np.errstate(divide="ignore", invalid="ignore"):   # depth 0 -> inf / nan, as the reference
+        xy_reprojected = K_xyz_reprojected[:2] / K_xyz_reprojected[2:3]
     x_reprojected = xy_reprojected[0].reshape([height, width]).astype(np.float32)
     y_reprojected = xy_reprojected[1].reshape([height, width]).astype(np.float32)
     return depth_reprojected, x_reprojected, y_reprojected, x_src, y_src
