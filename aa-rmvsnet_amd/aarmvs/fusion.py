@@ -8,8 +8,8 @@ launch (``aarmvs_fusion_filter``).  ``fuse_points`` back-projects the kept pixel
 points (fusion.py:235-246), and ``filter_depth`` is the per-scan driver (fusion.py:135-273):
 pair file, per reference view the image rescale/crop and camera re-centring, the GPU core
 against every source view, the three mask PNGs and the scan's PLY.  The file helpers
-read/write the formats the fusion step consumes: PFM maps (datasets/data_io.py:9-74), cam
-files (fusion.py:27-42), pair files (fusion.py:57-68), images (fusion.py:45-50), masks
+read/write the formats the fusion step consumes: PFM maps (``datasets.data_io``, the
+reference's datasets/data_io.py:9-74, re-exported here), cam files (fusion.py:27-42), pair files (fusion.py:57-68), images (fusion.py:45-50), masks
 (fusion.py:52-56) and a binary PLY writer for the point cloud.
 Depth maps must be CUDA float32 tensors; there is no CPU fallback.
 """
@@ -18,11 +18,11 @@ from __future__ import annotations
 import os
 
 import ctypes
-import re
-import sys
 
 import numpy as np
 import torch
+
+from datasets.data_io import read_pfm, save_pfm  # noqa: F401  (fusion.read_pfm / save_pfm)
 
 from . import _lib
 from ._lib import AarmvsError, check, lib
@@ -217,44 +217,6 @@ def save_mask(filename, mask):
     if mask.dtype != np.bool_:
         raise ValueError("save_mask: mask must be boolean")
     Image.fromarray(mask.astype(np.uint8) * 255).save(filename)
-def read_pfm(filename):
-    """(data float32 [H,W] or [H,W,3], scale), rows bottom-up in the file (data_io.py:9-45)."""
-    with open(filename, "rb") as f:
-        header = f.readline().decode("utf-8").rstrip()
-        if header not in ("PF", "Pf"):
-            raise ValueError("Not a PFM file.")
-        m = re.match(r"^(\d+)\s(\d+)\s$", f.readline().decode("utf-8"))
-        if not m:
-            raise ValueError("Malformed PFM header.")
-        width, height = map(int, m.groups())
-        scale = float(f.readline().rstrip())
-        endian = "<" if scale < 0 else ">"
-        data = np.fromfile(f, endian + "f")
-    shape = (height, width, 3) if header == "PF" else (height, width)
-    return np.flipud(np.reshape(data, shape)), abs(scale)
-
-
-def save_pfm(filename, image, scale=1):
-    """data_io.py:48-74: float32 [H,W] / [H,W,1] / [H,W,3], native byte order."""
-    if image.dtype != np.float32:
-        raise ValueError("Image dtype must be float32.")
-    if image.ndim == 3 and image.shape[2] == 3:
-        color = True
-    elif image.ndim == 2 or (image.ndim == 3 and image.shape[2] == 1):
-        color = False
-    else:
-        raise ValueError("Image must have H x W x 3, H x W x 1 or H x W dimensions.")
-    image = np.flipud(image)
-    endian = image.dtype.byteorder
-    if endian == "<" or (endian == "=" and sys.byteorder == "little"):
-        scale = -scale
-    with open(filename, "wb") as f:
-        f.write(b"PF\n" if color else b"Pf\n")
-        f.write(f"{image.shape[1]} {image.shape[0]}\n".encode("utf-8"))
-        f.write(("%f\n" % scale).encode("utf-8"))
-        np.ascontiguousarray(image).tofile(f)
-
-
 def read_camera_parameters(filename, scale=1.0, index=0, flag=0):
     """(intrinsics float32 3x3, extrinsics float32 4x4) of a cam.txt, intrinsics scaled and
     shifted for the resized / cropped image (fusion.py:27-42)."""
