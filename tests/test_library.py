@@ -89,3 +89,20 @@ def test_library_calls_run_under_their_tensors_device(monkeypatch):
     assert f(sw) == "ran" and entered == [torch.device("cuda", 3)]
     assert f(torch.zeros(1)) == "ran" and len(entered) == 1          # CPU tensors: no guard
     assert f(None, x=torch.device("cuda", 1)) == "ran" and entered[-1] == torch.device("cuda", 1)
+
+
+def test_deform_sample_rejects_bad_geometry_before_launching():
+    """aarmvs_deform_sample validates on the host (no device work, so it runs here): null
+    pointers, C other than 32 and non-positive sizes are refused with a message."""
+    from aarmvs import lib
+    L = lib()
+    fake = 0x1000   # never dereferenced: validation fails first
+    assert L.aarmvs_deform_sample(None, fake, None, 1, 32, 8, 8, 8, 8, 1, 1, fake, None) != 0
+    assert b"null" in L.aarmvs_last_error()
+    assert L.aarmvs_deform_sample(fake, fake, None, 1, 16, 8, 8, 8, 8, 1, 1, fake, None) != 0
+    assert b"32" in L.aarmvs_last_error()
+    assert L.aarmvs_deform_sample(fake, fake, None, 1, 32, 8, 8, 0, 8, 1, 1, fake, None) != 0
+    assert b"geometry" in L.aarmvs_last_error()
+    assert L.aarmvs_deform_sample_backward(fake, fake, fake, 1, 32, 8, 8, 8, 8, 1, 1, fake, fake, fake,
+                                           None, None) != 0   # mask given, its gradient missing
+    assert b"null" in L.aarmvs_last_error()
