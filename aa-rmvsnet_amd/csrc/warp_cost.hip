@@ -254,9 +254,11 @@ struct PipeArgs {
   // the launch's grouping and of block timing)
   double* part;
   int part_n;
+  int omega_ipb;              // omega_mfma: items per block (AARMVS_OMEGA_IPB, default 1)
 };
 
-__device__ __forceinline__ void part_put(const PipeArgs& a, int kp, int b, int v, int i, double s,
+template <typename PA>
+__device__ __forceinline__ void part_put(PA& a, int kp, int b, int v, int i, double s,
                                          double ss) {
   const size_t k = (((size_t)kp * a.B + b) * a.nsrc + v) * a.part_n + i;
   a.part[2 * k] = s;
@@ -687,6 +689,7 @@ struct OmegaTile {
   static constexpr int OUTH = kMTileH - 2, OUTW = TW - 2;
   static constexpr int BOXPX = 2 * NT;      // LDS source-box capacity (32-B pixels)
   static int tiles(int H, int W) { return ((W + OUTW - 1) / OUTW) * ((H + OUTH - 1) / OUTH); }
+  __device__ static int tiles_d(int H, int W) { return ((W + OUTW - 1) / OUTW) * ((H + OUTH - 1) / OUTH); }
 };
 constexpr int kOmegaTW = 16;   // the library's tile width
 
@@ -695,13 +698,13 @@ constexpr int kOmegaTW = 16;   // the library's tile width
 // loads, 16 sampling positions without the homography divisions (the own pixel), 32 no Y
 // image / gather (t1 from the accumulators), 64 no statistics atomics, 128 no B-fragment loads
 // BAL: sign-balanced accumulation, for the training sweep only: +9% time
-template <int ABL = 0, int TW = kOmegaTW, bool BAL = false>
-__global__ void __launch_bounds__(OmegaTile<TW>::NT) __attribute__((amdgpu_waves_per_eu(4)))
-omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restrict__ Rel,
-                  const unsigned* __restrict__ xbound) {
+// one (tile, view, plane) item of omega_mfma_kernel (seq: its index in the launch's order)
+template <int ABL, int TW, bool BAL, typename PA>
+__device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
+                                           const float* __restrict__ Rel,
+                                           const unsigned* __restrict__ xbound, const int seq) {
   using T = OmegaTile<TW>;
   constexpr int kMThreads = T::NT, kMBoxPx = T::BOXPX, kMOutH = T::OUTH, kMOutW = T::OUTW;
-  if (blockDim.x != kMThreads) return;   // LDS images are sized for exactly this block
   constexpr int NB = (2 * kMBoxPx + kMThreads - 1) / kMThreads;   // box pieces per thread
   constexpr int YFL = kMThreads * kMYStride;                      // Y image floats
   static_assert(YFL >= (kMBoxPx + 1) * 8, "the box fits in the Y image space");
@@ -710,12 +713,11 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   float* const yimg = smem;
   __shared__ int red[kMThreads / 64][4];
   __shared__ double wsum[kMThreads / 64][2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tid;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));   // see omega_mfma_kernel
+  const int lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.z;
   const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
-  // a tile's (view, plane) blocks are consecutive on one XCD: the reference tile, and a
-  // view's source box across the npl neighbouring planes, come from its L2
-  const int seq = xcd_tile(blockIdx.x, gridDim.x);
   const int tile = seq / (nsrc * a.npl), vk = seq - tile * (nsrc * a.npl);
   const int v = vk / a.npl, kp = vk - v * a.npl;
   const int tiles_x = (W + kMOutW - 1) / kMOutW;
@@ -958,6 +960,32 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
   }
 }
 
+// The kernel: a block takes a.omega_ipb consecutive items (default 1).  A tile's (view, plane)
+// items are consecutive on one XCD (xcd_tile): the reference tile, and a view's source box
+// across the npl neighbouring planes, come from its L2.
+template <int ABL = 0, int TW = kOmegaTW, bool BAL = false>
+__global__ void __launch_bounds__(OmegaTile<TW>::NT) __attribute__((amdgpu_waves_per_eu(4)))
+omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restrict__ Rel,
+                  const unsigned* __restrict__ xbound) {
+  if (blockDim.x != OmegaTile<TW>::NT) return;   // LDS images are sized for exactly this block
+  const int ipb = a.omega_ipb > 1 ? a.omega_ipb : 1;
+  const int total = OmegaTile<TW>::tiles_d(a.H, a.W) * a.nsrc * a.npl;
+  const int bs = xcd_tile(blockIdx.x, gridDim.x);
+#pragma unroll 1
+  for (int it = 0; it < ipb; ++it) {
+    const int seq = bs * ipb + it;
+    if (seq >= total) break;
+    if (it) __syncthreads();   // the previous item's LDS reads are done
+    // the item reads the arguments through a pointer the compiler cannot prove invariant
+    // across items: otherwise it hoists every argument load out of the loop (SGPR spills)
+    uint32_t z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    typedef const __attribute__((address_space(4))) PipeArgs KPipeArgs;
+    KPipeArgs& ka = *(KPipeArgs*)((const __attribute__((address_space(4))) char*)&a + z);
+    omega_item<ABL, TW, BAL>(ka, P, Rel, xbound, seq);
+  }
+}
+
 // GN #STAGE (1 or 2) partial sums of the omega chain on t1 (plane d_next).
 template <int STAGE>
 __global__ void __launch_bounds__(256) omega_stats_kernel(PipeArgs a,
@@ -1084,6 +1112,19 @@ static int pipe_box_cap() {
   return (s && *s) ? std::max(4, std::atoi(s)) : INT_MAX;
 }
 
+// omega_mfma items per block: a block walks ipb consecutive (plane) items of one (tile, view),
+// so its fixed cost (prologue, box set-up, statistics hand-off) is paid once per ipb items:
+// -3..10% omega time at the headline geometry.  Default 4, halved while the
+// grid would hold fewer than 8 blocks per CU; AARMVS_OMEGA_IPB=n forces n (results are
+// bit-identical for every n: the items' arithmetic does not change).
+static int omega_ipb(int items, int cu_count) {
+  const char* s = std::getenv("AARMVS_OMEGA_IPB");
+  if (s && *s) return std::max(1, std::min(8, std::atoi(s)));
+  int ipb = 4;
+  while (ipb > 1 && (items + ipb - 1) / ipb < 8 * std::max(1, cu_count)) ipb >>= 1;
+  return ipb;
+}
+
 static PipeArgs pipe_args_c8(const CostArgs& ca, const SweepGeom& g, const Workspace& ws) {
   PipeArgs a = pipe_args(ca, g, ws);
   // the pipeline reads the c8 copies of the features in the workspace
@@ -1136,11 +1177,13 @@ hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Work
     const int ntiles = OmegaTile<kOmegaTW>::tiles(g.H, g.W);
     ProfScope ps(s, K_OMEGA_CONV);
     a.part_n = ntiles;
+    a.omega_ipb = omega_ipb(ntiles * g.nsrc * n * g.B, g.cu_count);
+    const int nblk = (ntiles * g.nsrc * n + a.omega_ipb - 1) / a.omega_ipb;
     if (balanced)
-      hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW, true>), dim3(ntiles * g.nsrc * n, 1, g.B),
+      hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW, true>), dim3(nblk, 1, g.B),
                          dim3(OmegaTile<kOmegaTW>::NT), 0, s, a, a.params, a.rel, ws.xbound);
     else
-      hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW>), dim3(ntiles * g.nsrc * n, 1, g.B),
+      hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW>), dim3(nblk, 1, g.B),
                          dim3(OmegaTile<kOmegaTW>::NT), 0, s, a, a.params, a.rel, ws.xbound);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

@@ -199,6 +199,25 @@ def test_pipeline_box_fallbacks_are_bit_identical(monkeypatch, cap):
         assert torch.equal(a[k], b[k]), k
 
 
+@pytest.mark.parametrize("ipb", ["1", "3", "8"])
+def test_omega_items_per_block_are_bit_identical(monkeypatch, ipb):
+    """AARMVS_OMEGA_IPB sets how many consecutive (plane) items of one (tile, view) an
+    omega_conv block walks (default: 4, fewer on small grids).  The items' arithmetic is
+    unchanged, so the sweep must be bit-identical; D = 6 leaves a ragged last block."""
+    B, N, H, W, D = 2, 3, 64, 96, 6
+    sc = syn.scene(B, N, H, W, D, seed=11)
+    feats = torch.from_numpy(sc["features"]).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    sw = _sweep_obj(2)
+    args = (feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+            [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]))
+    a = sw(*args, want_cost=True, debug=True)
+    monkeypatch.setenv("AARMVS_OMEGA_IPB", ipb)
+    b = sw(*args, want_cost=True, debug=True)
+    for k in ("cost", "slice", "omega", "depth", "conf"):
+        assert torch.equal(a[k], b[k]), k
+
+
 def test_two_stream_schedule_is_bit_identical():
     """The omega pipeline of plane d+1 on a second stream (the default) against the
     single-stream schedule: same kernels, same inputs, so bit-identical outputs; a
