@@ -262,10 +262,14 @@ __global__ void __launch_bounds__(256) pack_cell_h3_kernel(const float* __restri
     const int mt = rest % mt_n, tap = (rest / mt_n) % 9, c = rest / (mt_n * 9);
     const int r = l & 31, h = l >> 5;
     const int co = (r >> 3) * hid + 8 * mt + (r & 7);
-    const int ci = 16 * c + 8 * h + j;
-    // taps with (tap + chunk) odd negated: the cells' sign-balanced accumulation (convlstm.hip)
+    // a chunk of 8 valid channels is paired (convlstm.hip h3_mfma_chunk): its slot s < 5 holds
+    // tap 2s (K half 0) and tap 2s+1 (K half 1) of those channels; slots 5..8 stay zero
+    const bool paired = cin - 16 * c == 8;
+    const int tp = paired ? 2 * tap + h : tap;
+    const int ci = paired ? 16 * c + j : 16 * c + 8 * h + j;
+    // slots with (slot + chunk) odd negated: the cells' sign-balanced accumulation (convlstm.hip)
     const bool neg = ((tap + c) & 1) != 0;
-    const float v = ci < cin ? w[(co * cin + ci) * 9 + tap] * sc : 0.f;
+    const float v = ci < cin && tp < 9 ? w[(co * cin + ci) * 9 + tp] * sc : 0.f;
     const _Float16 vh = (_Float16)v, vl = (_Float16)(v - (float)vh);
     hip[i] = vh;
     lop[i] = vl;

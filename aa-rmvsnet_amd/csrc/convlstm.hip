@@ -218,6 +218,8 @@ struct H3Cfg {
   static constexpr int chunk_nv(int c) {
     return D::CH[chunk_part(c)] - chunk_lc0(c) < 16 ? D::CH[chunk_part(c)] - chunk_lc0(c) : 16;
   }
+  // 8 valid channels: two taps per k-step (h3_mfma_chunk), the chunk's second half unused
+  static constexpr bool chunk_paired(int c) { return chunk_nv(c) == 8; }
 };
 
 // byte offset of (pixel p, 16-B half h) in a chunk plane
@@ -359,13 +361,47 @@ __device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], fl
 // -0.164 -> +0.001 ulp over 108 MFMAs).  BAL: the training cells only (their record is what
 // the BPTT differentiates); the inference cells accumulate every tap into acc with the
 // positive fragments (pack_cell_h3_kernel's second copy): 32 fewer accumulator registers.
+//
+// A chunk of 8 valid channels (cell 4's h4 part) is "paired": its k-step s takes tap 2s in the
+// K half of lanes 0-31 and tap 2s+1 in the K half of lanes 32-63 (the weights packed to match,
+// pack_cell_h3_kernel), so the chunk costs 5 k-steps instead of 9 with a zero K half each;
+// tap 9 of step 4 is a zero weight against tap 8's pixels.
 template <class C, int CH, bool PIPE = false, bool BAL = true, int ONCE = 0>
 __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], floatx16 (&accn)[C::MT][C::RW],
                                               const char* wl_hi, const char* wl_lo, const char* in_hi,
                                               const char* in_lo, int wave, int lane) {
   constexpr int MT = C::MT, RW = C::RW;
   const int col = lane & 31, h = lane >> 5;
-  if constexpr (PIPE) {
+  if constexpr (C::chunk_paired(CH)) {
+    // (PIPE ignored: the plain fragment schedule.)  The lane's tap offsets are recomputed here
+    // rather than hoisted out of the tile loop (5 live VGPRs: the training cell spilled)
+    int hv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(hv) : "v"(h));
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      const int tap = min(2 * s + hv, 8);
+      half8 bh[RW], bl[RW];
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const int boff = h3_pix((wave * RW + r + tap / 3) * C::W2 + col + tap % 3, 0);
+        bh[r] = *reinterpret_cast<const half8*>(in_hi + boff);
+        bl[r] = *reinterpret_cast<const half8*>(in_lo + boff);
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int aoff = ((((CH * 9 + s) * MT + m) * 64) + lane) * 16;
+        const half8 ah = *reinterpret_cast<const half8*>(wl_hi + aoff);
+        const half8 al = *reinterpret_cast<const half8*>(wl_lo + aoff);
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          floatx16& d = (BAL && ((s + CH) & 1)) ? accn[m][r] : acc[m][r];
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[r], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[r], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[r], d, 0, 0, 0);
+        }
+      }
+    }
+  } else if constexpr (PIPE) {
     half8 bh[2][RW], bl[2][RW], ah[2][MT], al[2][MT];
     auto fetch = [&](int tap, int s) {
       if ((ONCE & 2) && tap > 0) {   // microbenchmark ablation: B fragments of tap 0 only
