@@ -823,6 +823,15 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       rf0 = ld_c8(rref, rpix, 2 * c + 2, HW);
       rf1 = ld_c8(rref, rpix, 2 * c + 3, HW);
     }
+    // this chunk's B fragments, issued before the barrier: their L1/L2 latency is hidden
+    // behind it and the centre-tap chain (2.5% of the kernel against loading them after;
+    // DMA'ing all 12 to LDS once per item instead was 1.8%)
+    half8 Bd, Bl, Bl2;
+    if constexpr ((ABL & 128) == 0) {
+      Bd = owm[(c * 3 + 0) * 64 + lane];
+      Bl = owm[(c * 3 + 1) * 64 + lane];
+      Bl2 = owm[(c * 3 + 2) * 64 + lane];
+    }
     if (!DB) {
       __syncthreads();   // every lane's box reads of chunk c are done
       if (c < 3) stage(c + 1);
@@ -872,15 +881,10 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     }
     const half8 A0 = __builtin_bit_cast(half8, u32x4{hw[0], hw[1], hw[2], hw[3]});
     const half8 A1 = __builtin_bit_cast(half8, u32x4{lw[0], lw[1], lw[2], lw[3]});
-    half8 Bd, Bl, Bl2;
     if constexpr ((ABL & 128) != 0) {
       Bd = A1;
       Bl = A0;
       Bl2 = A1;
-    } else {
-      Bd = owm[(c * 3 + 0) * 64 + lane];
-      Bl = owm[(c * 3 + 1) * 64 + lane];
-      Bl2 = owm[(c * 3 + 2) * 64 + lane];
     }
     if (!(ABL & 1)) {
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, acc0, 0, 0, 0);
