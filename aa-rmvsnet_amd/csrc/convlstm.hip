@@ -928,12 +928,19 @@ __global__ void __launch_bounds__(256) deconv_px2_kernel(const float* __restrict
 // input (lane: pixel l & 31, channels 8 (l >> 5) .. +7, 32 contiguous bytes).  Block: 4
 // waves x 2 rows = the 8 x 32 input tile of deconv_px2 (same GN partial grid).
 typedef _Float16 dhalf8 __attribute__((ext_vector_type(8)));
+// The 12 A fragments sit in LDS (12 KB per block, read per use) rather than in 48 VGPRs per
+// lane, and a wave issues the loads of its two rows' three input rows (the middle one shared:
+// 6 pixel loads instead of 8) before any MFMA, keeping them fp32 and splitting each just
+// before use: 4 waves per SIMD instead of 3, 40 vs 48.6 us (deconv_1) and 16 vs 17.6 us
+// (deconv_0) per plane at the headline against the round-4 form (A fragments in registers,
+// each row's loads just before its MFMAs), bit-identical.
 template <int ABL = 0>
-__global__ void __launch_bounds__(256) deconv_mfma_kernel(const float* __restrict__ in,
-                                                          const float* __restrict__ wfrag,
-                                                          const float* __restrict__ bias, int Hi,
-                                                          int Wi, float* __restrict__ out,
-                                                          double* __restrict__ gn_part) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) deconv_mfma_kernel(const float* __restrict__ in,
+                                                           const float* __restrict__ wfrag,
+                                                           const float* __restrict__ bias, int Hi,
+                                                           int Wi, float* __restrict__ out,
+                                                           double* __restrict__ gn_part) {
+  __shared__ dhalf8 afs[12 * 64];
   __shared__ double red[4 * 4];
   const int b = blockIdx.z, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int x0 = blockIdx.x * kDpTW;
@@ -941,22 +948,27 @@ __global__ void __launch_bounds__(256) deconv_mfma_kernel(const float* __restric
   const int Wo = 2 * Wi;
   const float* ib = in + (size_t)b * 16 * Hi * Wi;
   const dhalf8* af = reinterpret_cast<const dhalf8*>(wfrag);
-  dhalf8 ah[6], al[6];
-#pragma unroll
-  for (int p = 0; p < 6; ++p) {
-    ah[p] = af[(p * 2 + 0) * 64 + lane];
-    al[p] = af[(p * 2 + 1) * 64 + lane];
-  }
+  for (int i = tid; i < 12 * 64; i += 256) afs[i] = af[i];
   const float inv = wfrag[6 * 2 * 64 * 8 / 2] * (1.0f / 16384.0f);
-  // B fragments of input pixel (y, x): channels 8 hh .. +7, x 2^14, split (zero outside)
-  auto bfrag = [&](int y, int x, dhalf8& bh, dhalf8& bl) {
-    float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
-    if (!(ABL & 4) && y < Hi && x < Wi) {
-      const float4* s = reinterpret_cast<const float4*>(ib + ((size_t)y * Wi + x) * 16 + 8 * hh);
-      q0 = s[0];
-      q1 = s[1];
+  const int iy0 = blockIdx.y * kDpTH + wave * 2, ix = x0 + n;
+  float4 raw[3][2][2];   // [input row iy0 + r][column ix + c][channel quad]
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
+      if (!(ABL & 4) && iy0 + r < Hi && ix + c < Wi) {
+        const float4* sp = reinterpret_cast<const float4*>(ib + ((size_t)(iy0 + r) * Wi + ix + c) * 16 + 8 * hh);
+        q0 = sp[0];
+        q1 = sp[1];
+      }
+      raw[r][c][0] = q0;
+      raw[r][c][1] = q1;
     }
-    const float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+  __syncthreads();   // A fragments in LDS
+  // B fragment of one input pixel: channels 8 hh .. +7, x 2^14, split
+  auto split = [&](const float4 (&q)[2], dhalf8& bh, dhalf8& bl) {
+    const float v[8] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float t = v[j] * 16384.0f;
@@ -967,52 +979,52 @@ __global__ void __launch_bounds__(256) deconv_mfma_kernel(const float* __restric
   };
   double part[4] = {0.0, 0.0, 0.0, 0.0};   // fp64 GroupNorm partials (E[x^2] - E[x]^2 cancels)
   typedef float fx16 __attribute__((ext_vector_type(16)));
-#pragma unroll 1
+#pragma unroll
   for (int rr = 0; rr < 2; ++rr) {
-    const int iy = blockIdx.y * kDpTH + wave * 2 + rr;
-    if (iy >= Hi) break;
-    const int ix = x0 + n;
-    dhalf8 b00h, b00l, b01h, b01l, b10h, b10l, b11h, b11l;
-    bfrag(iy, ix, b00h, b00l);
-    bfrag(iy, ix + 1, b01h, b01l);
-    bfrag(iy + 1, ix, b10h, b10l);
-    bfrag(iy + 1, ix + 1, b11h, b11l);
-    fx16 a01, a23;
+    const int iy = iy0 + rr;
+    if (iy < Hi) {
+      dhalf8 b00h, b00l, b01h, b01l, b10h, b10l, b11h, b11l;
+      split(raw[rr][0], b00h, b00l);
+      split(raw[rr][1], b01h, b01l);
+      split(raw[rr + 1][0], b10h, b10l);
+      split(raw[rr + 1][1], b11h, b11l);
+      fx16 a01, a23;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) a01[r] = a23[r] = 0.f;
-    if (!(ABL & 2)) {
-      auto mm = [&](fx16 acc, int p, dhalf8 bh, dhalf8 bl) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[p], bh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[p], bl, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[p], bh, acc, 0, 0, 0);
-        return acc;
-      };
-      a01 = mm(a01, 0, b00h, b00l);
-      a01 = mm(a01, 1, b01h, b01l);
-      a23 = mm(a23, 2, b00h, b00l);
-      a23 = mm(a23, 3, b01h, b01l);
-      a23 = mm(a23, 4, b10h, b10l);
-      a23 = mm(a23, 5, b11h, b11l);
-    }
-    if (ix < Wi) {
-      float* ob = out + (size_t)b * 16 * 4 * Hi * Wi;
-      // D row m = (r & 3) + 8 (r >> 2) + 4 hh: slot r >> 3, channels 4 hh + 8 ((r >> 2) & 1) + (r & 3)
+      for (int r = 0; r < 16; ++r) a01[r] = a23[r] = 0.f;
+      if (!(ABL & 2)) {
+        auto mm = [&](fx16 acc, int p, dhalf8 bh, dhalf8 bl) {
+          const dhalf8 ah = afs[(p * 2 + 0) * 64 + lane], al = afs[(p * 2 + 1) * 64 + lane];
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
+          return acc;
+        };
+        a01 = mm(a01, 0, b00h, b00l);
+        a01 = mm(a01, 1, b01h, b01l);
+        a23 = mm(a23, 2, b00h, b00l);
+        a23 = mm(a23, 3, b01h, b01l);
+        a23 = mm(a23, 4, b10h, b10l);
+        a23 = mm(a23, 5, b11h, b11l);
+      }
+      if (ix < Wi) {
+        float* ob = out + (size_t)b * 16 * 4 * Hi * Wi;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {   // r = 4 g .. 4 g + 3
-        const int slot = g >> 1, c0 = 4 * hh + 8 * (g & 1), grp = g & 1;
+        for (int g = 0; g < 4; ++g) {
+          const int slot = g >> 1, c0 = 4 * hh + 8 * (g & 1), grp = g & 1;
 #pragma unroll
-        for (int acc_i = 0; acc_i < 2; ++acc_i) {
-          const fx16& A = acc_i ? a23 : a01;
-          const int oy = 2 * iy + acc_i, ox = 2 * ix + slot;
-          float v4[4];
+          for (int acc_i = 0; acc_i < 2; ++acc_i) {
+            const fx16& A = acc_i ? a23 : a01;
+            const int oy = 2 * iy + acc_i, ox = 2 * ix + slot;
+            float v4[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            v4[u] = fmaf(A[4 * g + u], inv, bias[c0 + u]);
-            part[2 * grp] += (double)v4[u];
-            part[2 * grp + 1] += (double)v4[u] * v4[u];
+            for (int u = 0; u < 4; ++u) {
+              v4[u] = fmaf(A[4 * g + u], inv, bias[c0 + u]);
+              part[2 * grp] += (double)v4[u];
+              part[2 * grp + 1] += (double)v4[u] * v4[u];
+            }
+            float4* d = reinterpret_cast<float4*>(ob + ((size_t)oy * Wo + ox) * 16 + c0);
+            if (!(ABL & 1) || v4[0] == 1234.5f) *d = make_float4(v4[0], v4[1], v4[2], v4[3]);
           }
-          float4* d = reinterpret_cast<float4*>(ob + ((size_t)oy * Wo + ox) * 16 + c0);
-          if (!(ABL & 1) || v4[0] == 1234.5f) *d = make_float4(v4[0], v4[1], v4[2], v4[3]);
         }
       }
     }
@@ -1066,48 +1078,58 @@ hipError_t launch_wta_update(const float* cost, const float* depth_d, float* max
   return hipGetLastError();
 }
 
+// The haloed h4 tile sits in LDS pixel-major (32 B per pixel, the NHWC layout): a pixel's 9
+// taps are 18 ds_read_b128 (the fma order stays channel-major, tap-minor), the staging 2 16-B
+// stores per pixel (27.8 vs 28.8 us per plane at the headline against a channel-major tile
+// read by 72 scalar LDS loads; bit-identical).
 __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__ h4,
-                                                       const float* __restrict__ w,
-                                                       const float* __restrict__ bias, int H,
-                                                       int W, const float* __restrict__ dvals,
-                                                       int d, int D, float* __restrict__ cost_out,
-                                                       int wta, float* __restrict__ max_prob,
-                                                       float* __restrict__ exp_sum,
-                                                       float* __restrict__ depth,
-                                                       double* __restrict__ zero_stats,
-                                                       int zero_n) {
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bias, int H,
+                                                        int W, const float* __restrict__ dvals,
+                                                        int d, int D, float* __restrict__ cost_out,
+                                                        int wta, float* __restrict__ max_prob,
+                                                        float* __restrict__ exp_sum,
+                                                        float* __restrict__ depth,
+                                                        double* __restrict__ zero_stats,
+                                                        int zero_n) {
 #pragma clang fp contract(off)
-  // the select arithmetic of drmvsnet.py:328-333 is reproduced op for op
-  __shared__ float t[8][kHeadTH + 2][kHeadTW + 2];
-  // the plane's U-Net GroupNorm statistics are consumed: clear them for the next plane
+  constexpr int TW2 = kHeadTW + 2, NPX = (kHeadTH + 2) * TW2;
+  __shared__ float4 t[NPX][2];
   if (zero_stats && blockIdx.x == 0 && blockIdx.y == 0)
     for (int i = threadIdx.x; i < zero_n; i += blockDim.x) zero_stats[i] = 0.0;
   const int b = blockIdx.y, HW = H * W;
   const int tiles_x = (W + kHeadTW - 1) / kHeadTW;
   const int y0 = (blockIdx.x / tiles_x) * kHeadTH, x0 = (blockIdx.x % tiles_x) * kHeadTW;
   const float* hb = h4 + (size_t)b * 8 * HW;
-  // h4 tile (NHWC: 32 B per pixel) with a 1-px zero-padded halo -> LDS [ci][y][x]
-  for (int rem = threadIdx.x; rem < (kHeadTH + 2) * (kHeadTW + 2); rem += 256) {
-    const int yy = y0 - 1 + rem / (kHeadTW + 2), xx = x0 - 1 + rem % (kHeadTW + 2);
+  for (int rem = threadIdx.x; rem < NPX; rem += 256) {
+    const int yy = y0 - 1 + rem / TW2, xx = x0 - 1 + rem % TW2;
     float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
     if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
       const float4* src = reinterpret_cast<const float4*>(hb + ((size_t)yy * W + xx) * 8);
       q0 = src[0];
       q1 = src[1];
     }
-    const float v8[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-#pragma unroll
-    for (int ci = 0; ci < 8; ++ci) (&t[ci][0][0])[rem] = v8[ci];
+    t[rem][0] = q0;
+    t[rem][1] = q1;
   }
   __syncthreads();
   const int ty = threadIdx.x / kHeadTW, tx = threadIdx.x % kHeadTW;
   const int y = y0 + ty, x = x0 + tx;
   if (y >= H || x >= W) return;
   const int p = y * W + x;
+  float v[9][8];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int q = (ty + tap / 3) * TW2 + tx + tap % 3;
+    const float4 a0 = t[q][0], a1 = t[q][1];
+    v[tap][0] = a0.x; v[tap][1] = a0.y; v[tap][2] = a0.z; v[tap][3] = a0.w;
+    v[tap][4] = a1.x; v[tap][5] = a1.y; v[tap][6] = a1.z; v[tap][7] = a1.w;
+  }
   float acc = 0.f;
+#pragma unroll
   for (int ci = 0; ci < 8; ++ci)
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) acc = fmaf(t[ci][ty + tap / 3][tx + tap % 3], w[ci * 9 + tap], acc);
+    for (int tap = 0; tap < 9; ++tap) acc = fmaf(v[tap][ci], w[ci * 9 + tap], acc);
   const float cost = acc + bias[0];
   if (cost_out) cost_out[((size_t)b * D + d) * HW + p] = cost;
   if (wta) {
