@@ -48,9 +48,13 @@ __device__ __forceinline__ int scale_exp(unsigned bits) {
   return ilogbf(m) - 14;
 }
 
-__device__ __forceinline__ void split16(float v, _Float16& hi, _Float16& lo) {
-  hi = (_Float16)v;
-  lo = (_Float16)(v - (float)hi);
+// a pair (a, b) split the same way: the hi pair as one v_cvt_pk_f16_f32 read back for the lo
+// parts (6 instructions per pair instead of 8 for two split16)
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split16x2(float a, float b, half2v& hi, half2v& lo) {
+  hi = __builtin_convertvector((float2v){a, b}, half2v);
+  lo = __builtin_convertvector((float2v){a - (float)hi[0], b - (float)hi[1]}, half2v);
 }
 
 // max |v| of a wave folded into *dst (float bits: non-negative floats order as unsigned)
@@ -409,11 +413,13 @@ __global__ void __launch_bounds__(512) dgrad_kernel(DgradArgs a) {
       const float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
       bhalf8 hv, lv;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        _Float16 hi, lo;
-        split16(v[k] * zs, hi, lo);
-        hv[k] = hi;
-        lv[k] = lo;
+      for (int k = 0; k < 8; k += 2) {
+        half2v hi, lo;
+        split16x2(v[k] * zs, v[k + 1] * zs, hi, lo);
+        hv[k] = hi[0];
+        hv[k + 1] = hi[1];
+        lv[k] = lo[0];
+        lv[k + 1] = lo[1];
       }
       *reinterpret_cast<bhalf8*>(in_hi + dg_pix(p, hh)) = hv;
       *reinterpret_cast<bhalf8*>(in_lo + dg_pix(p, hh)) = lv;
@@ -775,10 +781,6 @@ constexpr size_t wgrad2_lds() {
   return (size_t)2 * CZ * kW2ZS * 2 + (size_t)2 * NCH * 16 * kW2IS * 2;
 }
 
-__device__ __forceinline__ unsigned pack_h2(_Float16 a, _Float16 b) {
-  return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
-}
-
 template <int CZ, int NCH>
 __global__ void __launch_bounds__(512) wgrad2_kernel(WgradArgs a) {
   constexpr int MT = CZ / 16, NS = 8 / MT;
@@ -920,12 +922,11 @@ __global__ void __launch_bounds__(512) wgrad2_kernel(WgradArgs a) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         bacc[i] += v0[i] + v1[i];
-        _Float16 h0, l0, h1, l1;
-        split16(v0[i] * zsg, h0, l0);
-        split16(v1[i] * zsg, h1, l1);
+        half2v hp, lp;
+        split16x2(v0[i] * zsg, v1[i] * zsg, hp, lp);
         const int o = (8 * zcg + i) * kW2ZS + zr * 32 + zx;
-        *reinterpret_cast<unsigned*>(zt + o) = pack_h2(h0, h1);
-        *reinterpret_cast<unsigned*>(zt + CZ * kW2ZS + o) = pack_h2(l0, l1);
+        *reinterpret_cast<unsigned*>(zt + o) = __builtin_bit_cast(unsigned, hp);
+        *reinterpret_cast<unsigned*>(zt + CZ * kW2ZS + o) = __builtin_bit_cast(unsigned, lp);
       }
     }
     if (irole) {
@@ -975,12 +976,11 @@ __global__ void __launch_bounds__(512) wgrad2_kernel(WgradArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          _Float16 h0, l0, h1, l1;
-          split16(v[0][i] * usc, h0, l0);
-          split16(v[1][i] * usc, h1, l1);
+          half2v hp, lp;
+          split16x2(v[0][i] * usc, v[1][i] * usc, hp, lp);
           const int o = (16 * c + 8 * hh + i) * kW2IS + rr * kW2RL + 6 + 2 * cp;
-          *reinterpret_cast<unsigned*>(it + o) = pack_h2(h0, h1);
-          *reinterpret_cast<unsigned*>(it + CIN * kW2IS + o) = pack_h2(l0, l1);
+          *reinterpret_cast<unsigned*>(it + o) = __builtin_bit_cast(unsigned, hp);
+          *reinterpret_cast<unsigned*>(it + CIN * kW2IS + o) = __builtin_bit_cast(unsigned, lp);
         }
         __builtin_amdgcn_sched_barrier(0);   // one half's values live at a time
       }
