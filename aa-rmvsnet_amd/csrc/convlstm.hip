@@ -95,6 +95,7 @@ struct CellArgs {
   const float* bias;    // [4*hid]
   const unsigned* xbound;   // cell 0: float bits of a bound on |x| (fp16 range guard), or null
   int B, H, W;          // cell resolution
+  int skew;             // double-buffered kernel: waves with bit skew-1 set stage first (0: none)
 };
 
 // Staging scales of the split-fp16 operands.  An fp32 value a is staged as fp16 hi + lo with
@@ -148,6 +149,7 @@ struct CellDef<0> {   // [x, h0] @ H
   static constexpr int HID = 16;
   static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1, H3PIPE = 1;
   static constexpr int MIN_WAVES = 1;   // amdgpu_waves_per_eu lower bound (register budget)
+  static constexpr int SKEW = 3;        // CellArgs::skew of the double-buffered kernel
 };
 template <>
 struct CellDef<1> {   // [maxpool(h0'), h1] @ H/2
@@ -156,6 +158,7 @@ struct CellDef<1> {   // [maxpool(h0'), h1] @ H/2
   static constexpr int HID = 16;
   static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1, H3PIPE = 1;
   static constexpr int MIN_WAVES = 1;
+  static constexpr int SKEW = 2;
 };
 template <>
 struct CellDef<2> : CellDef<1> {};   // [maxpool(h1'), h2] @ H/4
@@ -166,6 +169,7 @@ struct CellDef<3> {   // [gnrelu(u0), h1', h3] @ H/2
   static constexpr int HID = 16;
   static constexpr int H3RW = 1, H3WAVES = 8, H3DB = AARMVS_C3DB, H3PIPE = 1;
   static constexpr int MIN_WAVES = 1;
+  static constexpr int SKEW = 0;
 };
 template <>
 struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
@@ -176,6 +180,7 @@ struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
   // <= 128 VGPRs: two 512-thread blocks per CU (the sign-balanced accumulator pair took the
   // compiler's choice to 130, one block per CU: 160 -> 202 us per plane at the headline)
   static constexpr int MIN_WAVES = 4;
+  static constexpr int SKEW = 0;
 };
 
 // ---------------------------------------------------------------------------
@@ -706,6 +711,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
   __syncthreads();
   int par = 0;
   const int hi = lane >> 5, col = lane & 31;
+  const bool early = a.skew > 0 && ((wave >> (a.skew - 1)) & 1) != 0;
   for (; tile < ntiles; tile += gridDim.x) {
     coords(tile, b, y0, x0);
     const int next = tile + (int)gridDim.x;
@@ -730,15 +736,26 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
       constexpr int AC = A_NEXT ? CH + 2 - NCHK : CH + 2;
       const char* cur = inb + 2 * par * PB;
       char* oth = inb + 2 * (par ^ 1) * PB;
+      auto stage = [&] {
+        if (!(ABL & 2)) {
+          if (!F_NEXT || next < ntiles) st.template store<F>(oth, oth + PB, gn, tid, 0, W);
+          if (!A_NEXT)
+            st.template load<AC>(a, b, y0, x0, tid);
+          else if (next < ntiles)
+            st.template load<AC>(a, nb, ny0, nx0, tid);
+        }
+      };
+      // The step's barrier aligns every wave's phases, so a SIMD's two waves would stage (VALU)
+      // and run their MFMAs at the same times.  With a.skew = k > 0 the waves with bit k-1 of
+      // their index set (half of them) stage before their MFMAs and the others after, so that
+      // staging overlaps MFMAs on a SIMD shared by one wave of each half (which bit pairs the
+      // waves that way is measured per cell: CellDef::SKEW).  Buffer `oth` is free from the
+      // start of the step (last read by the previous step's MFMAs, before its barrier), so
+      // either order is safe and the results are the same.
+      if (early) stage();
       xguard_rescale<C, KIND, CH, PRECISE>(acc, accn, xr);
       if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE, (ABL >> 3) & 3>(acc, accn, wl_hi, wl_lo, cur, cur + PB, wave, lane);
-      if (!(ABL & 2)) {
-        if (!F_NEXT || next < ntiles) st.template store<F>(oth, oth + PB, gn, tid, 0, W);
-        if (!A_NEXT)
-          st.template load<AC>(a, b, y0, x0, tid);
-        else if (next < ntiles)
-          st.template load<AC>(a, nb, ny0, nx0, tid);
-      }
+      if (!early) stage();
       if constexpr (CH == NCHK - 1) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
@@ -776,13 +793,23 @@ static hipError_t run_cell_h3_(const CellArgs& a, const float* inv_scale, int cu
   const int ntiles = a.B * ((a.W + C::TW - 1) / C::TW) * ((a.H + C::TH - 1) / C::TH);
   const int per_cu = std::max(1, (int)((160 * 1024) / lds));
   const int grid = std::max(1, std::min(ntiles, cu * per_cu));
+  // the staging order of the double-buffered kernel's wave halves (lstm_cell_h3db_kernel): per
+  // cell the wave bit measured fastest at the headline (tools/gpu_envsets_ab.sh over
+  // AARMVS_CELL_SKEW = 0..3: cell 0 311 -> 296 us with bit 2, cell 1 100.5 -> 91.3 with bit 1,
+  // cell 2 29.3 -> 28.5; bit-identical); AARMVS_CELL_SKEW overrides it for every cell
+  static const int skew_env = [] {
+    const char* e = std::getenv("AARMVS_CELL_SKEW");
+    return (e && *e) ? std::atoi(e) : -1;
+  }();
+  CellArgs ak = a;
+  ak.skew = skew_env >= 0 ? skew_env : CellDef<KIND>::SKEW;
   ProfScope ps(s, kid);
   if (DB)
     hipLaunchKernelGGL((lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE>), dim3(grid),
-                       dim3(C::THREADS), lds, s, a, inv_scale);
+                       dim3(C::THREADS), lds, s, ak, inv_scale);
   else
     hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE>), dim3(grid),
-                       dim3(C::THREADS), lds, s, a, inv_scale);
+                       dim3(C::THREADS), lds, s, ak, inv_scale);
   return hipGetLastError();
 }
 // The training sweep (a.z_out set: the record for the BPTT) runs the unbiased gate activations
