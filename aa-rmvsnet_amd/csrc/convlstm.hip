@@ -134,10 +134,16 @@ template <int KIND>
 struct CellDef;
 // (A/B builds only: the staging variant of cells 3 and 4; the library uses the defaults)
 #ifndef AARMVS_C3DB
-#define AARMVS_C3DB 0
+#define AARMVS_C3DB 1
 #endif
 #ifndef AARMVS_C4DB
 #define AARMVS_C4DB 0
+#endif
+#ifndef AARMVS_C3SKEW
+#define AARMVS_C3SKEW 3
+#endif
+#ifndef AARMVS_C4SKEW
+#define AARMVS_C4SKEW 0
 #endif
 #ifndef AARMVS_C4PIPE
 #define AARMVS_C4PIPE 0
@@ -169,7 +175,7 @@ struct CellDef<3> {   // [gnrelu(u0), h1', h3] @ H/2
   static constexpr int HID = 16;
   static constexpr int H3RW = 1, H3WAVES = 8, H3DB = AARMVS_C3DB, H3PIPE = 1;
   static constexpr int MIN_WAVES = 1;
-  static constexpr int SKEW = 0;
+  static constexpr int SKEW = AARMVS_C3SKEW;
 };
 template <>
 struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
@@ -180,7 +186,7 @@ struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
   // <= 128 VGPRs: two 512-thread blocks per CU (the sign-balanced accumulator pair took the
   // compiler's choice to 130, one block per CU: 160 -> 202 us per plane at the headline)
   static constexpr int MIN_WAVES = 4;
-  static constexpr int SKEW = 0;
+  static constexpr int SKEW = AARMVS_C4SKEW;
 };
 
 // ---------------------------------------------------------------------------
