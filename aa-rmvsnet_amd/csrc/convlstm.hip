@@ -784,7 +784,9 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
 // DB0/PIPE0 DB0/PIPE1 DB1/PIPE0 DB1/PIPE1): cell0 .405 .379 .352 .324, cell1 .097 .090
 // .091 .086, cell3 .087 .082 .083 .082, cell4 .155 .170 .208 .193 (cell 4's second
 // buffer or second fragment set costs it a block per CU).  A warp-specialised form (4
-// staging waves beside the 8 MFMA waves) measured slower (cell 0 0.43 vs 0.40 ms).
+// staging waves beside the 8 MFMA waves) measured slower (cell 0 0.43 vs 0.40 ms).  Round 5:
+// with the double-buffered kernel's wave halves skewed (CellDef::SKEW) cell 3 is faster
+// double-buffered too (95.0 -> 90.8 us per plane in the sweep), cell 4 still is not (161 -> 200).
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
           int DB = CellDef<KIND>::H3DB, int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false>
 static hipError_t run_cell_h3_(const CellArgs& a, const float* inv_scale, int cu, int kid,
