@@ -805,10 +805,8 @@ static hipError_t run_cell_h3_(const CellArgs& a, const float* inv_scale, int cu
   // cell the wave bit measured fastest at the headline (tools/gpu_envsets_ab.sh over
   // AARMVS_CELL_SKEW = 0..3: cell 0 311 -> 296 us with bit 2, cell 1 100.5 -> 91.3 with bit 1,
   // cell 2 29.3 -> 28.5; bit-identical); AARMVS_CELL_SKEW overrides it for every cell
-  static const int skew_env = [] {
-    const char* e = std::getenv("AARMVS_CELL_SKEW");
-    return (e && *e) ? std::atoi(e) : -1;
-  }();
+  const char* skew_s = std::getenv("AARMVS_CELL_SKEW");   // read per launch (tests switch it)
+  const int skew_env = (skew_s && *skew_s) ? std::atoi(skew_s) : -1;
   CellArgs ak = a;
   ak.skew = skew_env >= 0 ? skew_env : CellDef<KIND>::SKEW;
   ProfScope ps(s, kid);

@@ -218,6 +218,25 @@ def test_omega_items_per_block_are_bit_identical(monkeypatch, ipb):
         assert torch.equal(a[k], b[k]), k
 
 
+@pytest.mark.parametrize("skew", ["0", "1", "2", "3"])
+def test_cell_wave_skew_is_bit_identical(monkeypatch, skew):
+    """AARMVS_CELL_SKEW picks which half of the double-buffered cells' waves stages before its
+    MFMAs (default: per cell, CellDef::SKEW).  Only the order of independent work changes, so
+    the sweep must be bit-identical to the default for every setting."""
+    B, N, H, W, D = 1, 3, 72, 100, 3
+    sc = syn.scene(B, N, H, W, D, seed=13)
+    feats = torch.from_numpy(sc["features"]).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    sw = _sweep_obj(3)
+    args = (feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+            [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]))
+    a = sw(*args, want_cost=True)
+    monkeypatch.setenv("AARMVS_CELL_SKEW", skew)
+    b = sw(*args, want_cost=True)
+    for k in ("cost", "depth", "conf"):
+        assert torch.equal(a[k], b[k]), k
+
+
 def test_two_stream_schedule_is_bit_identical():
     """The omega pipeline of plane d+1 on a second stream (the default) against the
     single-stream schedule: same kernels, same inputs, so bit-identical outputs; a
