@@ -254,7 +254,7 @@ __device__ __forceinline__ uint32_t h3_split2(float a, float b, uint32_t& lo_bit
 // each LDS plane as ONE 16-B store (8 channels as fp16 pairs) at h3_pix(p, h): 2-way bank
 // conflicts at most.  Out-of-image pixels and channels past the chunk's valid count load
 // zeros through the buffer range check.  NTH: staging threads (default: the block).
-template <int KIND, int RW, int WAVES, int NTH = 0>
+template <int KIND, int RW, int WAVES, int NTH = 0, bool PAIRSKIP = false>
 struct H3PixStager {
   using C = H3Cfg<KIND, RW, WAVES>;
   using D = typename C::D;
@@ -282,6 +282,8 @@ struct H3PixStager {
     for (int j = 0; j < NI; ++j) {
       const int e = tid + j * TH;
       const int h = e >= C::NPIX ? 1 : 0, p = e - h * C::NPIX;
+      // PAIRSKIP: a paired chunk's second half is never read (h3_mfma_chunk): no loads
+      if (PAIRSKIP && C::chunk_paired(CH) && h) continue;
       const int row = p / C::W2, col = p - row * C::W2;
       const int gy = y0 - 1 + row, gx = x0 - 1 + col;
       const bool in = e < NITEM && 8 * h < NV && gy >= 0 && gy < H && gx >= 0 && gx < W;
@@ -315,6 +317,7 @@ struct H3PixStager {
       const int e = tid + j * TH;
       if (e < NITEM) {
         const int h = e >= C::NPIX ? 1 : 0, p = e - h * C::NPIX;
+        if (PAIRSKIP && C::chunk_paired(CH) && h) continue;   // (and no stores)
         const bool in = in_mask & (1u << j);
         float v[8];
 #pragma unroll
@@ -602,7 +605,9 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
     y0 = (rem / tiles_x) * C::TH;
     x0 = (rem % tiles_x) * C::TW;
   };
-  H3PixStager<KIND, RW, WAVES> st;
+  // the inference cells skip a paired chunk's unused half; the training cells (PRECISE) keep
+  // the uniform staging loop (skipping it costs the 128-VGPR cell 4 spills there)
+  H3PixStager<KIND, RW, WAVES, 0, !PRECISE> st;
   const int xe = KIND == 0 ? xguard_exp(a.xbound)
                  : D::MODE[0] == SRC_GNRELU ? gguard_exp(a.part[0].gamma, a.part[0].beta, H, W) : 0;
   st.xs = ldexpf(1.0f, -xe);
