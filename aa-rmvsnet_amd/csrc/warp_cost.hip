@@ -11,6 +11,7 @@
 // statistic reduced in a fixed order), then one cost_x launch writing the group's slices.
 #include <hip/hip_runtime.h>
 
+#include <cfloat>
 #include <climits>
 #include <cstdlib>
 #include <cstring>
@@ -116,12 +117,18 @@ hipError_t launch_homo_warp(const float* src, const float* rel, const float* dep
 // taps, many reference pixels into one source pixel.  fp32 atomics would make each sum depend on
 // the order the atomics are served in, so the sums are formed in 64-bit fixed point instead
 // (integer adds are associative: bit-reproducible), as the sweep's own dL/dsrc (cbw_feat):
-//   1. warp_bwd_max: max |grad_out| per batch element (float bits, order-independent max);
+//   1. warp_bwd_max: max |grad_out| per batch element (float bits, order-independent max; a NaN
+//      counts as +inf);
 //   2. warp_bwd_scatter: each contribution wt * g scaled by 2^k_b (exact) and rounded to an
 //      integer, k_b such that any source pixel's total (<= HW max|g|: the bilinear weights of
 //      one reference pixel sum to <= 1) stays below 2^61; quantum 2^-k_b ~ HW max|g| 2^-62;
 //   3. warp_bwd_fold: grad_src += (float)(sum 2^-k_b), one rounding.
-// Workspace: [B] exponents' source words + [B][C][HW] int64 accumulators (zeroed here).
+// A batch element whose grad_out holds a NaN or an infinity has no fixed-point scale: its
+// contributions go to grad_src as fp32 atomics, which carry the NaN / infinity to exactly the
+// source pixels grid_sample's backward carries them to, and leave the others finite (not
+// bit-reproducible, like the reference's own scatter); the fold skips it.
+// Batch elements are processed 64 at a time.  Workspace: 64 exponents' source words (256 B) +
+// [min(B, 64)][C][HW] int64 accumulators (zeroed here per chunk of batch elements).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) warp_bwd_max_kernel(const float* __restrict__ gout, size_t n_per_b,
                                                            unsigned* __restrict__ gmax) {
@@ -137,11 +144,16 @@ __global__ void __launch_bounds__(256) warp_bwd_max_kernel(const float* __restri
     atomicMax(gmax + b, (unsigned)w);
 }
 
-__device__ __forceinline__ int warp_bwd_exp(unsigned maxbits, int HW) {
-  const double tot = (double)__uint_as_float(maxbits) * (double)HW;
-  if (!(tot > 0.0) || !(tot < 1e300)) return 0;
-  const int k = 61 - ilogb(tot) - 1;
-  return k > 120 ? 120 : (k < -120 ? -120 : k);
+// the fixed-point exponent of a batch element; false: its grad_out is not finite
+__device__ __forceinline__ bool warp_bwd_exp(unsigned maxbits, int HW, int& k) {
+  const float mx = __uint_as_float(maxbits);
+  k = 0;
+  if (!(mx <= FLT_MAX)) return false;
+  const double tot = (double)mx * (double)HW;
+  if (!(tot > 0.0)) return true;
+  const int kk = 61 - ilogb(tot) - 1;
+  k = kk > 120 ? 120 : (kk < -120 ? -120 : kk);
+  return true;
 }
 
 __global__ void __launch_bounds__(256) homo_warp_bwd_kernel(const float* __restrict__ gout,
@@ -149,25 +161,32 @@ __global__ void __launch_bounds__(256) homo_warp_bwd_kernel(const float* __restr
                                                             const float* __restrict__ depth,
                                                             const unsigned* __restrict__ gmax,
                                                             int C, int H, int W,
-                                                            unsigned long long* __restrict__ acc) {
+                                                            unsigned long long* __restrict__ acc,
+                                                            float* __restrict__ gsrc) {
   const int b = blockIdx.y;
   const int HW = H * W;
   const float* m = rel + 12 * b;
   const float dep = depth[b];
-  const int k = warp_bwd_exp(gmax[b], HW);
+  int k;
+  const bool fixed = warp_bwd_exp(gmax[b], HW, k);
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
     float ix, iy;
     sample_pos(m, dep, (float)(p % W), (float)(p / W), H, W, ix, iy);
     const Taps t = make_taps(ix, iy, H, W);
     const float* g = gout + (size_t)b * C * HW + p;
     unsigned long long* s = acc + (size_t)b * C * HW;
+    float* gs = gsrc + (size_t)b * C * HW;
     for (int c = 0; c < C; ++c) {
       const float gv = g[(size_t)c * HW];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         if (t.ok[q]) {
-          const long long f = (long long)rint(ldexp((double)(t.wt[q] * gv), k));
-          if (f != 0) atomicAdd(s + (size_t)c * HW + t.idx[q], (unsigned long long)f);
+          if (fixed) {
+            const long long f = (long long)rint(ldexp((double)(t.wt[q] * gv), k));
+            if (f != 0) atomicAdd(s + (size_t)c * HW + t.idx[q], (unsigned long long)f);
+          } else {
+            atomicAdd(gs + (size_t)c * HW + t.idx[q], t.wt[q] * gv);
+          }
         }
     }
   }
@@ -177,7 +196,8 @@ __global__ void __launch_bounds__(256) warp_bwd_fold_kernel(const unsigned long 
                                                             const unsigned* __restrict__ gmax, size_t n_per_b,
                                                             int HW, float* __restrict__ gsrc) {
   const int b = blockIdx.y;
-  const int k = warp_bwd_exp(gmax[b], HW);
+  int k;
+  if (!warp_bwd_exp(gmax[b], HW, k)) return;   // non-finite grad_out: scattered in fp32
   const unsigned long long* a = acc + (size_t)b * n_per_b;
   float* o = gsrc + (size_t)b * n_per_b;
   for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n_per_b; i += (size_t)gridDim.x * 256) {
@@ -186,28 +206,37 @@ __global__ void __launch_bounds__(256) warp_bwd_fold_kernel(const unsigned long 
   }
 }
 
+constexpr int kWarpBwdChunk = 64;   // batch elements per pass (the 256-B exponent header)
+
 size_t homo_warp_bwd_workspace_bytes(int B, int C, int H, int W) {
-  return 256 + (size_t)B * C * H * W * 8;
+  return 256 + (size_t)std::min(B, kWarpBwdChunk) * C * H * W * 8;
 }
 
 hipError_t launch_homo_warp_bwd(const float* gout, const float* rel, const float* depth, int B,
                                 int C, int H, int W, float* gsrc, void* workspace, hipStream_t s) {
   const int HW = H * W;
   const size_t nb = (size_t)C * HW;
-  if (B > 64) return hipErrorInvalidValue;   // the maxima fit the 256-B header
   unsigned* gmax = static_cast<unsigned*>(workspace);
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + 256);
   ProfScope ps(s, K_WARP);
-  hipError_t e = hipMemsetAsync(workspace, 0, homo_warp_bwd_workspace_bytes(B, C, H, W), s);
-  if (e != hipSuccess) return e;
-  const unsigned gb = (unsigned)std::min<size_t>((nb + 255) / 256, 1024);
-  hipLaunchKernelGGL(warp_bwd_max_kernel, dim3(gb, B), dim3(256), 0, s, gout, nb, gmax);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  dim3 grid((unsigned)std::min((HW + 255) / 256, 4096), (unsigned)B);
-  hipLaunchKernelGGL(homo_warp_bwd_kernel, grid, dim3(256), 0, s, gout, rel, depth, gmax, C, H, W, acc);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(warp_bwd_fold_kernel, dim3(gb, B), dim3(256), 0, s, acc, gmax, nb, HW, gsrc);
-  return hipGetLastError();
+  hipError_t e = hipSuccess;
+  for (int b0 = 0; b0 < B; b0 += kWarpBwdChunk) {
+    const int nbt = std::min(B - b0, kWarpBwdChunk);
+    if ((e = hipMemsetAsync(workspace, 0, homo_warp_bwd_workspace_bytes(nbt, C, H, W), s)) != hipSuccess)
+      return e;
+    const float* go = gout + (size_t)b0 * nb;
+    float* gsb = gsrc + (size_t)b0 * nb;
+    const unsigned gb = (unsigned)std::min<size_t>((nb + 255) / 256, 1024);
+    hipLaunchKernelGGL(warp_bwd_max_kernel, dim3(gb, nbt), dim3(256), 0, s, go, nb, gmax);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    dim3 grid((unsigned)std::min((HW + 255) / 256, 4096), (unsigned)nbt);
+    hipLaunchKernelGGL(homo_warp_bwd_kernel, grid, dim3(256), 0, s, go, rel + 12 * (size_t)b0, depth + b0,
+                       gmax, C, H, W, acc, gsb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(warp_bwd_fold_kernel, dim3(gb, nbt), dim3(256), 0, s, acc, gmax, nb, HW, gsb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return e;
 }
 
 // ---------------------------------------------------------------------------
@@ -424,8 +453,10 @@ __device__ __forceinline__ Box box_reduce(int lx, int ly, int hx, int hy, int (*
 }
 
 // row of box pixel p: umulhi(p, ceil(2^32 / nx)), exact for p, nx < 2^16
+// ceil(2^32 / nx) = floor((2^32 - 1) / nx) + 1: a 32-bit division (the 64-bit form cost ~110
+// scalar instructions per omega item)
 __device__ __forceinline__ uint32_t box_magic(int nx) {
-  return nx > 1 ? (uint32_t)((0x100000000ull + (uint64_t)nx - 1) / (uint64_t)nx) : 0u;
+  return nx > 1 ? 0xFFFFFFFFu / (uint32_t)nx + 1u : 0u;
 }
 __device__ __forceinline__ int box_row(int p, int nx, uint32_t mg) {
   return nx > 1 ? (int)__umulhi((uint32_t)p, mg) : p;
@@ -643,6 +674,7 @@ __device__ __forceinline__ int img_half(uint32_t p, int s) { return s ^ (int)((p
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef float float2_t __attribute__((ext_vector_type(2)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -698,11 +730,49 @@ constexpr int kOmegaTW = 16;   // the library's tile width
 // loads, 16 sampling positions without the homography divisions (the own pixel), 32 no Y
 // image / gather (t1 from the accumulators), 64 no statistics atomics, 128 no B-fragment loads
 // BAL: sign-balanced accumulation, for the training sweep only: +9% time
+// wave_sum_d (device_common.h) of two values at once, in the same order and so with the same
+// result, on DPP moves with an undefined `old` operand: only lane 63's value is used, and every
+// lane it depends on is written at every step, so the zero fills of update_dpp are not needed
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64_u(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, ROWS, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ void wave_sum2_d(double& u, double& w) {
+  u += dpp_f64_u<0xB1, 0xF>(u);
+  w += dpp_f64_u<0xB1, 0xF>(w);
+  u += dpp_f64_u<0x4E, 0xF>(u);
+  w += dpp_f64_u<0x4E, 0xF>(w);
+  u += dpp_f64_u<0x141, 0xF>(u);
+  w += dpp_f64_u<0x141, 0xF>(w);
+  u += dpp_f64_u<0x140, 0xF>(u);
+  w += dpp_f64_u<0x140, 0xF>(w);
+  u += dpp_f64_u<0x142, 0xA>(u);
+  w += dpp_f64_u<0x142, 0xA>(w);
+  u += dpp_f64_u<0x143, 0xC>(u);
+  w += dpp_f64_u<0x143, 0xC>(w);
+  auto rl = [](double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  };
+  u = rl(u);
+  w = rl(w);
+}
+
 // one (tile, view, plane) item of omega_mfma_kernel (seq: its index in the launch's order)
+// OmegaPos: the item's tile (index, row and column of tiles), source view and plane, advanced
+// item by item by the kernel (no per-item integer divisions)
+struct OmegaPos {
+  int tile, ty, tx, v, kp;
+};
 template <int ABL, int TW, bool BAL, typename PA>
 __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
                                            const float* __restrict__ Rel,
-                                           const unsigned* __restrict__ xbound, const int seq) {
+                                           const unsigned* __restrict__ xbound, const OmegaPos ip) {
   using T = OmegaTile<TW>;
   constexpr int kMThreads = T::NT, kMBoxPx = T::BOXPX, kMOutH = T::OUTH, kMOutW = T::OUTW;
   constexpr int NB = (2 * kMBoxPx + kMThreads - 1) / kMThreads;   // box pieces per thread
@@ -718,21 +788,18 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   const int lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.z;
   const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
-  const int tile = seq / (nsrc * a.npl), vk = seq - tile * (nsrc * a.npl);
-  const int v = vk / a.npl, kp = vk - v * a.npl;
-  const int tiles_x = (W + kMOutW - 1) / kMOutW;
-  const int y0 = (tile / tiles_x) * kMOutH, x0 = (tile % tiles_x) * kMOutW;
+  const int tile = ip.tile, v = ip.v, kp = ip.kp;
+  const int y0 = ip.ty * kMOutH, x0 = ip.tx * kMOutW;
   const int hy = tid / TW, hx = tid % TW;   // haloed pixel of this lane
   const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
   const bool in_img = gy >= 0 && gy < H && gx >= 0 && gx < W;
   const bool interior = in_img && hy >= 1 && hy <= kMOutH && hx >= 1 && hx <= kMOutW;
-  // DB (ABL bit 256): two box buffers (chunk c+1's DMA in flight while chunk c is sampled;
-  // both fit in the Y image's space)
-  constexpr bool DB = (ABL & 256) != 0;
-  constexpr int kBoxFl = (kMBoxPx + 1) * 8;
-  static_assert(!DB || 2 * kBoxFl <= YFL, "two boxes fit in the Y image space");
+  // chunk c's reference pixels: one 16-B half per lane and DMA, half h of haloed pixel t at
+  // rimg[(h NT + t) 4], after the box (conflict-free, lane-linear reads)
+  constexpr int kRefFl = (kMBoxPx + 1) * 8;
+  static_assert(kRefFl + 2 * kMThreads * 4 <= YFL, "the box and the reference fit in the Y space");
+  float* const rimg = smem + kRefFl;
   if (tid < 8) box[kMBoxPx * 8 + tid] = 0.f;   // the zero pixel
-  if (DB && tid < 8) box[kBoxFl + kMBoxPx * 8 + tid] = 0.f;
 
   const float dep = a.dvals[b * a.D + a.d_next + kp];
   const float* __restrict__ m = Rel + 12 * (v * a.B + b);
@@ -767,15 +834,20 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
                         ((uint32_t)p - __umul24((uint32_t)r, (uint32_t)bx.nx));
     boff[j] = gp * 32u + 16u * (uint32_t)img_half((uint32_t)p, i & 1);
   }
+  const uint32_t rpix = in_img ? (uint32_t)(gy * W + gx) : fbytes / 32u;
   auto stage = [&](int c) {
     const uint32_t cb = (uint32_t)c * cbytes;
 #pragma unroll
     for (int j = 0; j < NB; ++j)
       if (!(ABL & 2) && tid + j * kMThreads < items)
-        dma16(rsrc, box + (DB && (c & 1) ? kBoxFl : 0) + (j * kMThreads + wave * 64) * 4, boff[j] + cb);
+        dma16(rsrc, box + (j * kMThreads + wave * 64) * 4, boff[j] + cb);
+    // this lane's reference pixel in the c8 image (past the buffer: zeros)
+    if (!(ABL & 8)) {
+      const uint32_t ro = cb + rpix * 32u;
+      dma16(rref, rimg + (wave * 64) * 4, ro);
+      dma16(rref, rimg + (kMThreads + wave * 64) * 4, ro + 16u);
+    }
   };
-  // this lane's reference pixel in the c8 image (past the buffer: zeros)
-  const uint32_t rpix = in_img ? (uint32_t)(gy * W + gx) : fbytes / 32u;
   // sq staging scale: bound 2^-e in [2^14, 2^15) (sq <= 4 max|f|^2 <= bound), e of either
   // sign, so that fp16 cannot overflow and the lo parts of small sq stay normal numbers
   int e = 0;
@@ -795,13 +867,11 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   float o4[4] = {0.f, 0.f, 0.f, 0.f};
 
   stage(0);
-  float4 rf0 = ld_c8(rref, rpix, 0, HW), rf1 = ld_c8(rref, rpix, 1, HW);
   dma_wait();
   __syncthreads();
 #pragma unroll 1
   for (int c = 0; c < 4; ++c) {
-    if (DB && c < 3) stage(c + 1);   // the other buffer: last read in chunk c - 1
-    const float* const bx_c = box + (DB && (c & 1) ? kBoxFl : 0);
+    const float* const bx_c = box;
     // sample the own pixel (8 channels) and form sq
     float4 g0, g1;
     if (ABL & 4) {
@@ -817,12 +887,12 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       g1 = bil4(ld_c8(rsrc, tp.pix[0], 2 * c + 1, HW), ld_c8(rsrc, tp.pix[1], 2 * c + 1, HW),
                 ld_c8(rsrc, tp.pix[2], 2 * c + 1, HW), ld_c8(rsrc, tp.pix[3], 2 * c + 1, HW), tp);
     }
+    // the reference pixel from LDS (DMA'd with the box: a register prefetch carried across
+    // the chunk loop cost 16 register copies per chunk)
+    const float4 rf0 = *reinterpret_cast<const float4*>(rimg + tid * 4);
+    const float4 rf1 = *reinterpret_cast<const float4*>(rimg + (kMThreads + tid) * 4);
     const float4 s0 = sqdiff4(g0, rf0), s1 = sqdiff4(g1, rf1);
     const float sq[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    if (c < 3 && !(ABL & 8)) {   // the next chunk's reference pixel, in flight during this chunk
-      rf0 = ld_c8(rref, rpix, 2 * c + 2, HW);
-      rf1 = ld_c8(rref, rpix, 2 * c + 3, HW);
-    }
     // this chunk's B fragments, issued before the barrier: their L1/L2 latency is hidden
     // behind it and the centre-tap chain (2.5% of the kernel against loading them after;
     // DMA'ing all 12 to LDS once per item instead was 1.8%)
@@ -832,10 +902,8 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       Bl = owm[(c * 3 + 1) * 64 + lane];
       Bl2 = owm[(c * 3 + 2) * 64 + lane];
     }
-    if (!DB) {
-      __syncthreads();   // every lane's box reads of chunk c are done
-      if (c < 3) stage(c + 1);
-    }
+    __syncthreads();   // every lane's box and reference reads of chunk c are done
+    if (c < 3) stage(c + 1);
     // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel, fp32
     {
       const float* wt = w0t + (4 * kC + 8 * c) * 4;
@@ -844,14 +912,16 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
 #pragma unroll
         for (int co = 0; co < 4; ++co) o4[co] = fmaf(sq[j], wt[j * 4 + co], o4[co]);
     }
-    // split sq 2^-e into fp16 hi + lo (out-of-image pixels: the conv's zero padding)
+    // split sq 2^-e into fp16 hi + lo.  Out-of-image pixels (the conv's zero padding) already
+    // have sq = 0: zero bilinear weights on the box's zero pixel (or past the buffer) and a
+    // reference read past the buffer.  Two values per v_cvt_pk_f16_f32.
     uint32_t hw[4], lw[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float p0 = in_img ? sq[2 * i] * sqs : 0.f, p1 = in_img ? sq[2 * i + 1] * sqs : 0.f;
-      const _Float16 h0 = (_Float16)p0, h1 = (_Float16)p1;
-      const half2_t hv = {h0, h1};
-      const half2_t lv = {(_Float16)(p0 - (float)h0), (_Float16)(p1 - (float)h1)};
+      const float2 pp = make_float2(sq[2 * i] * sqs, sq[2 * i + 1] * sqs);
+      const half2_t hv = __builtin_convertvector((float2_t){pp.x, pp.y}, half2_t);
+      const float2_t hb = __builtin_convertvector(hv, float2_t);
+      const half2_t lv = __builtin_convertvector((float2_t){pp.x - hb[0], pp.y - hb[1]}, half2_t);
       hw[i] = __builtin_bit_cast(uint32_t, hv);
       lw[i] = __builtin_bit_cast(uint32_t, lv);
     }
@@ -899,10 +969,9 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     }
     if (c < 3) {
       dma_wait();
-      __syncthreads();   // chunk c+1's box visible (DB: and chunk c's buffer free)
+      __syncthreads();   // chunk c+1's box and reference visible
     }
   }
-  if (DB) __syncthreads();   // chunk 3's box reads done before Y overwrites the boxes
   // Y image (over the box space: every lane passed chunk 3's box reads before the barrier
   // above): D[row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)][col = lane & 31] of row group g
   if constexpr ((ABL & 32) == 0) {
@@ -947,8 +1016,7 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     ps = ((double)out.x + (double)out.y) + ((double)out.z + (double)out.w);
     pss = ((double)out.x * out.x + (double)out.y * out.y) + ((double)out.z * out.z + (double)out.w * out.w);
   }
-  ps = wave_sum_d(ps);
-  pss = wave_sum_d(pss);
+  wave_sum2_d(ps, pss);
   if (lane == 0) {
     wsum[wave][0] = ps;
     wsum[wave][1] = pss;
@@ -973,20 +1041,44 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
                   const unsigned* __restrict__ xbound) {
   if (blockDim.x != OmegaTile<TW>::NT) return;   // LDS images are sized for exactly this block
   const int ipb = a.omega_ipb > 1 ? a.omega_ipb : 1;
-  const int total = OmegaTile<TW>::tiles_d(a.H, a.W) * a.nsrc * a.npl;
-  const int bs = xcd_tile(blockIdx.x, gridDim.x);
+  const int npl = a.npl, nsrc = a.nsrc;
+  const int tiles_x = (a.W + OmegaTile<TW>::OUTW - 1) / OmegaTile<TW>::OUTW;
+  const int total = OmegaTile<TW>::tiles_d(a.H, a.W) * nsrc * npl;
+  const int seq0 = xcd_tile(blockIdx.x, gridDim.x) * ipb;
+  // seq = (tile * nsrc + v) * npl + kp, decomposed once and then advanced
+  OmegaPos ip;
+  ip.tile = seq0 / (nsrc * npl);
+  {
+    const int vk = seq0 - ip.tile * (nsrc * npl);
+    ip.v = vk / npl;
+    ip.kp = vk - ip.v * npl;
+    ip.ty = ip.tile / tiles_x;
+    ip.tx = ip.tile - ip.ty * tiles_x;
+  }
 #pragma unroll 1
   for (int it = 0; it < ipb; ++it) {
-    const int seq = bs * ipb + it;
-    if (seq >= total) break;
-    if (it) __syncthreads();   // the previous item's LDS reads are done
+    if (seq0 + it >= total) break;
+    if (it) {
+      __syncthreads();   // the previous item's LDS reads are done
+      if (++ip.kp == npl) {
+        ip.kp = 0;
+        if (++ip.v == nsrc) {
+          ip.v = 0;
+          ++ip.tile;
+          if (++ip.tx == tiles_x) {
+            ip.tx = 0;
+            ++ip.ty;
+          }
+        }
+      }
+    }
     // the item reads the arguments through a pointer the compiler cannot prove invariant
     // across items: otherwise it hoists every argument load out of the loop (SGPR spills)
     uint32_t z;
     asm volatile("s_mov_b32 %0, 0" : "=s"(z));
     typedef const __attribute__((address_space(4))) PipeArgs KPipeArgs;
     KPipeArgs& ka = *(KPipeArgs*)((const __attribute__((address_space(4))) char*)&a + z);
-    omega_item<ABL, TW, BAL>(ka, P, Rel, xbound, seq);
+    omega_item<ABL, TW, BAL>(ka, P, Rel, xbound, ip);
   }
 }
 
