@@ -111,7 +111,8 @@ def homo_warp(src_fea: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor) -> 
 def homo_warp_backward(grad_out: torch.Tensor, rel: torch.Tensor, depth: torch.Tensor,
                        src_shape) -> torch.Tensor:
     """d loss / d src_fea of homo_warp: bilinear scatter-add of grad_out, summed in 64-bit fixed
-    point (bit-reproducible, aarmvs_homo_warp_backward)."""
+    point (bit-reproducible, aarmvs_homo_warp_backward; fp32 atomics for a batch element whose
+    grad_out is not finite).  Workspace: min(B, 64) * C * H * W * 8 bytes + 256."""
     _require_device(grad_out)
     g = grad_out.contiguous()
     B, C, H, W = src_shape
@@ -120,7 +121,7 @@ def homo_warp_backward(grad_out: torch.Tensor, rel: torch.Tensor, depth: torch.T
     grad_src = torch.zeros(B, C, H, W, device=g.device)
     n = lib().aarmvs_homo_warp_backward_workspace_bytes(B, C, H, W)
     if n == 0:
-        raise AarmvsError(f"aarmvs: homo_warp_backward geometry B={B} C={C} H={H} W={W} (B <= 64)")
+        raise AarmvsError(f"aarmvs: homo_warp_backward geometry B={B} C={C} H={H} W={W}")
     ws = torch.empty(n, dtype=torch.uint8, device=g.device)
     check(lib().aarmvs_homo_warp_backward(g.data_ptr(), rel_d.data_ptr(), dep.data_ptr(), B, C, H,
                                           W, grad_src.data_ptr(), ws.data_ptr(), _stream()),

@@ -46,8 +46,8 @@ const ParamLayout& param_layout() {
     pk += 64;
     l.ow0t_off = pk;
     pk += 4 * 32 * 9;
-    l.owb_off = pk;
-    pk += 4 * 2 * 64 * 8 / 2;   // halves -> floats
+    l.owc_off = pk;
+    pk += 4 * 4 * 6 * 4 / 2;    // halves -> floats (192: 64-float aligned)
     l.owb_scale_off = pk;
     pk += 64;
     l.owm_off = pk;
@@ -308,13 +308,18 @@ __global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __r
   }
   const float sc = ldexpf(1.0f, e);
   if (threadIdx.x == 0) pk[L.owb_scale_off] = ldexpf(1.0f, -e);
-  _Float16* b = reinterpret_cast<_Float16*>(pk + L.owb_off);
-  for (int i = threadIdx.x; i < 4 * 2 * 64 * 8; i += blockDim.x) {
-    const int ci8 = i & 7, lane = (i >> 3) & 63, k = (i >> 9) & 1, c = i >> 10;
-    const int n = lane & 15, g = lane >> 4, u = 4 * k + n / 4, tap = u < 4 ? u : u + 1, co = n & 3;
-    const float x = w[(co * 32 + 8 * c + ci8) * 9 + tap] * sc;
+  // the centre tap (tap 4) as v_mfma_f32_4x4x4f16 B operands, in the same three fp16 terms as
+  // the 32x32x16 fragments below: [chunk c][co j][term t (hi, lo, lo2)][K-step s][4 halves],
+  // element kk of step s against input channel 8 c + 4 s + kk (lane l of a 4x4 block holds
+  // column j = l & 3: 48 contiguous bytes per lane and chunk)
+  _Float16* bc = reinterpret_cast<_Float16*>(pk + L.owc_off);
+  for (int i = threadIdx.x; i < 4 * 4 * 6 * 4; i += blockDim.x) {
+    const int kk = i & 3, s = (i >> 2) & 1, t = (i >> 3) % 3, j = (i / 24) & 3, c = i / 96;
+    const float x = w[(j * 32 + 8 * c + 4 * s + kk) * 9 + 4] * sc;
     const _Float16 xh = (_Float16)x;
-    b[i] = g < 2 ? xh : (_Float16)(x - (float)xh);
+    const float r1 = x - (float)xh;
+    const _Float16 xl = (_Float16)r1;
+    bc[i] = t == 0 ? xh : t == 1 ? xl : (_Float16)(r1 - (float)xl);
   }
   // omega_mfma's v_mfma_f32_32x32x16_f16 B fragments: per chunk c and kind k against
   // A = [sq hi | sq lo]: 0: [W_hi; W_hi], 1: [W_lo; 0], 2: [W_lo2; W_lo] with W = W_hi + W_lo +
@@ -500,7 +505,7 @@ int aarmvs_homo_warp(const float* src_fea, const float* rel_proj, const float* d
 }
 
 size_t aarmvs_homo_warp_backward_workspace_bytes(int B, int C, int H, int W) {
-  if (B < 1 || B > 64 || C < 1 || H < 2 || W < 2) return 0;
+  if (B < 1 || C < 1 || H < 2 || W < 2) return 0;
   return homo_warp_bwd_workspace_bytes(B, C, H, W);
 }
 
@@ -509,8 +514,8 @@ int aarmvs_homo_warp_backward(const float* grad_out, const float* rel_proj, cons
                               hipStream_t stream) {
   if (!grad_out || !rel_proj || !depth || !grad_src || !workspace)
     return fail(AARMVS_ERR_INVALID, "homo_warp_backward: null pointer");
-  if (B < 1 || B > 64 || C < 1 || H < 2 || W < 2)
-    return fail(AARMVS_ERR_INVALID, "homo_warp_backward: need 1<=B<=64, C>=1, H>=2, W>=2");
+  if (B < 1 || C < 1 || H < 2 || W < 2)
+    return fail(AARMVS_ERR_INVALID, "homo_warp_backward: need B>=1, C>=1, H>=2, W>=2");
   hipError_t e = launch_homo_warp_bwd(grad_out, rel_proj, depth, B, C, H, W, grad_src, workspace, stream);
   return e == hipSuccess ? AARMVS_OK : hip_fail(e, "homo_warp_backward");
 }

@@ -265,7 +265,7 @@ struct PipeArgs {
   float* x;                   // [B,H,W,32] (NHWC)
   float* omega_out;           // [nsrc,B,H,W] (prev plane) or null
   const float* params;
-  size_t off_owb, off_owb_scale;   // omega conv MFMA B fragments, their scale
+  size_t off_owc, off_owb_scale;   // omega conv centre-tap 4x4x4 B operands, the fragments' scale
   size_t off_owm, off_owm_scale;   // omega_mfma's 32x32x16 B fragments, their scale
   size_t off_ow0t, off_ow0, off_ob0, off_og0w, off_og0b, off_ow1, off_ob1, off_og1w, off_og1b, off_ow2,
       off_ob2, off_og2w, off_og2b, off_owo, off_obo;
@@ -728,7 +728,8 @@ constexpr int kOmegaTW = 16;   // the library's tile width
 // ABL: ablation bits for the diagnostic harness only (tools/microbench/pipe_bench.cpp; the
 // library instantiates ABL = 0): 1 no MFMAs, 2 no box DMA, 4 no box sampling, 8 no reference
 // loads, 16 sampling positions without the homography divisions (the own pixel), 32 no Y
-// image / gather (t1 from the accumulators), 64 no statistics atomics, 128 no B-fragment loads
+// image / gather (t1 from the accumulators), 64 no statistics atomics, 128 no B-fragment loads,
+// 512 the centre tap on 4x4x4 MFMAs (CMF below)
 // BAL: sign-balanced accumulation, for the training sweep only: +9% time
 // wave_sum_d (device_common.h) of two values at once, in the same order and so with the same
 // result, on DPP moves with an undefined `old` operand: only lane 63's value is used, and every
@@ -861,10 +862,17 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   const float sqs = ldexpf(1.0f, -e);
   const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]: centre tap = tap 4
   const half8* __restrict__ owm = reinterpret_cast<const half8*>(P + a.off_owm);
+  // CMF (ABL bit 512, diagnostic): the centre tap on v_mfma_f32_4x4x4f16 instead of the fp32
+  // FMA chain.  Measured in round 6: 9.20 against 8.50 ms per headline launch (bit-different,
+  // parity green): ten dependent 4x4x4 MFMAs per chunk on one accumulator stall the wave more
+  // than the 32 FMAs they replace cost (the layout: tools/microbench/mfma4_layout.cpp)
+  constexpr bool CMF = (ABL & 512) != 0 && !BAL;
+  const half8* __restrict__ owc = reinterpret_cast<const half8*>(P + a.off_owc) + 3 * (lane & 3);
   floatx16 acc0, acc1;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
   float o4[4] = {0.f, 0.f, 0.f, 0.f};
+  floatx4 accc = {0.f, 0.f, 0.f, 0.f};
 
   stage(0);
   dma_wait();
@@ -904,8 +912,8 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     }
     __syncthreads();   // every lane's box and reference reads of chunk c are done
     if (c < 3) stage(c + 1);
-    // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel, fp32
-    {
+    // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel, fp32 (BAL)
+    if constexpr (!CMF) {
       const float* wt = w0t + (4 * kC + 8 * c) * 4;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -924,6 +932,25 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       const half2_t lv = __builtin_convertvector((float2_t){pp.x - hb[0], pp.y - hb[1]}, half2_t);
       hw[i] = __builtin_bit_cast(uint32_t, hv);
       lw[i] = __builtin_bit_cast(uint32_t, lv);
+    }
+    // CMF: the centre tap of the own pixel as sixteen 4x4 blocks (block = 4 lanes = 4 pixels,
+    // K = 4 channels), before the swaps: A = this lane's sq hi / lo of channels 4 s .. 4 s + 3,
+    // B = the tap's weights in three fp16 terms (hi sq x (W_hi + W_lo + W_lo2) + lo sq x (W_hi
+    // + W_lo), the off-centre taps' product set); D[pixel 4 b + r][co = lane & 3] in register
+    // r of lane 4 b + co
+    if constexpr (CMF) {
+      const half8 wh = owc[c * 12 + 0], wl = owc[c * 12 + 1], wl2 = owc[c * 12 + 2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const half4 ah = __builtin_bit_cast(half4, u32x2{hw[2 * st], hw[2 * st + 1]});
+        const half4 al = __builtin_bit_cast(half4, u32x2{lw[2 * st], lw[2 * st + 1]});
+        const half4 bh = st ? wh.hi : wh.lo, bl = st ? wl.hi : wl.lo, bl2 = st ? wl2.hi : wl2.lo;
+        accc = __builtin_amdgcn_mfma_f32_4x4x4f16(ah, bh, accc, 0, 0, 0);
+        accc = __builtin_amdgcn_mfma_f32_4x4x4f16(al, bh, accc, 0, 0, 0);
+        accc = __builtin_amdgcn_mfma_f32_4x4x4f16(ah, bl, accc, 0, 0, 0);
+        accc = __builtin_amdgcn_mfma_f32_4x4x4f16(ah, bl2, accc, 0, 0, 0);
+        accc = __builtin_amdgcn_mfma_f32_4x4x4f16(al, bl, accc, 0, 0, 0);
+      }
     }
     // lanes 0-31 / 32-63 hold rows 2w / 2w+1: after the swaps, (hw, lw) are the A operands
     // of row 2w (lanes 0-31 hi, 32-63 lo of pixel lane & 31) and of row 2w+1
@@ -982,6 +1009,11 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       yimg[(64 * wave + px) * kMYStride + col] = BAL ? -acc0[r] : acc0[r];   // (BAL: chunk 3 left -sum)
       yimg[(64 * wave + 32 + px) * kMYStride + col] = BAL ? -acc1[r] : acc1[r];
     }
+    // CMF: the centre tap in columns 32..35 of the pixel's Y row
+    if constexpr (CMF) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) yimg[(64 * wave + 4 * (lane >> 2) + r) * kMYStride + 32 + (lane & 3)] = accc[r];
+    }
   }
   __syncthreads();
   // GroupNorm partials in fp64 from the first addition on (var = E[x^2] - E[x]^2 cancels)
@@ -994,11 +1026,20 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       g4[2] = acc0[4] + acc1[5];
       g4[3] = acc0[6] + acc1[7];
     } else {
+    // neighbour q = tid + (dy TW + dx): one base address, constant offsets
+    const float* const yb = yimg + tid * kMYStride;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int tap = u < 4 ? u : u + 1;
-      const int q = (hy + tap / 3 - 1) * TW + hx + tap % 3 - 1;
-      const float4 yv = *reinterpret_cast<const float4*>(yimg + q * kMYStride + 4 * u);
+      const int dq = (tap / 3 - 1) * TW + tap % 3 - 1;
+      const float4 yv = *reinterpret_cast<const float4*>(yb + dq * kMYStride + 4 * u);
+      g4[0] += yv.x;
+      g4[1] += yv.y;
+      g4[2] += yv.z;
+      g4[3] += yv.w;
+    }
+    if constexpr (CMF) {
+      const float4 yv = *reinterpret_cast<const float4*>(yb + 32);
       g4[0] += yv.x;
       g4[1] += yv.y;
       g4[2] += yv.z;
@@ -1180,7 +1221,7 @@ static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspac
   a.omega_k = 0;
   a.off_ow0 = L.pk_off[P_OW0];
   a.off_ow0t = L.ow0t_off;
-  a.off_owb = L.owb_off;
+  a.off_owc = L.owc_off;
   a.off_owb_scale = L.owb_scale_off;
   a.off_owm = L.owm_off;
   a.off_owm_scale = L.owb_scale_off;

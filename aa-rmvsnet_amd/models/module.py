@@ -147,7 +147,10 @@ class DeformConv2d(nn.Module):
             nn.init.constant_(self.m_conv.weight, 0)
 
     def forward(self, x):
-        if x.is_cuda and self.kernel_size == 3 and x.shape[1] == 32 and x.dtype == torch.float32:
+        # the HIP sampler takes float32 only: under autocast p_conv / m_conv return float16
+        # offsets, so autocast (like any non-float32 input) takes the PyTorch expression
+        if (x.is_cuda and self.kernel_size == 3 and x.shape[1] == 32 and x.dtype == torch.float32
+                and not torch.is_autocast_enabled()):
             return self._forward_hip(x)
         ks = self.kernel_size
         n_taps = ks * ks

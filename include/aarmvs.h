@@ -77,8 +77,12 @@ int aarmvs_homo_warp(const float* src_fea, const float* rel_proj, const float* d
  * scatter of grad_out.  grad_src must be initialised by the caller (zeros for the
  * plain gradient).  The scatter sums are formed in 64-bit fixed point (exponent from
  * max |grad_out|), so the result is bit-reproducible whatever the order the GPU
- * serves the contributions in.  workspace: aarmvs_homo_warp_backward_workspace_bytes
- * (caller-owned, device memory; B <= 64). */
+ * serves the contributions in; a batch element whose grad_out holds a NaN or an
+ * infinity is scattered with fp32 atomics instead (the NaN/inf reaches the source
+ * pixels grid_sample's backward sends it to, the others stay finite).  Batch
+ * elements are processed 64 at a time.  workspace:
+ * aarmvs_homo_warp_backward_workspace_bytes = 256 + min(B,64)*C*H*W*8 bytes
+ * (caller-owned, device memory). */
 size_t aarmvs_homo_warp_backward_workspace_bytes(int B, int C, int H, int W);
 int aarmvs_homo_warp_backward(const float* grad_out, const float* rel_proj, const float* depth,
                               int B, int C, int H, int W, float* grad_src, void* workspace,

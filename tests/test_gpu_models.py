@@ -134,6 +134,47 @@ def test_homo_warping_depthwise_forward_backward():
     assert torch.equal(src.grad, g1)
 
 
+def test_homo_warp_backward_nonfinite_and_large_batch():
+    """a NaN / inf in grad_out reaches exactly the source pixels grid_sample's
+    backward sends it to, every other pixel keeps its finite gradient, and the other batch
+    elements keep the bit-reproducible fixed-point sums; B > 64 is processed in chunks."""
+    from aarmvs import ops
+    from oracle import sweep_oracle as orc
+    g = load("warp.npz")
+    _, N, H, W, C = (int(x) for x in g["shape"])
+    B = 3
+    sc = syn.scene(B, N, H, W, D=4, seed=int(g["seed"]), C=C)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    rel = orc.relative_projection(proj[:, 1], proj[:, 0])
+    dep = torch.from_numpy(sc["depth_values"][:, 1].copy())   # both bad pixels sample in-image
+    gout = torch.randn(B, C, H, W, generator=torch.Generator().manual_seed(3))
+    gout[1, 3, H // 2, W // 2] = float("nan")
+    gout[1, 5, 1, 2] = float("inf")
+    src_c = torch.from_numpy(sc["features"][1]).requires_grad_(True)
+    orc.homo_warp(src_c, rel, dep, fast=True).backward(gout)   # grid_sample's own backward
+    ref = src_c.grad.numpy()
+    got = ops.homo_warp_backward(gout.to(DEV), rel.to(DEV), dep.to(DEV), (B, C, H, W)).cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(np.isinf(got), np.isinf(ref))
+    fin = np.isfinite(ref)
+    assert 0 < (~fin[1]).sum() <= 8 and fin[[0, 2]].all()   # only the bad pixels' taps
+    np.testing.assert_allclose(got[fin], ref[fin], atol=1e-4 * np.abs(ref[fin]).max())
+    # the finite batch elements are the fixed-point sums of a finite-only call, bit for bit
+    clean = gout.clone()
+    clean[1] = 0.0
+    got_c = ops.homo_warp_backward(clean.to(DEV), rel.to(DEV), dep.to(DEV), (B, C, H, W)).cpu().numpy()
+    assert np.array_equal(got[[0, 2]], got_c[[0, 2]])
+    # B = 66 > 64: two chunks of batch elements, each element equal to its own single call
+    Bl = 66
+    rel_l = rel[:1].expand(Bl, 3, 4).contiguous()
+    dep_l = torch.from_numpy(np.linspace(500.0, 700.0, Bl).astype(np.float32))
+    g_l = torch.randn(Bl, 4, 8, 12, generator=torch.Generator().manual_seed(4))
+    big = ops.homo_warp_backward(g_l.to(DEV), rel_l.to(DEV), dep_l.to(DEV), (Bl, 4, 8, 12)).cpu()
+    for b in (0, 63, 64, 65):
+        one = ops.homo_warp_backward(g_l[b:b + 1].to(DEV), rel_l[b:b + 1].to(DEV), dep_l[b:b + 1].to(DEV),
+                                     (1, 4, 8, 12)).cpu()
+        assert torch.equal(big[b:b + 1], one)
+
+
 def test_training_backward_matches_cpu_autograd():
     """BPTT through the sweep (HIP forward + per-plane recompute) vs CPU autograd."""
     from oracle import sweep_oracle as orc

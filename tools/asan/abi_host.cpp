@@ -81,7 +81,8 @@ int main() {
   CHECK(aarmvs_homo_warp_backward(dummy, dummy, dummy, 1, 32, 8, 8, dummy, nullptr, nullptr) ==
         AARMVS_ERR_INVALID);   // no workspace
   CHECK(aarmvs_homo_warp_backward_workspace_bytes(1, 32, 8, 8) == 256 + 32 * 64 * 8);
-  CHECK(aarmvs_homo_warp_backward_workspace_bytes(65, 32, 8, 8) == 0);
+  CHECK(aarmvs_homo_warp_backward_workspace_bytes(65, 32, 8, 8) == 256 + 64 * 32 * 64 * 8);
+  CHECK(aarmvs_homo_warp_backward_workspace_bytes(1, 0, 8, 8) == 0);
   CHECK(aarmvs_sweep(nullptr, nullptr) == AARMVS_ERR_INVALID);
   aarmvs_sweep_args a;
   std::memset(&a, 0, sizeof(a));
