@@ -487,6 +487,28 @@ __device__ __forceinline__ TapP tap_p(const TapF& t, bool valid, int H, int W, b
   return o;
 }
 
+__device__ __forceinline__ TapP tap_p4(const TapF& t, bool valid, int H, int W, bool lds,
+                                      const Box& bx, uint32_t zpix) {
+  TapP o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o.wt[k] = t.wt[k];
+  // tap_p's result (omega_mfma): the four taps' validity from two column and two row tests (make_taps' tests on the same
+  // float coordinates), and their indices from the top-left one: one signed 24-bit multiply
+  // (a tap row or column may be -1; coordinates and extents are < 2^23 wherever a tap is
+  // valid, and an invalid tap's index is selected away)
+  const float xf1 = t.xf + 1.0f, yf1 = t.yf + 1.0f;
+  const bool cx0 = t.xf > -1.0f && t.xf < (float)W, cx1 = xf1 > -1.0f && xf1 < (float)W;
+  const bool cy0 = valid && t.yf > -1.0f && t.yf < (float)H;
+  const bool cy1 = valid && yf1 > -1.0f && yf1 < (float)H;
+  const int ox = lds ? bx.x0 : 0, oy = lds ? bx.y0 : 0, rs = lds ? bx.nx : W;
+  const int p00 = __mul24((int)t.yf - oy, rs) + ((int)t.xf - ox);
+  o.pix[0] = cy0 && cx0 ? (uint32_t)p00 : zpix;
+  o.pix[1] = cy0 && cx1 ? (uint32_t)(p00 + 1) : zpix;
+  o.pix[2] = cy1 && cx0 ? (uint32_t)(p00 + rs) : zpix;
+  o.pix[3] = cy1 && cx1 ? (uint32_t)(p00 + rs + 1) : zpix;
+  return o;
+}
+
 __device__ __forceinline__ float bil1(float v0, float v1, float v2, float v3, const TapP& t) {
   return __fmaf_rn(v3, t.wt[3], __fmaf_rn(v2, t.wt[2], __fmaf_rn(v1, t.wt[1], __fmul_rn(v0, t.wt[0]))));
 }
@@ -770,10 +792,25 @@ __device__ __forceinline__ void wave_sum2_d(double& u, double& w) {
 struct OmegaPos {
   int tile, ty, tx, v, kp;
 };
+// The block's GroupNorm partial of an item is summed over the block's waves one item later (by
+// thread 0, after the next item's first barrier; the kernel sums the last item's after its
+// loop): no barrier of its own.  wsum[par][wave] holds item parity par's wave sums.
+template <int NW>
+__device__ __forceinline__ void omega_block_sum(const double (*ws)[2], double& s0, double& s1) {
+  s0 = 0.0;
+  s1 = 0.0;
+  for (int w = 0; w < NW; ++w) {
+    s0 += ws[w][0];
+    s1 += ws[w][1];
+  }
+}
+
 template <int ABL, int TW, bool BAL, typename PA>
 __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
                                            const float* __restrict__ Rel,
-                                           const unsigned* __restrict__ xbound, const OmegaPos ip) {
+                                           const unsigned* __restrict__ xbound, const OmegaPos ip,
+                                           double (*wsum)[OmegaTile<TW>::NT / 64][2], int par,
+                                           bool has_prev, const OmegaPos pv) {
   using T = OmegaTile<TW>;
   constexpr int kMThreads = T::NT, kMBoxPx = T::BOXPX, kMOutH = T::OUTH, kMOutW = T::OUTW;
   constexpr int NB = (2 * kMBoxPx + kMThreads - 1) / kMThreads;   // box pieces per thread
@@ -783,13 +820,12 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   float* const box = smem;   // chunk c's source box, then (after the last chunk) Y
   float* const yimg = smem;
   __shared__ int red[kMThreads / 64][4];
-  __shared__ double wsum[kMThreads / 64][2];
   int tid;
   asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));   // see omega_mfma_kernel
   const int lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.z;
   const int H = a.H, W = a.W, HW = H * W, nsrc = a.nsrc;
-  const int tile = ip.tile, v = ip.v, kp = ip.kp;
+  const int v = ip.v, kp = ip.kp;
   const int y0 = ip.ty * kMOutH, x0 = ip.tx * kMOutW;
   const int hy = tid / TW, hx = tid % TW;   // haloed pixel of this lane
   const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
@@ -800,7 +836,6 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   constexpr int kRefFl = (kMBoxPx + 1) * 8;
   static_assert(kRefFl + 2 * kMThreads * 4 <= YFL, "the box and the reference fit in the Y space");
   float* const rimg = smem + kRefFl;
-  if (tid < 8) box[kMBoxPx * 8 + tid] = 0.f;   // the zero pixel
 
   const float dep = a.dvals[b * a.D + a.d_next + kp];
   const float* __restrict__ m = Rel + 12 * (v * a.B + b);
@@ -822,9 +857,16 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     box_extend(tf, H, W, lx, ly, bhx, bhy);
   }
   const Box bx = box_reduce<kMThreads / 64>(lx, ly, bhx, bhy, red);
+  // after box_reduce's barrier: every wave is past the previous item's Y gather and wave sums
+  if (tid < 8) box[kMBoxPx * 8 + tid] = 0.f;   // the zero pixel
+  if (has_prev && tid == 0) {
+    double s0, s1;
+    omega_block_sum<kMThreads / 64>(wsum[par ^ 1], s0, s1);
+    if (!(ABL & 64)) part_put(a, pv.kp, b, pv.v, pv.tile, s0, s1);
+  }
   const bool lds = bx.nx * bx.ny <= min(kMBoxPx, a.box_cap);
   const uint32_t zp = lds ? (uint32_t)kMBoxPx : fbytes / 32u;
-  const TapP tp = tap_p(tf, in_img, H, W, lds, bx, zp);
+  const TapP tp = tap_p4(tf, in_img, H, W, lds, bx, zp);
   const int items = lds ? bx.nx * bx.ny * 2 : 0;
   const uint32_t mg = box_magic(bx.nx);
   uint32_t boff[NB];
@@ -868,9 +910,11 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   // than the 32 FMAs they replace cost (the layout: tools/microbench/mfma4_layout.cpp)
   constexpr bool CMF = (ABL & 512) != 0 && !BAL;
   const half8* __restrict__ owc = reinterpret_cast<const half8*>(P + a.off_owc) + 3 * (lane & 3);
-  floatx16 acc0, acc1;
+  floatx16 acc0, acc1;   // first written by chunk 0's MFMAs (ABL 1: zero here)
+  if constexpr ((ABL & 1) != 0) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+  }
   float o4[4] = {0.f, 0.f, 0.f, 0.f};
   floatx4 accc = {0.f, 0.f, 0.f, 0.f};
 
@@ -984,8 +1028,14 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       Bl2 = A1;
     }
     if (!(ABL & 1)) {
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, acc1, 0, 0, 0);
+      if (c == 0) {   // the accumulators start from the MFMA's inline-zero C operand (no zero fill)
+        const floatx16 z = {};
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, z, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, z, 0, 0, 0);
+      } else {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, acc1, 0, 0, 0);
+      }
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl, acc1, 0, 0, 0);
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl2, acc0, 0, 0, 0);
@@ -1027,16 +1077,18 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       g4[3] = acc0[6] + acc1[7];
     } else {
     // neighbour q = tid + (dy TW + dx): one base address, constant offsets
+    // (the sum starts from tap 0's value rather than 0 + it: the same sum but for the sign
+    // of an exactly zero one)
     const float* const yb = yimg + tid * kMYStride;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int tap = u < 4 ? u : u + 1;
       const int dq = (tap / 3 - 1) * TW + tap % 3 - 1;
       const float4 yv = *reinterpret_cast<const float4*>(yb + dq * kMYStride + 4 * u);
-      g4[0] += yv.x;
-      g4[1] += yv.y;
-      g4[2] += yv.z;
-      g4[3] += yv.w;
+      g4[0] = u ? g4[0] + yv.x : yv.x;
+      g4[1] = u ? g4[1] + yv.y : yv.y;
+      g4[2] = u ? g4[2] + yv.z : yv.z;
+      g4[3] = u ? g4[3] + yv.w : yv.w;
     }
     if constexpr (CMF) {
       const float4 yv = *reinterpret_cast<const float4*>(yb + 32);
@@ -1059,17 +1111,8 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   }
   wave_sum2_d(ps, pss);
   if (lane == 0) {
-    wsum[wave][0] = ps;
-    wsum[wave][1] = pss;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    double s0 = 0.0, s1 = 0.0;
-    for (int w = 0; w < kMThreads / 64; ++w) {
-      s0 += wsum[w][0];
-      s1 += wsum[w][1];
-    }
-    if (!(ABL & 64)) part_put(a, kp, b, v, tile, s0, s1);
+    wsum[par][wave][0] = ps;
+    wsum[par][wave][1] = pss;
   }
 }
 
@@ -1096,11 +1139,17 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     ip.ty = ip.tile / tiles_x;
     ip.tx = ip.tile - ip.ty * tiles_x;
   }
+  constexpr int NW = OmegaTile<TW>::NT / 64;
+  __shared__ double wsum[2][NW][2];
+  OmegaPos pv = ip;
+  int it = 0;
 #pragma unroll 1
-  for (int it = 0; it < ipb; ++it) {
+  for (; it < ipb; ++it) {
     if (seq0 + it >= total) break;
+    // (no barrier between items: the next item's LDS writes all follow box_reduce's barrier,
+    // which every wave reaches after the previous item's last LDS read)
     if (it) {
-      __syncthreads();   // the previous item's LDS reads are done
+      pv = ip;
       if (++ip.kp == npl) {
         ip.kp = 0;
         if (++ip.v == nsrc) {
@@ -1119,7 +1168,15 @@ omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restri
     asm volatile("s_mov_b32 %0, 0" : "=s"(z));
     typedef const __attribute__((address_space(4))) PipeArgs KPipeArgs;
     KPipeArgs& ka = *(KPipeArgs*)((const __attribute__((address_space(4))) char*)&a + z);
-    omega_item<ABL, TW, BAL>(ka, P, Rel, xbound, ip);
+    omega_item<ABL, TW, BAL>(ka, P, Rel, xbound, ip, wsum, it & 1, it > 0, pv);
+  }
+  if (it > 0) {   // the last item's block sum
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s0, s1;
+      omega_block_sum<NW>(wsum[(it - 1) & 1], s0, s1);
+      if (!(ABL & 64)) part_put(a, ip.kp, (int)blockIdx.z, ip.v, ip.tile, s0, s1);
+    }
   }
 }
 

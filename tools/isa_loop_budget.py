@@ -2,7 +2,9 @@
 named by a substring, weights each basic block by TRIP^(loop depth - 1) (the item loop is
 depth 1, the chunk loop depth 2), and counts instruction classes.
 
-usage: python tools/isa_loop_budget.py FILE.s NAME_SUBSTRING [TRIP=4]"""
+usage: python tools/isa_loop_budget.py FILE.s NAME_SUBSTRING [TRIP=4] [BASE=1]
+(BASE: the loop depth counted once, i.e. the item loop's; 0 when the compiler does not
+annotate the item loop as a loop)"""
 import re
 import sys
 
@@ -26,6 +28,7 @@ def kernel_lines(path, sub):
 def main():
     path, sub = sys.argv[1], sys.argv[2]
     trip = float(sys.argv[3]) if len(sys.argv) > 3 else 4.0
+    base = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     depth = 0
     cnt = {}
     for ln in kernel_lines(path, sub):
@@ -39,7 +42,7 @@ def main():
         c = classify(s.split()[0])
         if c is None:
             continue
-        w = trip ** max(depth - 1, 0)
+        w = trip ** max(depth - base, 0)
         cnt[c] = cnt.get(c, 0) + w
         if "_dpp" in s.split()[0] or "row_" in s or "quad_perm" in s:
             cnt["dpp"] = cnt.get("dpp", 0) + w
