@@ -380,8 +380,9 @@ class DepthSweep:
     """
 
     def __init__(self, params: dict, device, overlap: bool = True):
-        """``overlap``: run each next plane's omega pipeline on a second stream, concurrent
-        with the current plane's cost slice and regulariser step (same results)."""
+        """``overlap``: run the next plane group's cost stage on a second stream beside the
+        current group's regulariser steps, and (eval sweeps) the back of each plane's U-Net step
+        on a library stream beside the front of the next plane's (same results, bit for bit)."""
         self.device = torch.device(device)
         self.packed = pack_params(params, self.device)
         self._ws = {}

@@ -192,8 +192,13 @@ TrainLayout train_layout(int B, int H, int W);
 UnetIO unet_io_ws(const Workspace& ws, int parity);
 UnetIO unet_io_record(const TrainLayout& T, const aarmvs_train_record& r, int d);
 
+// stages: bit 0 the front (cells 0, 1, 2: the encoder), bit 1 the back (deconv_0, cell 3,
+// deconv_1, cell 4); the back of plane d reads only the front's outputs of plane d, so the front
+// of plane d + 1 may run beside it (the sweep's two-stream regulariser)
+constexpr int kUnetFront = 1, kUnetBack = 2, kUnetAll = 3;
 hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
-                            const Workspace& ws, const UnetIO& io, hipStream_t s);
+                            const Workspace& ws, const UnetIO& io, hipStream_t s,
+                            int stages = kUnetAll);
 hipError_t launch_head_wta(const float* params, const SweepGeom& g, const UnetIO& io,
                            const Workspace& ws, const float* depth_values, int d,
                            float* cost_out, bool wta, hipStream_t s);

@@ -564,6 +564,19 @@ float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int plan
 
 }  // extern "C"
 
+// Two-stream regulariser (eval sweeps): the back of the U-Net step of plane d (deconv_0, cell 3,
+// deconv_1, cell 4, the head) on a library-owned stream beside the front of plane d + 1 (cells
+// 0, 1, 2) on the caller's stream.  The front of plane d + 1 writes the other ping-pong slot of
+// h0..h2 than the one the back of plane d reads; the front of plane d + 2 waits for the back of
+// plane d.  On whenever the caller asks for concurrency (an aux stream for the cost stage);
+// AARMVS_REG_STREAMS=0/1 forces it off/on.  Measured (round 6, bit-identical): config 1
+// 0.231 -> 0.300 G hyp/s, config 2 1.180 -> 1.233, the headline 1.150 -> 1.160.
+static bool reg_two_stream(bool aux) {
+  const char* s = std::getenv("AARMVS_REG_STREAMS");
+  if (s && *s) return std::atoi(s) != 0;
+  return aux;
+}
+
 // planes per cost-stage group: kPlaneGroup, or AARMVS_NPL=n (1 <= n <= kPlaneGroup; A/B runs)
 static int plane_group() {
   const char* s = std::getenv("AARMVS_NPL");
@@ -607,13 +620,17 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   // group parity two events: ev_cost[p] "group's slices ready" (aux -> main) and
   // ev_used[p] "group's slices consumed" (main -> aux, before group i+2 reuses the slots).
   hipStream_t aux = (a->aux_stream && a->aux_stream != stream) ? a->aux_stream : nullptr;
+  const bool reg2 = !rec && reg_two_stream(aux != nullptr);
   const int G = plane_group();
-  // ev_cost[2], ev_used[2], fork/join: a per-thread, per-device set reused across calls (a
+  // ev_cost[2], ev_used[2], fork/join, and the two-stream regulariser's ev_front[2],
+  // ev_back[2], fork/join and stream: a per-thread, per-device set reused across calls (a
   // training forward makes one call per plane).  Events are only recorded/waited on the
-  // caller's streams, and a record overwrites the previous one, so reuse is safe.
+  // caller's streams and the set's own, and a record overwrites the previous one, so reuse is
+  // safe.
   struct EventSet {
     int dev = -1;
-    hipEvent_t ev[5] = {};
+    hipEvent_t ev[10] = {};
+    hipStream_t back = nullptr;
   };
   static thread_local EventSet evs_dev[kMaxDevices];   // one set per device
   auto sweep_fail = [&](hipError_t err, const char* where) { return hip_fail(err, where); };
@@ -621,14 +638,19 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   if ((e = current_device(dev)) != hipSuccess) return sweep_fail(e, "sweep: get device");
   EventSet& evs = evs_dev[dev];
   hipEvent_t* ev = evs.ev;
-  if (aux && evs.dev != dev) {
+  if ((aux || reg2) && evs.dev != dev) {
     for (hipEvent_t& x : evs.ev)
       if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
         return sweep_fail(e, "sweep: event create");
+    if ((e = hipStreamCreateWithFlags(&evs.back, hipStreamNonBlocking)) != hipSuccess)
+      return sweep_fail(e, "sweep: stream create");
     evs.dev = dev;
   }
   hipEvent_t* ev_cost = ev;
   hipEvent_t* ev_used = ev + 2;
+  hipEvent_t* ev_front = ev + 5;
+  hipEvent_t* ev_back = ev + 7;
+  hipStream_t back = reg2 ? evs.back : nullptr;
   hipStream_t cs = aux ? aux : stream;   // the cost stage's stream
 
   if (a->d_begin == 0) {
@@ -662,8 +684,15 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         (e = hipStreamWaitEvent(aux, ev[4], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: fork");
   }
-  // every return from here on (errors included) leaves the aux stream's work ordered on `stream`
+  if (back) {   // fork: the regulariser's back stream starts after `stream`'s work so far
+    if ((e = hipEventRecord(ev[9], stream)) != hipSuccess ||
+        (e = hipStreamWaitEvent(back, ev[9], 0)) != hipSuccess)
+      return sweep_fail(e, "sweep: fork");
+  }
+  // every return from here on (errors included) leaves the aux and back streams' work ordered
+  // on `stream`
   StreamJoin join{stream, aux, ev[4]};
+  StreamJoin join_back{stream, back, ev[9]};
   // the WTA images are maintained on every plane, whether or not this call returns depth:
   // a sweep split into d_range calls gives the same depth/confidence however its earlier
   // pieces were requested (24 B/px per plane, <0.5% of a plane's time)
@@ -702,6 +731,24 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         e = launch_layout(xd, a->slice_out, a->B, kC, a->H * a->W, false, stream);
         if (e != hipSuccess) return sweep_fail(e, "sweep: slice copy");
       }
+      if (back) {
+        // the front of plane d overwrites the h0..h2 slots the back of plane d - 2 read
+        if (d - 2 >= a->d_begin && (e = hipStreamWaitEvent(stream, ev_back[d & 1], 0)) != hipSuccess)
+          return sweep_fail(e, "sweep: event wait");
+        if ((e = launch_unet_step(xd, params, g, ws, io, stream, kUnetFront)) != hipSuccess)
+          return sweep_fail(e, "sweep: regulariser step");
+        if ((e = hipEventRecord(ev_front[d & 1], stream)) != hipSuccess ||
+            (e = hipStreamWaitEvent(back, ev_front[d & 1], 0)) != hipSuccess)
+          return sweep_fail(e, "sweep: event");
+        if ((e = launch_unet_step(xd, params, g, ws, io, back, kUnetBack)) != hipSuccess)
+          return sweep_fail(e, "sweep: regulariser step");
+        if ((e = launch_head_wta(params, g, io, ws, a->depth_values, d, a->cost_out, wta, back)) !=
+            hipSuccess)
+          return sweep_fail(e, "sweep: head/wta");
+        if ((e = hipEventRecord(ev_back[d & 1], back)) != hipSuccess)
+          return sweep_fail(e, "sweep: event record");
+        continue;
+      }
       if ((e = launch_unet_step(xd, params, g, ws, io, stream)) != hipSuccess)
         return sweep_fail(e, "sweep: regulariser step");
       if ((e = launch_head_wta(params, g, io, ws, a->depth_values, d, a->cost_out, wta,
@@ -717,6 +764,7 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         (e = hipStreamWaitEvent(stream, ev[4], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: join");
   }
+  if (back && (e = join_back.join()) != hipSuccess) return sweep_fail(e, "sweep: join");
   if ((a->depth_out || a->conf_out) && a->d_end == a->D) {
     if ((e = launch_finalize(g, ws, a->depth_out, a->conf_out, stream)) != hipSuccess)
       return sweep_fail(e, "sweep: finalize");

@@ -1350,7 +1350,7 @@ UnetIO unet_io_record(const TrainLayout& T, const aarmvs_train_record& r, int d)
 }
 
 hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
-                            const Workspace& ws, const UnetIO& io, hipStream_t s) {
+                            const Workspace& ws, const UnetIO& io, hipStream_t s, int stages) {
   const ParamLayout& L = param_layout();
   const int H = g.H, W = g.W, B = g.B, cu = g.cu_count;
   hipError_t e;
@@ -1380,6 +1380,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a.c_in += b * hid * px;
     if (a.z_out) a.z_out += b * 4 * hid * px;
   };
+  if (stages & kUnetFront) {
   // cell 0: [x, h0] @ H
   CellArgs a0 = cell(0, {{x, 32, SRC_PLAIN, nullptr, nullptr, nullptr},
                          {io.h_prev[0], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
@@ -1393,6 +1394,8 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   CellArgs a2 = cell(2, {{io.h_new[1], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {io.h_prev[2], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
   if ((e = run_cell_h3<2>(a2, params + L.h3_scale_off + 2, cu, K_CELL2, s)) != hipSuccess) return e;
+  }
+  if (!(stages & kUnetBack)) return hipSuccess;
   // GroupNorm statistics are per batch element, so the two cells that consume the deconvs'
   // normalised outputs are launched per batch element; each reduces its element's deconv
   // partials itself (gn_table) and block 0 stores the statistics.

@@ -261,6 +261,36 @@ def test_two_stream_schedule_is_bit_identical():
     assert torch.equal(a["depth"], c["depth"]) and torch.equal(a["conf"], c["conf"])
 
 
+@pytest.mark.parametrize("B,N,H,W,D", [(1, 3, 128, 160, 37), (2, 4, 64, 96, 5)])
+def test_two_stream_regulariser_is_bit_identical(monkeypatch, B, N, H, W, D):
+    """The regulariser's back (deconvs, cells 3-4, head) of plane d on the library's stream
+    beside the front (cells 0-2) of plane d+1 (AARMVS_REG_STREAMS=1) against the one-stream
+    order: bit-identical cost volume, depth and confidence, also over continued d_ranges whose
+    boundaries fall inside and at the end of plane groups, with and without the cost-stage
+    stream (config 1's 160x128 at D=37 crosses three plane groups)."""
+    from aarmvs import ops
+    sc = syn.scene(B, N, H, W, D, seed=21)
+    feats = torch.from_numpy(sc["features"]).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    args = (feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
+            [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]))
+    P = P_of(6)
+    monkeypatch.setenv("AARMVS_REG_STREAMS", "0")
+    ref = ops.DepthSweep(P, DEV, overlap=True)(*args, want_cost=True)
+    monkeypatch.setenv("AARMVS_REG_STREAMS", "1")
+    for overlap in (True, False):
+        got = ops.DepthSweep(P, DEV, overlap=overlap)(*args, want_cost=True)
+        for k in ("cost", "depth", "conf"):
+            assert torch.equal(got[k], ref[k]), (overlap, k)
+    sw = ops.DepthSweep(P, DEV, overlap=True)
+    cost = torch.empty(B, D, H, W, device=DEV)
+    cuts = [0, 1, min(16, D - 1), D] if D > 17 else [0, 2, D]
+    for d0, d1 in zip(cuts[:-1], cuts[1:]):
+        c = sw(*args, d_range=(d0, d1), cost_out=cost)
+    assert torch.equal(cost, ref["cost"])
+    assert torch.equal(c["depth"], ref["depth"]) and torch.equal(c["conf"], ref["conf"])
+
+
 def test_full_size_properties():
     """BASELINE's full frame (1600x1184, N=7) at D=3, where the oracle is too slow: the
     two-stream and single-stream schedules and a continued d_range must agree bit for bit,
