@@ -604,10 +604,11 @@ class DepthSweep:
             off += n
         return grad_ref, grad_src, grads, grad_x
 
-    def state(self, B, H, W, nsrc, parity, cell, which) -> torch.Tensor:
-        """View of a hidden/cell state inside the workspace (after a sweep call)."""
+    def state(self, B, H, W, nsrc, planes, cell, which) -> torch.Tensor:
+        """View of a hidden/cell state inside the workspace after the sweep has processed
+        ``planes`` planes (or ``unet_step`` steps): the state those planes left."""
         ws = self.workspace(B, H, W, nsrc)
-        ptr = lib().aarmvs_state_ptr(ws.data_ptr(), B, H, W, nsrc, parity, cell, which)
+        ptr = lib().aarmvs_state_ptr(ws.data_ptr(), B, H, W, nsrc, planes, cell, which)
         if not ptr:
             raise AarmvsError("aarmvs: bad state query")
         hid = (16, 16, 16, 16, 8)[cell]

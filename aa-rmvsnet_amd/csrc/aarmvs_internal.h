@@ -84,12 +84,17 @@ const ParamLayout& param_layout();
 // ---------------------------------------------------------------------------
 // Workspace layout.
 // ---------------------------------------------------------------------------
+constexpr int kHRing[5] = {3, 2, 2, 2, 2};
+inline int h_slot(int k, int e) { return e % kHRing[k]; }
+
 struct Workspace {
   double* omega_stats;    // [kPlaneGroup][B][nsrc][3][kSlots][2] omega GN statistics per group plane
   double* omega_part;     // [kPlaneGroup][B][nsrc][omega_part_n][2] per-block GN partial sums
   int omega_part_n;       // partials per (plane, b, view): >= omega tiles, >= statistics blocks
   double* reg_stats;      // [B][2 deconvs][2 groups][kSlots][2] U-Net GN statistics
-  double* reg_part;       // [B][deconv blocks][4] a deconv's per-block GN partials (one deconv at a time)
+  double* reg_part;       // [B][deconv_1 blocks][4] deconv_1's per-block GN partials
+  double* reg_part0;      // [B][deconv_0 blocks][4] deconv_0's (its own region: the two deconvs
+                          // of neighbouring planes may run at once on the regulariser's streams)
   unsigned* xbound;       // float bits of an upper bound on |x| (cost slice) for this sweep:
                           // 8 max|feature|^2 (to_c8) or max|x| (unet_step); cell 0's fp16 range
   float* max_prob;        // [B,HW]
@@ -101,7 +106,9 @@ struct Workspace {
   float* t1;              // [kPlaneGroup][B][nsrc][HW][4] omega conv3x3 output per group plane
   float* u0;              // [B,16,H/2,W/2] deconv_0 output (pre-GN)
   float* u1;              // [B,16,H,W]     deconv_1 output (pre-GN)
-  float* h[5][2];         // ping-pong hidden states
+  float* h[5][3];         // hidden states: a ring of kHRing[k] slots (plane d reads slot d % r
+                          // and writes slot (d + 1) % r); h0 has 3 (read by cell 4 two stream
+                          // stages after cell 0 writes it), the others 2
   float* c[5];            // cell states (updated in place)
   size_t bytes;
   size_t omega_stats_bytes;  // one plane
@@ -189,13 +196,15 @@ struct TrainLayout {
   size_t cell_px[5];   // B * pixels of cell k
 };
 TrainLayout train_layout(int B, int H, int W);
-UnetIO unet_io_ws(const Workspace& ws, int parity);
+UnetIO unet_io_ws(const Workspace& ws, int d);   // plane d (absolute index in the sweep)
 UnetIO unet_io_record(const TrainLayout& T, const aarmvs_train_record& r, int d);
 
-// stages: bit 0 the front (cells 0, 1, 2: the encoder), bit 1 the back (deconv_0, cell 3,
-// deconv_1, cell 4); the back of plane d reads only the front's outputs of plane d, so the front
-// of plane d + 1 may run beside it (the sweep's two-stream regulariser)
-constexpr int kUnetFront = 1, kUnetBack = 2, kUnetAll = 3;
+// stages: the step's four parts (kUnetP0..P3, run in that order); a part of plane d reads only
+// the earlier parts' outputs of plane d and its own state, so the parts of neighbouring planes
+// may run at once on different streams (the sweep's multi-stream regulariser)
+constexpr int kUnetP0 = 1, kUnetP1 = 2, kUnetP2 = 4, kUnetP3 = 8;   // cells 0-1 | cell 2 |
+                                                                     // deconv_0 + cell 3 | deconv_1 + cell 4
+constexpr int kUnetFront = kUnetP0 | kUnetP1, kUnetBack = kUnetP2 | kUnetP3, kUnetAll = 15;
 hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
                             const Workspace& ws, const UnetIO& io, hipStream_t s,
                             int stages = kUnetAll);

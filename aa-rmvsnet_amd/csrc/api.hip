@@ -185,6 +185,8 @@ Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
   // deconv_1's blocks (8 x 32 tiles of its H/2 x W/2 input) outnumber deconv_0's
   ws.reg_part = reinterpret_cast<double*>(
       take((size_t)B * ((W / 2 + 31) / 32) * ((H / 2 + 7) / 8) * 4 * sizeof(double)));
+  ws.reg_part0 = reinterpret_cast<double*>(
+      take((size_t)B * ((W / 4 + 31) / 32) * ((H / 4 + 7) / 8) * 4 * sizeof(double)));
   ws.u0 = reinterpret_cast<float*>(take(B * 16 * HW2 * 4));
   ws.u1 = reinterpret_cast<float*>(take(B * 16 * HW * 4));
   const size_t state_begin = off;
@@ -192,8 +194,7 @@ Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
   const size_t cell_px[5] = {HW, HW2, HW4, HW2, HW};
   for (int k = 0; k < 5; ++k) {
     const size_t n = (size_t)B * kCellHid[k] * cell_px[k] * 4;
-    ws.h[k][0] = reinterpret_cast<float*>(take(n));
-    ws.h[k][1] = reinterpret_cast<float*>(take(n));
+    for (int r = 0; r < 3; ++r) ws.h[k][r] = r < kHRing[k] ? reinterpret_cast<float*>(take(n)) : nullptr;
     ws.c[k] = reinterpret_cast<float*>(take(n));
   }
   ws.state_bytes = off - state_begin;
@@ -555,26 +556,37 @@ size_t aarmvs_train_record_bytes(int B, int H, int W, int which) {
   }
 }
 
-float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int plane_parity,
+float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int planes,
                         int cell, int which) {
-  if (!workspace || cell < 0 || cell > 4 || check_geom(B, H, W, nsrc) != AARMVS_OK) return nullptr;
+  if (!workspace || cell < 0 || cell > 4 || planes < 0 || check_geom(B, H, W, nsrc) != AARMVS_OK)
+    return nullptr;
   Workspace ws = carve_workspace(workspace, B, H, W, nsrc);
-  return which == 0 ? ws.h[cell][plane_parity & 1] : ws.c[cell];
+  return which == 0 ? ws.h[cell][h_slot(cell, planes)] : ws.c[cell];
 }
 
 }  // extern "C"
 
-// Two-stream regulariser (eval sweeps): the back of the U-Net step of plane d (deconv_0, cell 3,
-// deconv_1, cell 4, the head) on a library-owned stream beside the front of plane d + 1 (cells
-// 0, 1, 2) on the caller's stream.  The front of plane d + 1 writes the other ping-pong slot of
-// h0..h2 than the one the back of plane d reads; the front of plane d + 2 waits for the back of
-// plane d.  On whenever the caller asks for concurrency (an aux stream for the cost stage);
-// AARMVS_REG_STREAMS=0/1 forces it off/on.  Measured (round 6, bit-identical): config 1
-// 0.231 -> 0.300 G hyp/s, config 2 1.180 -> 1.233, the headline 1.150 -> 1.160.
-static bool reg_two_stream(bool aux) {
+// Multi-stream regulariser (eval sweeps).  The U-Net step is four parts run in order (P0: cells
+// 0-1, P1: cell 2, P2: deconv_0 + cell 3, P3: deconv_1 + cell 4 and the head); a part of plane d
+// needs the earlier parts of plane d and its own state only, so the parts of neighbouring planes
+// can run at once on different streams: with 2 streams P0-P1 | P2-P3, with 3 streams P0 | P1-P2 |
+// P3, the later streams library-owned.  Per part and plane an event (a ring of 4 per part):
+//   data: a part waits for the previous part of its plane when that ran on another stream;
+//   slots: a part that overwrites a hidden-state slot waits for that slot's readers on other
+//   streams kHRing planes back (P0 writes h0 (ring 3, read by P3) and h1 (read by P1, P2); P1
+//   writes h2 (read by P2); P2 writes h3 (read by P3)).
+// Bit-identical to one stream (the same kernels on the same inputs).  AARMVS_REG_STREAMS=1/2/3
+// forces the count; by default 3 whenever the caller asks for concurrency (an aux stream).
+constexpr int kRegMaxStreams = 3, kRegEvRing = 4;
+static int reg_streams(bool aux) {
   const char* s = std::getenv("AARMVS_REG_STREAMS");
-  if (s && *s) return std::atoi(s) != 0;
-  return aux;
+  const int n = (s && *s) ? std::atoi(s) : (aux ? 3 : 1);
+  return std::max(1, std::min(kRegMaxStreams, n));
+}
+// the stream of each part for n streams
+static void reg_part_streams(int n, int (&ps)[4]) {
+  static const int map[kRegMaxStreams][4] = {{0, 0, 0, 0}, {0, 0, 1, 1}, {0, 1, 1, 2}};
+  for (int i = 0; i < 4; ++i) ps[i] = map[n - 1][i];
 }
 
 // planes per cost-stage group: kPlaneGroup, or AARMVS_NPL=n (1 <= n <= kPlaneGroup; A/B runs)
@@ -620,17 +632,20 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   // group parity two events: ev_cost[p] "group's slices ready" (aux -> main) and
   // ev_used[p] "group's slices consumed" (main -> aux, before group i+2 reuses the slots).
   hipStream_t aux = (a->aux_stream && a->aux_stream != stream) ? a->aux_stream : nullptr;
-  const bool reg2 = !rec && reg_two_stream(aux != nullptr);
+  // (a training forward, with its record, stays on one stream: 3 streams measured 254 -> 894 ms
+  // per config-4 training step)
+  const int nreg = rec ? 1 : reg_streams(aux != nullptr);
+  int pstream[4];
+  reg_part_streams(nreg, pstream);
   const int G = plane_group();
-  // ev_cost[2], ev_used[2], fork/join, and the two-stream regulariser's ev_front[2],
-  // ev_back[2], fork/join and stream: a per-thread, per-device set reused across calls (a
-  // training forward makes one call per plane).  Events are only recorded/waited on the
-  // caller's streams and the set's own, and a record overwrites the previous one, so reuse is
-  // safe.
+  // ev_cost[2], ev_used[2], fork/join, and the regulariser's part events, fork/join events and
+  // streams: a per-thread, per-device set reused across calls (a training forward makes one
+  // call per plane).  Events are only recorded/waited on the caller's streams and the set's
+  // own, and a record overwrites the previous one, so reuse is safe.
   struct EventSet {
     int dev = -1;
-    hipEvent_t ev[10] = {};
-    hipStream_t back = nullptr;
+    hipEvent_t ev[5 + 4 * kRegEvRing + kRegMaxStreams] = {};
+    hipStream_t reg[kRegMaxStreams] = {};
   };
   static thread_local EventSet evs_dev[kMaxDevices];   // one set per device
   auto sweep_fail = [&](hipError_t err, const char* where) { return hip_fail(err, where); };
@@ -638,19 +653,20 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   if ((e = current_device(dev)) != hipSuccess) return sweep_fail(e, "sweep: get device");
   EventSet& evs = evs_dev[dev];
   hipEvent_t* ev = evs.ev;
-  if ((aux || reg2) && evs.dev != dev) {
+  if ((aux || nreg > 1) && evs.dev != dev) {
     for (hipEvent_t& x : evs.ev)
       if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
         return sweep_fail(e, "sweep: event create");
-    if ((e = hipStreamCreateWithFlags(&evs.back, hipStreamNonBlocking)) != hipSuccess)
-      return sweep_fail(e, "sweep: stream create");
+    for (int i = 1; i < kRegMaxStreams; ++i)
+      if ((e = hipStreamCreateWithFlags(&evs.reg[i], hipStreamNonBlocking)) != hipSuccess)
+        return sweep_fail(e, "sweep: stream create");
     evs.dev = dev;
   }
   hipEvent_t* ev_cost = ev;
   hipEvent_t* ev_used = ev + 2;
-  hipEvent_t* ev_front = ev + 5;
-  hipEvent_t* ev_back = ev + 7;
-  hipStream_t back = reg2 ? evs.back : nullptr;
+  hipEvent_t(*ev_part)[kRegEvRing] = reinterpret_cast<hipEvent_t(*)[kRegEvRing]>(ev + 5);
+  hipEvent_t* ev_regjoin = ev + 5 + 4 * kRegEvRing;
+  hipStream_t rs[kRegMaxStreams] = {stream, nreg > 1 ? evs.reg[1] : nullptr, nreg > 2 ? evs.reg[2] : nullptr};
   hipStream_t cs = aux ? aux : stream;   // the cost stage's stream
 
   if (a->d_begin == 0) {
@@ -684,15 +700,16 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         (e = hipStreamWaitEvent(aux, ev[4], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: fork");
   }
-  if (back) {   // fork: the regulariser's back stream starts after `stream`'s work so far
-    if ((e = hipEventRecord(ev[9], stream)) != hipSuccess ||
-        (e = hipStreamWaitEvent(back, ev[9], 0)) != hipSuccess)
+  // fork: the regulariser's own streams start after `stream`'s work so far
+  for (int i = 1; i < nreg; ++i)
+    if ((e = hipEventRecord(ev_regjoin[i], stream)) != hipSuccess ||
+        (e = hipStreamWaitEvent(rs[i], ev_regjoin[i], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: fork");
-  }
-  // every return from here on (errors included) leaves the aux and back streams' work ordered
-  // on `stream`
+  // every return from here on (errors included) leaves the aux and regulariser streams' work
+  // ordered on `stream`
   StreamJoin join{stream, aux, ev[4]};
-  StreamJoin join_back{stream, back, ev[9]};
+  StreamJoin join_r1{stream, rs[1], ev_regjoin[1]};
+  StreamJoin join_r2{stream, rs[2], ev_regjoin[2]};
   // the WTA images are maintained on every plane, whether or not this call returns depth:
   // a sweep split into d_range calls gives the same depth/confidence however its earlier
   // pieces were requested (24 B/px per plane, <0.5% of a plane's time)
@@ -726,27 +743,37 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     for (int k = 0; k < n; ++k) {
       const int d = g0 + k;
       const float* xd = xs + (size_t)k * ws.x_plane;
-      const UnetIO io = rec ? unet_io_record(T, *rec, d) : unet_io_ws(ws, d & 1);
+      const UnetIO io = rec ? unet_io_record(T, *rec, d) : unet_io_ws(ws, d);
       if (d == d_last && a->slice_out) {
         e = launch_layout(xd, a->slice_out, a->B, kC, a->H * a->W, false, stream);
         if (e != hipSuccess) return sweep_fail(e, "sweep: slice copy");
       }
-      if (back) {
-        // the front of plane d overwrites the h0..h2 slots the back of plane d - 2 read
-        if (d - 2 >= a->d_begin && (e = hipStreamWaitEvent(stream, ev_back[d & 1], 0)) != hipSuccess)
-          return sweep_fail(e, "sweep: event wait");
-        if ((e = launch_unet_step(xd, params, g, ws, io, stream, kUnetFront)) != hipSuccess)
-          return sweep_fail(e, "sweep: regulariser step");
-        if ((e = hipEventRecord(ev_front[d & 1], stream)) != hipSuccess ||
-            (e = hipStreamWaitEvent(back, ev_front[d & 1], 0)) != hipSuccess)
-          return sweep_fail(e, "sweep: event");
-        if ((e = launch_unet_step(xd, params, g, ws, io, back, kUnetBack)) != hipSuccess)
-          return sweep_fail(e, "sweep: regulariser step");
-        if ((e = launch_head_wta(params, g, io, ws, a->depth_values, d, a->cost_out, wta, back)) !=
-            hipSuccess)
-          return sweep_fail(e, "sweep: head/wta");
-        if ((e = hipEventRecord(ev_back[d & 1], back)) != hipSuccess)
-          return sweep_fail(e, "sweep: event record");
+      if (nreg > 1) {
+        // wait for part q of plane e on another stream (planes before this call: joined)
+        auto wait_part = [&](int p, int q, int e) -> hipError_t {
+          if (e < a->d_begin || pstream[q] == pstream[p]) return hipSuccess;
+          return hipStreamWaitEvent(rs[pstream[p]], ev_part[q][e % kRegEvRing], 0);
+        };
+        UnetIO iom = io;
+        iom.clear_stats = false;   // the statistics are stored, never accumulated (one writer each)
+        for (int p = 0; p < 4; ++p) {
+          hipStream_t sp = rs[pstream[p]];
+          if (p > 0 && (e = wait_part(p, p - 1, d)) != hipSuccess) return sweep_fail(e, "sweep: event wait");
+          // the hidden-state slots this part overwrites, last read kHRing planes back
+          if (p == 0 && ((e = wait_part(0, 3, d - kHRing[0])) != hipSuccess ||
+                         (e = wait_part(0, 1, d - kHRing[1])) != hipSuccess ||
+                         (e = wait_part(0, 2, d - kHRing[1])) != hipSuccess))
+            return sweep_fail(e, "sweep: event wait");
+          if (p == 1 && (e = wait_part(1, 2, d - kHRing[2])) != hipSuccess) return sweep_fail(e, "sweep: event wait");
+          if (p == 2 && (e = wait_part(2, 3, d - kHRing[3])) != hipSuccess) return sweep_fail(e, "sweep: event wait");
+          if ((e = launch_unet_step(xd, params, g, ws, iom, sp, 1 << p)) != hipSuccess)
+            return sweep_fail(e, "sweep: regulariser step");
+          if (p == 3 && (e = launch_head_wta(params, g, iom, ws, a->depth_values, d, a->cost_out, wta, sp)) !=
+                            hipSuccess)
+            return sweep_fail(e, "sweep: head/wta");
+          if ((e = hipEventRecord(ev_part[p][d % kRegEvRing], sp)) != hipSuccess)
+            return sweep_fail(e, "sweep: event record");
+        }
         continue;
       }
       if ((e = launch_unet_step(xd, params, g, ws, io, stream)) != hipSuccess)
@@ -764,7 +791,8 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         (e = hipStreamWaitEvent(stream, ev[4], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: join");
   }
-  if (back && (e = join_back.join()) != hipSuccess) return sweep_fail(e, "sweep: join");
+  if ((e = join_r1.join()) != hipSuccess || (e = join_r2.join()) != hipSuccess)
+    return sweep_fail(e, "sweep: join");
   if ((a->depth_out || a->conf_out) && a->d_end == a->D) {
     if ((e = launch_finalize(g, ws, a->depth_out, a->conf_out, stream)) != hipSuccess)
       return sweep_fail(e, "sweep: finalize");
@@ -900,7 +928,7 @@ int aarmvs_unet_step(const float* x, int B, int H, int W, int nsrc, int step,
     return hip_fail(e, "unet_step: bound reset");
   if ((e = launch_layout(x, ws.x, B, kC, H * W, true, stream, ws.xbound)) != hipSuccess)
     return hip_fail(e, "unet_step: x layout");
-  const UnetIO io = unet_io_ws(ws, step & 1);
+  const UnetIO io = unet_io_ws(ws, step);
   if ((e = launch_unet_step(ws.x, params, g, ws, io, stream)) != hipSuccess)
     return hip_fail(e, "unet_step");
   // head conv only (no WTA): cost_out is [B,1,H,W] == [B,D=1,H,W] at plane 0

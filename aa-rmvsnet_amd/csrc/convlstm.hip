@@ -1312,12 +1312,11 @@ TrainLayout train_layout(int B, int H, int W) {
   return T;
 }
 
-UnetIO unet_io_ws(const Workspace& ws, int parity) {
-  const int cur = parity & 1, nxt = cur ^ 1;
+UnetIO unet_io_ws(const Workspace& ws, int d) {
   UnetIO io{};
   for (int k = 0; k < 5; ++k) {
-    io.h_prev[k] = ws.h[k][cur];
-    io.h_new[k] = ws.h[k][nxt];
+    io.h_prev[k] = ws.h[k][h_slot(k, d)];
+    io.h_new[k] = ws.h[k][h_slot(k, d + 1)];
     io.c_prev[k] = ws.c[k];
     io.c_new[k] = ws.c[k];
     io.z[k] = nullptr;
@@ -1380,7 +1379,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a.c_in += b * hid * px;
     if (a.z_out) a.z_out += b * 4 * hid * px;
   };
-  if (stages & kUnetFront) {
+  if (stages & kUnetP0) {
   // cell 0: [x, h0] @ H
   CellArgs a0 = cell(0, {{x, 32, SRC_PLAIN, nullptr, nullptr, nullptr},
                          {io.h_prev[0], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
@@ -1390,24 +1389,26 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   CellArgs a1 = cell(1, {{io.h_new[0], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {io.h_prev[1], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 2);
   if ((e = run_cell_h3<1>(a1, params + L.h3_scale_off + 1, cu, K_CELL1, s)) != hipSuccess) return e;
+  }
+  if (stages & kUnetP1) {
   // cell 2: [maxpool(h1'), h2] @ H/4
   CellArgs a2 = cell(2, {{io.h_new[1], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {io.h_prev[2], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
   if ((e = run_cell_h3<2>(a2, params + L.h3_scale_off + 2, cu, K_CELL2, s)) != hipSuccess) return e;
   }
-  if (!(stages & kUnetBack)) return hipSuccess;
   // GroupNorm statistics are per batch element, so the two cells that consume the deconvs'
   // normalised outputs are launched per batch element; each reduces its element's deconv
   // partials itself (gn_table) and block 0 stores the statistics.
-  int nblk0 = 0, nblk1 = 0;
+  if (stages & kUnetP2) {
   // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
+  int nblk0 = 0;
   {
     const int Hi = H / 4, Wi = W / 4;
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
     {
       ProfScope ps(s, K_DECONV0);
       hipLaunchKernelGGL(deconv_mfma_kernel<0>, grid, dim3(256), 0, s, io.h_new[2], params + L.dcm_off[0],
-                         params + L.pk_off[P_D0B], Hi, Wi, io.u0, ws.reg_part);
+                         params + L.pk_off[P_D0B], Hi, Wi, io.u0, ws.reg_part0);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     nblk0 = (int)(grid.x * grid.y);
@@ -1417,7 +1418,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     const double* st = io.reg_stats + reg_stat_index(b, 0, 0);
     const size_t hq = (size_t)(H / 2) * (W / 2);
     CellArgs a3 = cell(3, {{io.u0 + b * 16 * hq, 16, SRC_GNRELU, st, params + L.pk_off[P_D0GW],
-                            params + L.pk_off[P_D0GB], ws.reg_part + (size_t)b * nblk0 * 4, nblk0,
+                            params + L.pk_off[P_D0GB], ws.reg_part0 + (size_t)b * nblk0 * 4, nblk0,
                             io.reg_stats + reg_stat_index(b, 0, 0)},
                            {io.h_new[1] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr},
                            {io.h_prev[3] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr}},
@@ -1425,7 +1426,10 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     per_b(a3, b, hq, 16);
     if ((e = run_cell_h3<3>(a3, params + L.h3_scale_off + 3, cu, K_CELL3, s)) != hipSuccess) return e;
   }
+  }
+  if (!(stages & kUnetP3)) return hipSuccess;
   // deconv_1: h3' (H/2) -> u1 (H) + GN stats
+  int nblk1 = 0;
   {
     const int Hi = H / 2, Wi = W / 2;
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);

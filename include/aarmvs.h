@@ -190,10 +190,12 @@ size_t aarmvs_backward_scratch_bytes(int B, int H, int W, int nsrc);
 int aarmvs_sweep_backward(const aarmvs_backward_args* args, hipStream_t stream);
 
 /* Hidden state of the regulariser inside the workspace, for inspection/BPTT:
- * cell k in 0..4, which = 0 for h, 1 for c.  Valid after an aarmvs_sweep call;
- * returns a device pointer to [B,H_k,W_k,hid_k] (NHWC: the workspace keeps the U-Net
- * tensors channel-innermost) or NULL. */
-float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int plane_parity,
+ * cell k in 0..4, which = 0 for h, 1 for c, planes = the number of planes (or
+ * aarmvs_unet_step steps) processed so far: the state they left (h lives in a ring of
+ * 3 slots for cell 0 and 2 for the others, indexed by plane).  Valid after an
+ * aarmvs_sweep call; returns a device pointer to [B,H_k,W_k,hid_k] (NHWC: the workspace
+ * keeps the U-Net tensors channel-innermost) or NULL. */
+float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int planes,
                         int cell, int which);
 
 /* ---------------------------------------------------------------------------

@@ -90,7 +90,7 @@ def test_recorded_forward_matches_eval_sweep_and_holds_the_tensors():
         n = B * (H // s) * (W // s) * hid
         for which in (0, 1):
             got = st[off: off + n].view(B, H // s, W // s, hid).permute(0, 3, 1, 2)
-            want = sw.state(B, H, W, N - 1, D & 1, k, which)
+            want = sw.state(B, H, W, N - 1, D, k, which)
             torch.testing.assert_close(got, want, rtol=0, atol=2e-5 * max(1.0, float(want.abs().max())))
             off += -(-n // 64) * 64
     # cell 0's gate pre-activations of plane 2 = conv3x3([x_2, h0 of plane 1]) in float64

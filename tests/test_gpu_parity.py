@@ -81,8 +81,8 @@ def test_unet_steps_match_reference():
         cost = sw.unet_step(torch.from_numpy(xs[s]).to(DEV), s)
         np.testing.assert_allclose(cost.cpu().numpy(), g["cost"][s], atol=1e-5, rtol=1e-5)
     for i in range(5):
-        h = sw.state(B, H, W, 1, steps & 1, i, 0).cpu().numpy()
-        c = sw.state(B, H, W, 1, steps & 1, i, 1).cpu().numpy()
+        h = sw.state(B, H, W, 1, steps, i, 0).cpu().numpy()
+        c = sw.state(B, H, W, 1, steps, i, 1).cpu().numpy()
         np.testing.assert_allclose(h, g[f"h{i}"], atol=1e-5)
         np.testing.assert_allclose(c, g[f"c{i}"], atol=1e-5)
 
@@ -261,13 +261,15 @@ def test_two_stream_schedule_is_bit_identical():
     assert torch.equal(a["depth"], c["depth"]) and torch.equal(a["conf"], c["conf"])
 
 
+@pytest.mark.parametrize("nreg", ["2", "3"])
 @pytest.mark.parametrize("B,N,H,W,D", [(1, 3, 128, 160, 37), (2, 4, 64, 96, 5)])
-def test_two_stream_regulariser_is_bit_identical(monkeypatch, B, N, H, W, D):
-    """The regulariser's back (deconvs, cells 3-4, head) of plane d on the library's stream
-    beside the front (cells 0-2) of plane d+1 (AARMVS_REG_STREAMS=1) against the one-stream
-    order: bit-identical cost volume, depth and confidence, also over continued d_ranges whose
-    boundaries fall inside and at the end of plane groups, with and without the cost-stage
-    stream (config 1's 160x128 at D=37 crosses three plane groups)."""
+def test_multi_stream_regulariser_is_bit_identical(monkeypatch, B, N, H, W, D, nreg):
+    """The U-Net step's parts of neighbouring planes on the library's streams
+    (AARMVS_REG_STREAMS=2: cells 0-2 | deconvs, cells 3-4, head; 3: cells 0-1 | cell 2,
+    deconv_0, cell 3 | deconv_1, cell 4, head) against the one-stream order: bit-identical cost
+    volume, depth and confidence, also over continued d_ranges whose boundaries fall inside and
+    at the end of plane groups, with and without the cost-stage stream (config 1's 160x128 at
+    D=37 crosses three plane groups)."""
     from aarmvs import ops
     sc = syn.scene(B, N, H, W, D, seed=21)
     feats = torch.from_numpy(sc["features"]).to(DEV)
@@ -275,9 +277,9 @@ def test_two_stream_regulariser_is_bit_identical(monkeypatch, B, N, H, W, D):
     args = (feats[0], [feats[v] for v in range(1, N)], proj[:, 0],
             [proj[:, v] for v in range(1, N)], torch.from_numpy(sc["depth_values"]))
     P = P_of(6)
-    monkeypatch.setenv("AARMVS_REG_STREAMS", "0")
-    ref = ops.DepthSweep(P, DEV, overlap=True)(*args, want_cost=True)
     monkeypatch.setenv("AARMVS_REG_STREAMS", "1")
+    ref = ops.DepthSweep(P, DEV, overlap=True)(*args, want_cost=True)
+    monkeypatch.setenv("AARMVS_REG_STREAMS", nreg)
     for overlap in (True, False):
         got = ops.DepthSweep(P, DEV, overlap=overlap)(*args, want_cost=True)
         for k in ("cost", "depth", "conf"):

@@ -32,7 +32,7 @@ static void carve(int B, int H, int W, int nsrc) {
   CHECK(bytes > 0);
   std::vector<unsigned char> ws(bytes);
   const int hid[5] = {16, 16, 16, 16, 8}, sc[5] = {1, 2, 4, 2, 1};
-  for (int par = 0; par < 2; ++par)
+  for (int par = 0; par < 3; ++par)
     for (int k = 0; k < 5; ++k)
       for (int which = 0; which < 2; ++which) {
         float* p = aarmvs_state_ptr(ws.data(), B, H, W, nsrc, par, k, which);

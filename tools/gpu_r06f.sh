@@ -10,7 +10,7 @@ run() {  # run NAME CONFIG REG extra...
   local n=$1 c=$2 r=$3; shift 3
   AARMVS_REG_STREAMS=$r timeout -k 10 300 python bench.py --config $c --no-cpu --no-train --no-e2e --no-fusion "$@" > gpurun_out/${T}_$n.json 2> gpurun_out/${T}_$n.err || exit 1
 }
-run c1_r0 plumbing_160x128_n3_d48 0
+run c1_r0 plumbing_160x128_n3_d48 1
 run c1_r1 plumbing_160x128_n3_d48 1
 run c2_r0 dtu_eval_800x600_n5_d256 0 --steps 3
 run c2_r1 dtu_eval_800x600_n5_d256 1 --steps 3

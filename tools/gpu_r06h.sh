@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-6 step h: the multi-stream regulariser (AARMVS_REG_STREAMS = 1, 2, 3 streams) -- its
+# bit-identity tests and the state-slot tests, then bench lines at configs 1 and 2 and the headline.
+set -o pipefail
+mkdir -p gpurun_out
+T=$1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bptt.py tests/test_gpu_training.py tests/test_gpu_train_fixtures.py -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || { tail -20 gpurun_out/${T}_tests.log; exit 1; }
+tail -2 gpurun_out/${T}_tests.log
+run() {  # run NAME CONFIG REG extra...
+  local n=$1 c=$2 r=$3; shift 3
+  AARMVS_REG_STREAMS=$r timeout -k 10 300 python bench.py --config $c --no-cpu --no-train --no-e2e --no-fusion --no-kernel-timing "$@" > gpurun_out/${T}_$n.json 2> gpurun_out/${T}_$n.err || exit 1
+}
+for r in 1 2 3; do run c1_r$r plumbing_160x128_n3_d48 $r; done
+for r in 1 2 3; do run c2_r$r dtu_eval_800x600_n5_d256 $r --steps 3; done
+for r in 1 3; do run c5_r$r tnt_1920x1056_n11_d898 $r --steps 1 --warmup 1; done
+for r in 1 2 3; do run h_r$r dtu_eval_1600x1184_n7_d512 $r --steps 2; done
+for r in 1 3; do AARMVS_REG_STREAMS=$r timeout -k 10 300 python bench.py --train --steps 3 > gpurun_out/${T}_t_r$r.json 2> gpurun_out/${T}_t_r$r.err || exit 1; tail -1 gpurun_out/${T}_t_r$r.json | cut -c1-400; done
+for f in gpurun_out/${T}_c*_r*.json gpurun_out/${T}_h_r*.json; do python -c "
+import json,sys; d=json.loads(open('$f').read().strip().split('\n')[-1]); print('$f'.split('/')[-1], round(d['value']/1e9,4), 'G', d['ms_per_step'], 'ms')"; done
