@@ -1212,11 +1212,11 @@ __global__ void __launch_bounds__(256) deconv_wgrad_kernel(DcwArgs a) {
 }
 
 // conv_0 (head) weight / bias gradient over a group: gW[ci][tap] = sum gcost[p] h4[p + off][ci],
-// gb = sum gcost.  Thread per pixel q of h4 (32-bit index arithmetic: the caller checks the
-// group's pixel count): the products g[q - off] h4[q][ci] -- the same pairs, each h4 pixel read
-// once (32 B) and the nine row-contiguous gcost values from L1, where the pixel-of-gcost form
-// read nine 32-B h4 pixels per pixel (434 us per 16-plane group at 640x512, 5% of HBM).
-// 73 sums, block reduce, one partial of kHwPart floats per block.
+// gb = sum gcost.  Thread per pixel (32-bit index arithmetic: the caller checks the group's
+// pixel count), 73 sums, block reduce, one partial of kHwPart floats per block.  (Round 6: the
+// transposed form -- each h4 pixel read once, the nine gcost neighbours from L1 -- measured
+// 454 against 432 us per 16-plane group at 640x512: the 73 accumulators and the block reduce,
+// not the h4 reads, bound it.)
 constexpr int kHwBlocks = 1024, kHwPart = 80;
 static_assert((size_t)kHwBlocks * kHwPart <= (size_t)kWgBlocks * kWgPartMax, "head partials fit wpart");
 struct HwArgs {
@@ -1235,23 +1235,23 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(HwArgs a) {
   const uint32_t HW = (uint32_t)a.H * (uint32_t)a.W, W = (uint32_t)a.W;
   const uint32_t n = (uint32_t)a.nplanes * (uint32_t)a.B * HW;
   for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < n; t += gridDim.x * 256u) {
-    const uint32_t kb = t / HW, q = t - kb * HW;
+    const uint32_t kb = t / HW, p = t - kb * HW;
     const int b = (int)(kb % (uint32_t)a.B), k = (int)(kb / (uint32_t)a.B);
-    const int y = (int)(q / W), x = (int)(q - (uint32_t)y * W);
-    const float* gb = a.gcost + ((size_t)b * a.D + a.d0 + k) * HW;
-    const float4* hv = reinterpret_cast<const float4*>(a.h4 + (size_t)k * a.hstride + ((size_t)b * HW + q) * 8);
-    const float4 q0 = hv[0], q1 = hv[1];
-    const float hh[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    const int y = (int)(p / W), x = (int)(p - (uint32_t)y * W);
+    const float g = a.gcost[((size_t)b * a.D + a.d0 + k) * HW + p];
+    const float* hb = a.h4 + (size_t)k * a.hstride + (size_t)b * HW * 8;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      const int py = y - (tap / 3 - 1), px = x - (tap % 3 - 1);
-      if (py >= 0 && py < a.H && px >= 0 && px < a.W) {
-        const float g = gb[py * a.W + px];
+      const int qy = y + tap / 3 - 1, qx = x + tap % 3 - 1;
+      if (qy >= 0 && qy < a.H && qx >= 0 && qx < a.W) {
+        const float4* hv = reinterpret_cast<const float4*>(hb + ((size_t)qy * a.W + qx) * 8);
+        const float4 q0 = hv[0], q1 = hv[1];
+        const float hh[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
         for (int ci = 0; ci < 8; ++ci) s[ci * 9 + tap] = fmaf(g, hh[ci], s[ci * 9 + tap]);
       }
     }
-    s[72] += gb[q];
+    s[72] += g;
   }
   block_sum<73>(s, red);
   if (threadIdx.x == 0) {
