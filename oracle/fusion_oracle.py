@@ -34,8 +34,11 @@ def remap_linear(src, map_x, map_y):
     H, W = src.shape
     mx = np.asarray(map_x, np.float32)
     my = np.asarray(map_y, np.float32)
-    X = np.rint(mx * np.float32(INTER_TAB_SIZE)).astype(np.int64)   # cvRound: half to even
-    Y = np.rint(my * np.float32(INTER_TAB_SIZE)).astype(np.int64)
+    # cvRound: half to even; a non-finite map casts to INT64_MIN (x86), i.e. outside the image,
+    # where the taps read the constant border 0 as cv2's INT_MIN does
+    with np.errstate(invalid="ignore"):
+        X = np.rint(mx * np.float32(INTER_TAB_SIZE)).astype(np.int64)
+        Y = np.rint(my * np.float32(INTER_TAB_SIZE)).astype(np.int64)
     sx, sy = X >> INTER_BITS, Y >> INTER_BITS
     fx = (X & (INTER_TAB_SIZE - 1)).astype(np.float32) / np.float32(INTER_TAB_SIZE)
     fy = (Y & (INTER_TAB_SIZE - 1)).astype(np.float32) / np.float32(INTER_TAB_SIZE)

@@ -21,7 +21,7 @@ import test_gpu_bptt as T  # noqa: E402
 KB = "omega.reweight_network.2.bias"
 
 
-def run(seed, shape=(1, 3, 32, 48, 6)):
+def run(seed, shape=(1, 3, 32, 48, 6), f32=False, where=False):
     from oracle import sweep_oracle as orc
     B, N, H, W, D = shape
     sc, P, feats, proj, dv, sw, args = T._setup(B, N, H, W, D, seed, 6)
@@ -47,11 +47,33 @@ def run(seed, shape=(1, 3, 32, 48, 6)):
     unit = 2.0 ** -24 * tsum[0]
     g64, ghyb, ggpu = float(gp64[KB]), float(P64[KB].grad), float(gp[KB])
     gxe = float(torch.linalg.norm(gx - torch.stack(gx64).double()) / torch.linalg.norm(torch.stack(gx64).double()))
-    print(f"seed {seed}: bias {g64:+.6e}; (ggpu - g64) / u sum|t| = {(ggpu - g64) / unit:+.4f} = "
+    e32 = ""
+    if f32:
+        prev = torch.get_num_threads()
+        errs = []
+        for nt in T.F32_THREADS:
+            torch.set_num_threads(nt)
+            _, _, gp32, _ = T._oracle_grads(feats, proj, dv, P, R, torch.float32)
+            errs.append((float(gp32[KB]) - g64) / unit)
+        torch.set_num_threads(prev)
+        e32 = "; float32 (threads " + ",".join(map(str, T.F32_THREADS)) + "): " + " ".join(f"{e:+.4f}" for e in errs)
+    print(f"{shape} seed {seed}: bias {g64:+.6e}; (ggpu - g64) / u sum|t| = {(ggpu - g64) / unit:+.4f} = "
           f"dL/dx share {(ghyb - g64) / unit:+.4f} + cost-slice backward {(ggpu - ghyb) / unit:+.4f}; "
-          f"dL/dx rel L2 {gxe:.2e}", flush=True)
+          f"dL/dx rel L2 {gxe:.2e}{e32}", flush=True)
+    if where:   # where the dL/dx error sits: per plane, and the largest element
+        g64x = torch.stack(gx64).double()
+        err = (gx - g64x).abs()
+        per = [f"{float(torch.linalg.norm(gx[d] - g64x[d]) / torch.linalg.norm(g64x[d])):.1e}" for d in range(D)]
+        i = int(err.argmax())
+        idx = np.unravel_index(i, tuple(err.shape))
+        print(f"   dL/dx rel L2 per plane {per}; largest |error| {float(err.max()):.3e} at "
+              f"[d,b,c,y,x] = {tuple(int(t) for t in idx)} (|ref| max {float(g64x.abs().max()):.3e}); "
+              f"elements with |error| > 1e-3 max: {int((err > 1e-3 * float(g64x.abs().max())).sum())}", flush=True)
 
 
 if __name__ == "__main__":
-    for s in sys.argv[1:]:
-        run(int(s))
+    # args: SEED[:B,N,H,W,D] ...; env F32=1 adds float32's errors, WHERE=1 the dL/dx error map
+    for a in sys.argv[1:]:
+        seed, _, shp = a.partition(":")
+        shape = tuple(int(x) for x in shp.split(",")) if shp else (1, 3, 32, 48, 6)
+        run(int(seed), shape, f32=os.environ.get("F32") == "1", where=os.environ.get("WHERE") == "1")

