@@ -84,7 +84,11 @@ const ParamLayout& param_layout();
 // ---------------------------------------------------------------------------
 // Workspace layout.
 // ---------------------------------------------------------------------------
-constexpr int kHRing[5] = {3, 2, 2, 2, 2};
+// hidden-state ring lengths: h_k of plane e is overwritten by plane e + kHRing[k], so the
+// multi-stream regulariser's unit writing h_k may run up to kHRing[k] - 1 planes ahead of the
+// last unit that reads it (h0: cell 4, four units on; h1: cell 3; h2: deconv_0; h3: deconv_1)
+constexpr int kHRingMax = 6;
+constexpr int kHRing[5] = {6, 4, 3, 3, 2};
 inline int h_slot(int k, int e) { return e % kHRing[k]; }
 
 struct Workspace {
@@ -106,9 +110,8 @@ struct Workspace {
   float* t1;              // [kPlaneGroup][B][nsrc][HW][4] omega conv3x3 output per group plane
   float* u0;              // [B,16,H/2,W/2] deconv_0 output (pre-GN)
   float* u1;              // [B,16,H,W]     deconv_1 output (pre-GN)
-  float* h[5][3];         // hidden states: a ring of kHRing[k] slots (plane d reads slot d % r
-                          // and writes slot (d + 1) % r); h0 has 3 (read by cell 4 two stream
-                          // stages after cell 0 writes it), the others 2
+  float* h[5][kHRingMax]; // hidden states: a ring of kHRing[k] slots (plane d reads slot d % r
+                          // and writes slot (d + 1) % r)
   float* c[5];            // cell states (updated in place)
   size_t bytes;
   size_t omega_stats_bytes;  // one plane
@@ -199,12 +202,11 @@ TrainLayout train_layout(int B, int H, int W);
 UnetIO unet_io_ws(const Workspace& ws, int d);   // plane d (absolute index in the sweep)
 UnetIO unet_io_record(const TrainLayout& T, const aarmvs_train_record& r, int d);
 
-// stages: the step's four parts (kUnetP0..P3, run in that order); a part of plane d reads only
-// the earlier parts' outputs of plane d and its own state, so the parts of neighbouring planes
-// may run at once on different streams (the sweep's multi-stream regulariser)
-constexpr int kUnetP0 = 1, kUnetP1 = 2, kUnetP2 = 4, kUnetP3 = 8;   // cells 0-1 | cell 2 |
-                                                                     // deconv_0 + cell 3 | deconv_1 + cell 4
-constexpr int kUnetFront = kUnetP0 | kUnetP1, kUnetBack = kUnetP2 | kUnetP3, kUnetAll = 15;
+// stages: the step's five units (bit u = unit u, run in that order: cell 0 | cell 1 | cell 2 |
+// deconv_0 + cell 3 | deconv_1 + cell 4); a unit of plane d reads only the earlier units'
+// outputs of plane d and its own state, so the units of neighbouring planes may run at once on
+// different streams (the sweep's multi-stream regulariser)
+constexpr int kUnetUnits = 5, kUnetAll = (1 << kUnetUnits) - 1;
 hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom& g,
                             const Workspace& ws, const UnetIO& io, hipStream_t s,
                             int stages = kUnetAll);

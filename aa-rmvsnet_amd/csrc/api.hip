@@ -194,7 +194,7 @@ Workspace carve_workspace(void* base, int B, int H, int W, int nsrc) {
   const size_t cell_px[5] = {HW, HW2, HW4, HW2, HW};
   for (int k = 0; k < 5; ++k) {
     const size_t n = (size_t)B * kCellHid[k] * cell_px[k] * 4;
-    for (int r = 0; r < 3; ++r) ws.h[k][r] = r < kHRing[k] ? reinterpret_cast<float*>(take(n)) : nullptr;
+    for (int r = 0; r < kHRingMax; ++r) ws.h[k][r] = r < kHRing[k] ? reinterpret_cast<float*>(take(n)) : nullptr;
     ws.c[k] = reinterpret_cast<float*>(take(n));
   }
   ws.state_bytes = off - state_begin;
@@ -566,27 +566,48 @@ float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int plan
 
 }  // extern "C"
 
-// Multi-stream regulariser (eval sweeps).  The U-Net step is four parts run in order (P0: cells
-// 0-1, P1: cell 2, P2: deconv_0 + cell 3, P3: deconv_1 + cell 4 and the head); a part of plane d
-// needs the earlier parts of plane d and its own state only, so the parts of neighbouring planes
-// can run at once on different streams: with 2 streams P0-P1 | P2-P3, with 3 streams P0 | P1-P2 |
-// P3, the later streams library-owned.  Per part and plane an event (a ring of 4 per part):
-//   data: a part waits for the previous part of its plane when that ran on another stream;
-//   slots: a part that overwrites a hidden-state slot waits for that slot's readers on other
-//   streams kHRing planes back (P0 writes h0 (ring 3, read by P3) and h1 (read by P1, P2); P1
-//   writes h2 (read by P2); P2 writes h3 (read by P3)).
-// Bit-identical to one stream (the same kernels on the same inputs).  AARMVS_REG_STREAMS=1/2/3
-// forces the count; by default 3 whenever the caller asks for concurrency (an aux stream).
-constexpr int kRegMaxStreams = 3, kRegEvRing = 4;
-static int reg_streams(bool aux) {
-  const char* s = std::getenv("AARMVS_REG_STREAMS");
+// Multi-stream regulariser.  The U-Net step is five units run in order (U0 cell 0, U1 cell 1,
+// U2 cell 2, U3 deconv_0 + cell 3, U4 deconv_1 + cell 4 and the head); a unit of plane d needs
+// the earlier units of plane d and its own state only, so the units of neighbouring planes can
+// run at once on different streams (stream 0 the caller's, the others library-owned).  Per unit
+// and plane an event (a ring of kRegEvRing per unit):
+//   data: a unit waits for the previous unit of its plane when that ran on another stream;
+//   slots: unit k < 4 overwrites h_k's slot of plane d - kHRing[k]; it waits for that plane's
+//   last reader of h_k when that ran on another stream (h0: U4, h1: U3, h2: U3, h3: U4; h4 is
+//   read by U4's own head).  The other readers of the slot finished before the last one (the
+//   data waits chain a plane's units).  c_k, u0, u1, the deconv partials and the WTA images
+//   each have one unit as their only reader and writer.
+// Bit-identical to one stream (the same kernels on the same inputs).  AARMVS_REG_STREAMS=1..5
+// forces the count (AARMVS_REG_STREAMS_REC for a training forward) and AARMVS_REG_MAP (five
+// digits, unit -> stream, unit 0 on stream 0) the assignment; by default 3 streams whenever the
+// caller asks for concurrency (an aux stream).
+constexpr int kRegMaxStreams = 5, kRegEvRing = 8;
+static_assert(kRegEvRing > kHRingMax, "a unit's event is re-recorded only after its waiters are enqueued");
+constexpr int kHLastReader[4] = {4, 3, 3, 4};
+static int reg_streams(bool aux, bool rec) {
+  const char* s = std::getenv(rec ? "AARMVS_REG_STREAMS_REC" : "AARMVS_REG_STREAMS");
   const int n = (s && *s) ? std::atoi(s) : (aux ? 3 : 1);
   return std::max(1, std::min(kRegMaxStreams, n));
 }
-// the stream of each part for n streams
-static void reg_part_streams(int n, int (&ps)[4]) {
-  static const int map[kRegMaxStreams][4] = {{0, 0, 0, 0}, {0, 0, 1, 1}, {0, 1, 1, 2}};
-  for (int i = 0; i < 4; ++i) ps[i] = map[n - 1][i];
+// the stream of each unit for n streams; returns the number of streams used
+static int reg_unit_streams(int n, int (&us)[kUnetUnits]) {
+  static const int map[kRegMaxStreams][kUnetUnits] = {
+      {0, 0, 0, 0, 0}, {0, 0, 0, 1, 1}, {0, 0, 1, 1, 2}, {0, 1, 1, 2, 3}, {0, 1, 2, 3, 4}};
+  for (int i = 0; i < kUnetUnits; ++i) us[i] = map[n - 1][i];
+  const char* m = n > 1 ? std::getenv("AARMVS_REG_MAP") : nullptr;
+  if (m && std::strlen(m) == kUnetUnits && m[0] == '0') {
+    int top = 0;
+    bool ok = true;
+    for (int i = 0; i < kUnetUnits; ++i) {
+      ok = ok && m[i] >= '0' && m[i] < '0' + kRegMaxStreams;
+      top = std::max(top, m[i] - '0');
+    }
+    if (ok) {
+      for (int i = 0; i < kUnetUnits; ++i) us[i] = m[i] - '0';
+      return top + 1;
+    }
+  }
+  return n;
 }
 
 // planes per cost-stage group: kPlaneGroup, or AARMVS_NPL=n (1 <= n <= kPlaneGroup; A/B runs)
@@ -632,19 +653,18 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   // group parity two events: ev_cost[p] "group's slices ready" (aux -> main) and
   // ev_used[p] "group's slices consumed" (main -> aux, before group i+2 reuses the slots).
   hipStream_t aux = (a->aux_stream && a->aux_stream != stream) ? a->aux_stream : nullptr;
-  // (a training forward, with its record, stays on one stream: 3 streams measured 254 -> 894 ms
-  // per config-4 training step)
-  const int nreg = rec ? 1 : reg_streams(aux != nullptr);
-  int pstream[4];
-  reg_part_streams(nreg, pstream);
+  // (a training forward, with its record: AARMVS_REG_STREAMS_REC; 3 streams by default too,
+  // config-4 training step 251.4 -> 243.3 ms, profiles/r06m_train_streams.txt)
+  int ustream[kUnetUnits];
+  const int nreg = reg_unit_streams(reg_streams(aux != nullptr, rec != nullptr), ustream);
   const int G = plane_group();
   // ev_cost[2], ev_used[2], fork/join, and the regulariser's part events, fork/join events and
-  // streams: a per-thread, per-device set reused across calls (a training forward makes one
-  // call per plane).  Events are only recorded/waited on the caller's streams and the set's
+  // streams: a per-thread, per-device set reused across calls (a sweep split into d_range
+  // pieces makes one call per piece).  Events are only recorded/waited on the caller's streams and the set's
   // own, and a record overwrites the previous one, so reuse is safe.
   struct EventSet {
     int dev = -1;
-    hipEvent_t ev[5 + 4 * kRegEvRing + kRegMaxStreams] = {};
+    hipEvent_t ev[5 + kUnetUnits * kRegEvRing + kRegMaxStreams] = {};
     hipStream_t reg[kRegMaxStreams] = {};
   };
   static thread_local EventSet evs_dev[kMaxDevices];   // one set per device
@@ -657,16 +677,18 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     for (hipEvent_t& x : evs.ev)
       if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
         return sweep_fail(e, "sweep: event create");
-    for (int i = 1; i < kRegMaxStreams; ++i)
-      if ((e = hipStreamCreateWithFlags(&evs.reg[i], hipStreamNonBlocking)) != hipSuccess)
-        return sweep_fail(e, "sweep: stream create");
     evs.dev = dev;
   }
+  // the library's streams, created when first used (each may hold a hardware queue)
+  for (int i = 1; i < nreg; ++i)
+    if (!evs.reg[i] && (e = hipStreamCreateWithFlags(&evs.reg[i], hipStreamNonBlocking)) != hipSuccess)
+      return sweep_fail(e, "sweep: stream create");
   hipEvent_t* ev_cost = ev;
   hipEvent_t* ev_used = ev + 2;
   hipEvent_t(*ev_part)[kRegEvRing] = reinterpret_cast<hipEvent_t(*)[kRegEvRing]>(ev + 5);
-  hipEvent_t* ev_regjoin = ev + 5 + 4 * kRegEvRing;
-  hipStream_t rs[kRegMaxStreams] = {stream, nreg > 1 ? evs.reg[1] : nullptr, nreg > 2 ? evs.reg[2] : nullptr};
+  hipEvent_t* ev_regjoin = ev + 5 + kUnetUnits * kRegEvRing;
+  hipStream_t rs[kRegMaxStreams] = {stream};
+  for (int i = 1; i < nreg; ++i) rs[i] = evs.reg[i];
   hipStream_t cs = aux ? aux : stream;   // the cost stage's stream
 
   if (a->d_begin == 0) {
@@ -708,8 +730,11 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   // every return from here on (errors included) leaves the aux and regulariser streams' work
   // ordered on `stream`
   StreamJoin join{stream, aux, ev[4]};
-  StreamJoin join_r1{stream, rs[1], ev_regjoin[1]};
-  StreamJoin join_r2{stream, rs[2], ev_regjoin[2]};
+  StreamJoin join_r[kRegMaxStreams] = {{stream, nullptr, nullptr},
+                                       {stream, rs[1], ev_regjoin[1]},
+                                       {stream, rs[2], ev_regjoin[2]},
+                                       {stream, rs[3], ev_regjoin[3]},
+                                       {stream, rs[4], ev_regjoin[4]}};
   // the WTA images are maintained on every plane, whether or not this call returns depth:
   // a sweep split into d_range calls gives the same depth/confidence however its earlier
   // pieces were requested (24 B/px per plane, <0.5% of a plane's time)
@@ -749,29 +774,25 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         if (e != hipSuccess) return sweep_fail(e, "sweep: slice copy");
       }
       if (nreg > 1) {
-        // wait for part q of plane e on another stream (planes before this call: joined)
-        auto wait_part = [&](int p, int q, int e) -> hipError_t {
-          if (e < a->d_begin || pstream[q] == pstream[p]) return hipSuccess;
-          return hipStreamWaitEvent(rs[pstream[p]], ev_part[q][e % kRegEvRing], 0);
+        // wait for unit q of plane e on another stream (planes before this call: joined)
+        auto wait_unit = [&](int u, int q, int e) -> hipError_t {
+          if (e < a->d_begin || ustream[q] == ustream[u]) return hipSuccess;
+          return hipStreamWaitEvent(rs[ustream[u]], ev_part[q][e % kRegEvRing], 0);
         };
         UnetIO iom = io;
         iom.clear_stats = false;   // the statistics are stored, never accumulated (one writer each)
-        for (int p = 0; p < 4; ++p) {
-          hipStream_t sp = rs[pstream[p]];
-          if (p > 0 && (e = wait_part(p, p - 1, d)) != hipSuccess) return sweep_fail(e, "sweep: event wait");
-          // the hidden-state slots this part overwrites, last read kHRing planes back
-          if (p == 0 && ((e = wait_part(0, 3, d - kHRing[0])) != hipSuccess ||
-                         (e = wait_part(0, 1, d - kHRing[1])) != hipSuccess ||
-                         (e = wait_part(0, 2, d - kHRing[1])) != hipSuccess))
+        for (int u = 0; u < kUnetUnits; ++u) {
+          hipStream_t su = rs[ustream[u]];
+          if (u > 0 && (e = wait_unit(u, u - 1, d)) != hipSuccess) return sweep_fail(e, "sweep: event wait");
+          // the hidden-state slot this unit overwrites, last read kHRing planes back
+          if (u < 4 && (e = wait_unit(u, kHLastReader[u], d - kHRing[u])) != hipSuccess)
             return sweep_fail(e, "sweep: event wait");
-          if (p == 1 && (e = wait_part(1, 2, d - kHRing[2])) != hipSuccess) return sweep_fail(e, "sweep: event wait");
-          if (p == 2 && (e = wait_part(2, 3, d - kHRing[3])) != hipSuccess) return sweep_fail(e, "sweep: event wait");
-          if ((e = launch_unet_step(xd, params, g, ws, iom, sp, 1 << p)) != hipSuccess)
+          if ((e = launch_unet_step(xd, params, g, ws, iom, su, 1 << u)) != hipSuccess)
             return sweep_fail(e, "sweep: regulariser step");
-          if (p == 3 && (e = launch_head_wta(params, g, iom, ws, a->depth_values, d, a->cost_out, wta, sp)) !=
-                            hipSuccess)
+          if (u == kUnetUnits - 1 &&
+              (e = launch_head_wta(params, g, iom, ws, a->depth_values, d, a->cost_out, wta, su)) != hipSuccess)
             return sweep_fail(e, "sweep: head/wta");
-          if ((e = hipEventRecord(ev_part[p][d % kRegEvRing], sp)) != hipSuccess)
+          if ((e = hipEventRecord(ev_part[u][d % kRegEvRing], su)) != hipSuccess)
             return sweep_fail(e, "sweep: event record");
         }
         continue;
@@ -791,8 +812,8 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
         (e = hipStreamWaitEvent(stream, ev[4], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: join");
   }
-  if ((e = join_r1.join()) != hipSuccess || (e = join_r2.join()) != hipSuccess)
-    return sweep_fail(e, "sweep: join");
+  for (int i = 1; i < nreg; ++i)
+    if ((e = join_r[i].join()) != hipSuccess) return sweep_fail(e, "sweep: join");
   if ((a->depth_out || a->conf_out) && a->d_end == a->D) {
     if ((e = launch_finalize(g, ws, a->depth_out, a->conf_out, stream)) != hipSuccess)
       return sweep_fail(e, "sweep: finalize");

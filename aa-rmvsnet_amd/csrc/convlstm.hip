@@ -1379,18 +1379,20 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     a.c_in += b * hid * px;
     if (a.z_out) a.z_out += b * 4 * hid * px;
   };
-  if (stages & kUnetP0) {
+  if (stages & 1) {
   // cell 0: [x, h0] @ H
   CellArgs a0 = cell(0, {{x, 32, SRC_PLAIN, nullptr, nullptr, nullptr},
                          {io.h_prev[0], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
   a0.xbound = ws.xbound;
   if ((e = run_cell_h3<0>(a0, params + L.h3_scale_off + 0, cu, K_CELL0, s)) != hipSuccess) return e;
+  }
+  if (stages & 2) {
   // cell 1: [maxpool(h0'), h1] @ H/2
   CellArgs a1 = cell(1, {{io.h_new[0], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {io.h_prev[1], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 2);
   if ((e = run_cell_h3<1>(a1, params + L.h3_scale_off + 1, cu, K_CELL1, s)) != hipSuccess) return e;
   }
-  if (stages & kUnetP1) {
+  if (stages & 4) {
   // cell 2: [maxpool(h1'), h2] @ H/4
   CellArgs a2 = cell(2, {{io.h_new[1], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {io.h_prev[2], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
@@ -1399,7 +1401,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   // GroupNorm statistics are per batch element, so the two cells that consume the deconvs'
   // normalised outputs are launched per batch element; each reduces its element's deconv
   // partials itself (gn_table) and block 0 stores the statistics.
-  if (stages & kUnetP2) {
+  if (stages & 8) {
   // deconv_0: h2' (H/4) -> u0 (H/2) + GN stats
   int nblk0 = 0;
   {
@@ -1427,7 +1429,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
     if ((e = run_cell_h3<3>(a3, params + L.h3_scale_off + 3, cu, K_CELL3, s)) != hipSuccess) return e;
   }
   }
-  if (!(stages & kUnetP3)) return hipSuccess;
+  if (!(stages & 16)) return hipSuccess;
   // deconv_1: h3' (H/2) -> u1 (H) + GN stats
   int nblk1 = 0;
   {

@@ -139,12 +139,15 @@ typedef struct aarmvs_sweep_args {
                                              are computed in groups of up to 16 planes, and
                                              the next group's (omega conv, GroupNorm
                                              statistics, cost_x) run on it beside the current
-                                             group's regulariser steps (events per group); an
-                                             eval sweep with it also runs the back of each
-                                             plane's U-Net step (deconvs, cells 3-4, head) on a
-                                             library-owned stream beside the front (cells 0-2)
-                                             of the next plane.  At return all work is ordered
-                                             on `stream`; results are bit-identical either way */
+                                             group's regulariser steps (events per group); a
+                                             sweep with it also spreads each plane's U-Net
+                                             step (five units: cell 0 | cell 1 | cell 2 |
+                                             deconv_0, cell 3 | deconv_1, cell 4, head) over
+                                             `stream` and library-owned streams, so that the
+                                             units of neighbouring planes run at once (events
+                                             per unit and plane).  At return all work is
+                                             ordered on `stream`; results are bit-identical
+                                             either way */
   const aarmvs_train_record* record;      /* training record, or NULL (eval): the cost
                                              slices and regulariser tensors of the planes
                                              d_begin..d_end-1 go to its slabs           */

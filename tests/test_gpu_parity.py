@@ -261,15 +261,20 @@ def test_two_stream_schedule_is_bit_identical():
     assert torch.equal(a["depth"], c["depth"]) and torch.equal(a["conf"], c["conf"])
 
 
-@pytest.mark.parametrize("nreg", ["2", "3"])
+@pytest.mark.parametrize("nreg", ["2", "3", "4", "5", "5:02121"])
 @pytest.mark.parametrize("B,N,H,W,D", [(1, 3, 128, 160, 37), (2, 4, 64, 96, 5)])
 def test_multi_stream_regulariser_is_bit_identical(monkeypatch, B, N, H, W, D, nreg):
-    """The U-Net step's parts of neighbouring planes on the library's streams
-    (AARMVS_REG_STREAMS=2: cells 0-2 | deconvs, cells 3-4, head; 3: cells 0-1 | cell 2,
-    deconv_0, cell 3 | deconv_1, cell 4, head) against the one-stream order: bit-identical cost
-    volume, depth and confidence, also over continued d_ranges whose boundaries fall inside and
-    at the end of plane groups, with and without the cost-stage stream (config 1's 160x128 at
-    D=37 crosses three plane groups)."""
+    """The U-Net step's five units (cell 0 | cell 1 | cell 2 | deconv_0, cell 3 | deconv_1,
+    cell 4, head) of neighbouring planes on the library's streams (AARMVS_REG_STREAMS=2: cells
+    0-2 | the rest; 3: cells 0-1 | cell 2, deconv_0, cell 3 | deconv_1, cell 4, head; 4: cell 1
+    and cell 2 share a stream; 5: one unit per stream; "5:02121" an assignment out of unit order,
+    AARMVS_REG_MAP) against the one-stream order: bit-identical cost volume, depth and
+    confidence, also over continued d_ranges whose boundaries fall inside and at the end of
+    plane groups, with and without the cost-stage stream (config 1's 160x128 at D=37 crosses
+    three plane groups)."""
+    nreg, _, umap = nreg.partition(":")
+    if umap:
+        monkeypatch.setenv("AARMVS_REG_MAP", umap)
     from aarmvs import ops
     sc = syn.scene(B, N, H, W, D, seed=21)
     feats = torch.from_numpy(sc["features"]).to(DEV)
