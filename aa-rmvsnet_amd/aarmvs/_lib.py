@@ -102,6 +102,7 @@ SIGNATURES = {
                                           c_void_p, c_void_p, c_void_p]),
     "aarmvs_sweep_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "aarmvs_sweep": (c_int, [ctypes.POINTER(SweepArgs), c_void_p]),
+    "aarmvs_aux_stream": (c_int, [ctypes.POINTER(c_void_p)]),
     "aarmvs_train_record_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "aarmvs_backward_scratch_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "aarmvs_sweep_backward": (c_int, [ctypes.POINTER(BackwardArgs), c_void_p]),

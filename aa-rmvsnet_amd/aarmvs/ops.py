@@ -373,6 +373,18 @@ def wta_update(cost: torch.Tensor, depth_d: torch.Tensor, max_prob: torch.Tensor
                                   _stream()), "wta_update")
 
 
+def aux_stream(device) -> torch.cuda.ExternalStream:
+    """The library's aux stream of ``device`` (aarmvs_aux_stream): one per device, shared by every
+    DepthSweep.  The process gets four hardware queues and streams beyond four share them (a
+    stream's event wait then stalls its queue partner); with this stream, the default stream and
+    the library's two unit / backward streams, a sweep or a training step uses exactly four."""
+    device = torch.device(device)
+    ptr = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        check(lib().aarmvs_aux_stream(ctypes.byref(ptr)), "aux_stream")
+    return torch.cuda.ExternalStream(ptr.value, device=device)
+
+
 class DepthSweep:
     """Runs EMVSNet's depth loop (drmvsnet.py:273-291 / :306-342) on the HIP library.
 
@@ -396,7 +408,7 @@ class DepthSweep:
     @overlap.setter
     def overlap(self, on: bool):
         if on and self._aux is None:
-            self._aux = torch.cuda.Stream(device=self.device)
+            self._aux = aux_stream(self.device)
         elif not on:
             self._aux = None
 

@@ -276,6 +276,15 @@ inline hipError_t ensure_dyn_lds(const void* fn, int bytes, bool (&done)[kMaxDev
   if (e == hipSuccess) done[dev] = true;
   return e;
 }
+// The library's own streams (i = 1 .. kLibStreams), created on first use per device and shared
+// by every call of the process, from any host thread (sweeps: the regulariser's unit streams;
+// backward: the plane pipeline's and the group stage's).  A process gets GPU_MAX_HW_QUEUES = 4
+// hardware queues here and every stream it creates holds one, so streams beyond four share a
+// queue, where one stream's event wait stalls the other's work: the library keeps the process's
+// total (the caller's stream and aux stream included) at four.  Calls on different host threads
+// that share a stream are only ordered, never mixed: each call's events are its thread's own.
+constexpr int kLibStreams = 4;   // 1-3: unit / backward streams; 4: aarmvs_aux_stream
+hipError_t library_stream(int dev, int i, hipStream_t& out);
 // Joins an auxiliary stream back into the caller's stream when it goes out of scope: on every
 // return after a fork (errors included), nothing the call enqueued on the aux stream is left
 // unordered with the caller's stream, whose buffers the caller may free on an error.

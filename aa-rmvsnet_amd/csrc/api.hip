@@ -556,6 +556,14 @@ size_t aarmvs_train_record_bytes(int B, int H, int W, int which) {
   }
 }
 
+int aarmvs_aux_stream(hipStream_t* out) {
+  if (!out) return fail(AARMVS_ERR_INVALID, "aux_stream: null out");
+  int dev = 0;
+  hipError_t e = current_device(dev);
+  if (e == hipSuccess) e = library_stream(dev, kLibStreams, *out);
+  return e == hipSuccess ? AARMVS_OK : hip_fail(e, "aux_stream");
+}
+
 float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int planes,
                         int cell, int which) {
   if (!workspace || cell < 0 || cell > 4 || planes < 0 || check_geom(B, H, W, nsrc) != AARMVS_OK)
@@ -577,22 +585,38 @@ float* aarmvs_state_ptr(void* workspace, int B, int H, int W, int nsrc, int plan
 //   read by U4's own head).  The other readers of the slot finished before the last one (the
 //   data waits chain a plane's units).  c_k, u0, u1, the deconv partials and the WTA images
 //   each have one unit as their only reader and writer.
-// Bit-identical to one stream (the same kernels on the same inputs).  AARMVS_REG_STREAMS=1..5
-// forces the count (AARMVS_REG_STREAMS_REC for a training forward) and AARMVS_REG_MAP (five
-// digits, unit -> stream, unit 0 on stream 0) the assignment; by default 3 streams whenever the
-// caller asks for concurrency (an aux stream).
+// Bit-identical to one stream (the same kernels on the same inputs).
+// How many streams: a process gets GPU_MAX_HW_QUEUES = 4 hardware queues here, and streams
+// beyond that share them (a stream waiting on an event then blocks the other's work), so a
+// sweep uses at most four: with an aux stream (the caller asks for concurrency), the cost stage
+// on it and the units on three (the caller's + two library streams: cells 0-1 | cell 2,
+// deconv_0, cell 3 | deconv_1, cell 4, head).  Small frames (B*H*W <= kSmallFramePx) instead
+// put the cost stage on the caller's stream beside cells 0-1 and the other units on the aux
+// stream and two library streams (cell 2 | deconv_0, cell 3 | deconv_1, cell 4, head), still
+// four streams (the library's are shared with the backward, library_stream): their kernels are a few
+// microseconds of one or two tiles per block, so the chain's latency, not the cost stage, is
+// what overlapping hides (config 1: 0.279 -> 0.334 G hyp/s, profiles/r06o_small_frames.txt).
+// Overrides (A/B runs): AARMVS_REG_STREAMS=1..5 the unit stream count (AARMVS_REG_STREAMS_REC for
+// a training forward), AARMVS_REG_MAP five digits unit -> stream (unit 0 on stream 0),
+// AARMVS_SMALL_PX the small-frame threshold.
 constexpr int kRegMaxStreams = 5, kRegEvRing = 8;
+static_assert(kRegMaxStreams - 1 <= kLibStreams, "the unit streams beyond the caller's are library streams");
 static_assert(kRegEvRing > kHRingMax, "a unit's event is re-recorded only after its waiters are enqueued");
 constexpr int kHLastReader[4] = {4, 3, 3, 4};
-static int reg_streams(bool aux, bool rec) {
+constexpr long kSmallFramePx = 65536;
+static bool small_frame(long px) {
+  const char* s = std::getenv("AARMVS_SMALL_PX");
+  return px <= ((s && *s) ? std::atol(s) : kSmallFramePx);
+}
+static int reg_streams(bool aux, bool rec, bool small) {
   const char* s = std::getenv(rec ? "AARMVS_REG_STREAMS_REC" : "AARMVS_REG_STREAMS");
-  const int n = (s && *s) ? std::atoi(s) : (aux ? 3 : 1);
+  const int n = (s && *s) ? std::atoi(s) : (!aux ? 1 : small ? 4 : 3);
   return std::max(1, std::min(kRegMaxStreams, n));
 }
 // the stream of each unit for n streams; returns the number of streams used
 static int reg_unit_streams(int n, int (&us)[kUnetUnits]) {
   static const int map[kRegMaxStreams][kUnetUnits] = {
-      {0, 0, 0, 0, 0}, {0, 0, 0, 1, 1}, {0, 0, 1, 1, 2}, {0, 1, 1, 2, 3}, {0, 1, 2, 3, 4}};
+      {0, 0, 0, 0, 0}, {0, 0, 0, 1, 1}, {0, 0, 1, 1, 2}, {0, 0, 1, 2, 3}, {0, 1, 2, 3, 4}};
   for (int i = 0; i < kUnetUnits; ++i) us[i] = map[n - 1][i];
   const char* m = n > 1 ? std::getenv("AARMVS_REG_MAP") : nullptr;
   if (m && std::strlen(m) == kUnetUnits && m[0] == '0') {
@@ -615,6 +639,22 @@ static int plane_group() {
   const char* s = std::getenv("AARMVS_NPL");
   const int n = (s && *s) ? std::atoi(s) : kPlaneGroup;
   return std::max(1, std::min(kPlaneGroup, n));
+}
+
+hipError_t aarmvs::library_stream(int dev, int i, hipStream_t& out) {
+  static std::mutex mu;
+  static hipStream_t pool[kMaxDevices][kLibStreams + 1] = {};
+  if (dev < 0 || dev >= kMaxDevices || i < 1 || i > kLibStreams) return hipErrorInvalidValue;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!pool[dev][i]) {
+    hipError_t e = hipStreamCreateWithFlags(&pool[dev][i], hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      pool[dev][i] = nullptr;
+      return e;
+    }
+  }
+  out = pool[dev][i];
+  return hipSuccess;
 }
 
 extern "C" {
@@ -655,8 +695,15 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   hipStream_t aux = (a->aux_stream && a->aux_stream != stream) ? a->aux_stream : nullptr;
   // (a training forward, with its record: AARMVS_REG_STREAMS_REC; 3 streams by default too,
   // config-4 training step 251.4 -> 243.3 ms, profiles/r06m_train_streams.txt)
+  const bool small = aux && small_frame((long)a->B * a->H * a->W);
   int ustream[kUnetUnits];
-  const int nreg = reg_unit_streams(reg_streams(aux != nullptr, rec != nullptr), ustream);
+  const int nreg = reg_unit_streams(reg_streams(aux != nullptr, rec != nullptr, small), ustream);
+  // small frames: the cost stage on the caller's stream, the aux stream one of the units' streams
+  hipStream_t unit_aux = nullptr;
+  if (small && nreg > 3) {
+    unit_aux = aux;
+    aux = nullptr;
+  }
   const int G = plane_group();
   // ev_cost[2], ev_used[2], fork/join, and the regulariser's part events, fork/join events and
   // streams: a per-thread, per-device set reused across calls (a sweep split into d_range
@@ -665,7 +712,6 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   struct EventSet {
     int dev = -1;
     hipEvent_t ev[5 + kUnetUnits * kRegEvRing + kRegMaxStreams] = {};
-    hipStream_t reg[kRegMaxStreams] = {};
   };
   static thread_local EventSet evs_dev[kMaxDevices];   // one set per device
   auto sweep_fail = [&](hipError_t err, const char* where) { return hip_fail(err, where); };
@@ -673,22 +719,24 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   if ((e = current_device(dev)) != hipSuccess) return sweep_fail(e, "sweep: get device");
   EventSet& evs = evs_dev[dev];
   hipEvent_t* ev = evs.ev;
-  if ((aux || nreg > 1) && evs.dev != dev) {
+  if ((aux || unit_aux || nreg > 1) && evs.dev != dev) {
     for (hipEvent_t& x : evs.ev)
       if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
         return sweep_fail(e, "sweep: event create");
     evs.dev = dev;
   }
-  // the library's streams, created when first used (each may hold a hardware queue)
-  for (int i = 1; i < nreg; ++i)
-    if (!evs.reg[i] && (e = hipStreamCreateWithFlags(&evs.reg[i], hipStreamNonBlocking)) != hipSuccess)
-      return sweep_fail(e, "sweep: stream create");
   hipEvent_t* ev_cost = ev;
   hipEvent_t* ev_used = ev + 2;
   hipEvent_t(*ev_part)[kRegEvRing] = reinterpret_cast<hipEvent_t(*)[kRegEvRing]>(ev + 5);
   hipEvent_t* ev_regjoin = ev + 5 + kUnetUnits * kRegEvRing;
   hipStream_t rs[kRegMaxStreams] = {stream};
-  for (int i = 1; i < nreg; ++i) rs[i] = evs.reg[i];
+  for (int i = 1, li = 1; i < nreg; ++i) {
+    if (i == 1 && unit_aux) {
+      rs[1] = unit_aux;
+      continue;
+    }
+    if ((e = library_stream(dev, li++, rs[i])) != hipSuccess) return sweep_fail(e, "sweep: stream create");
+  }
   hipStream_t cs = aux ? aux : stream;   // the cost stage's stream
 
   if (a->d_begin == 0) {

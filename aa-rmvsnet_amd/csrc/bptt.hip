@@ -1519,7 +1519,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
   // Makefile) gave results that depended on what ran beside it.
   struct PipeSet {
     int dev = -1;
-    hipStream_t aux = nullptr, grp = nullptr;
+    hipStream_t aux = nullptr, grp = nullptr;   // the library's streams 1 and 2 (library_stream)
     hipEvent_t ev[9] = {};   // evA[2], evB[2], fork, evP, evG[2], group join
   };
   static thread_local PipeSet ps_dev[kMaxDevices];   // aux streams + events per device
@@ -1535,8 +1535,8 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
   const hipStream_t sg0 = s;   // the caller's stream
   if (pipe_on && !g_prof_on) {   // (per-kernel timing runs on one stream: isolated kernel spans)
     if (ps.dev != dev) {
-      CK(hipStreamCreateWithFlags(&ps.aux, hipStreamNonBlocking));
-      CK(hipStreamCreateWithFlags(&ps.grp, hipStreamNonBlocking));
+      CK(library_stream(dev, 1, ps.aux));
+      CK(library_stream(dev, 2, ps.grp));
       for (hipEvent_t& x : ps.ev) CK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
       ps.dev = dev;
     }

@@ -145,9 +145,11 @@ typedef struct aarmvs_sweep_args {
                                              deconv_0, cell 3 | deconv_1, cell 4, head) over
                                              `stream` and library-owned streams, so that the
                                              units of neighbouring planes run at once (events
-                                             per unit and plane).  At return all work is
-                                             ordered on `stream`; results are bit-identical
-                                             either way */
+                                             per unit and plane; at most four streams in all,
+                                             and for small frames, B*H*W <= 65536, the cost
+                                             stage moves to `stream` so that the units get
+                                             four).  At return all work is ordered on
+                                             `stream`; results are bit-identical either way */
   const aarmvs_train_record* record;      /* training record, or NULL (eval): the cost
                                              slices and regulariser tensors of the planes
                                              d_begin..d_end-1 go to its slabs           */
@@ -155,6 +157,11 @@ typedef struct aarmvs_sweep_args {
 
 size_t aarmvs_sweep_workspace_bytes(int B, int H, int W, int nsrc);
 int aarmvs_sweep(const aarmvs_sweep_args* args, hipStream_t stream);
+/* A stream for aux_stream owned by the library (one per device, created on first use, never
+ * destroyed): a process gets four hardware queues and streams beyond four share them, so a
+ * caller without streams of its own passes this one rather than creating a fifth (the library's
+ * other streams are its two to three unit / backward streams).  *out: the current device's. */
+int aarmvs_aux_stream(hipStream_t* out);
 
 /* ---------------------------------------------------------------------------
  * Backward of a training sweep (the BPTT through drmvsnet.py:273-291): given the record

@@ -261,7 +261,7 @@ def test_two_stream_schedule_is_bit_identical():
     assert torch.equal(a["depth"], c["depth"]) and torch.equal(a["conf"], c["conf"])
 
 
-@pytest.mark.parametrize("nreg", ["2", "3", "4", "5", "5:02121"])
+@pytest.mark.parametrize("nreg", ["default", "2", "3", "4", "5", "5:02121"])
 @pytest.mark.parametrize("B,N,H,W,D", [(1, 3, 128, 160, 37), (2, 4, 64, 96, 5)])
 def test_multi_stream_regulariser_is_bit_identical(monkeypatch, B, N, H, W, D, nreg):
     """The U-Net step's five units (cell 0 | cell 1 | cell 2 | deconv_0, cell 3 | deconv_1,
@@ -271,7 +271,8 @@ def test_multi_stream_regulariser_is_bit_identical(monkeypatch, B, N, H, W, D, n
     AARMVS_REG_MAP) against the one-stream order: bit-identical cost volume, depth and
     confidence, also over continued d_ranges whose boundaries fall inside and at the end of
     plane groups, with and without the cost-stage stream (config 1's 160x128 at D=37 crosses
-    three plane groups)."""
+    three plane groups).  "default": the library's choice, which for these small frames (B*H*W
+    <= 65536) is the cost stage on the caller's stream and the units over four streams."""
     nreg, _, umap = nreg.partition(":")
     if umap:
         monkeypatch.setenv("AARMVS_REG_MAP", umap)
@@ -284,7 +285,10 @@ def test_multi_stream_regulariser_is_bit_identical(monkeypatch, B, N, H, W, D, n
     P = P_of(6)
     monkeypatch.setenv("AARMVS_REG_STREAMS", "1")
     ref = ops.DepthSweep(P, DEV, overlap=True)(*args, want_cost=True)
-    monkeypatch.setenv("AARMVS_REG_STREAMS", nreg)
+    if nreg == "default":
+        monkeypatch.delenv("AARMVS_REG_STREAMS")
+    else:
+        monkeypatch.setenv("AARMVS_REG_STREAMS", nreg)
     for overlap in (True, False):
         got = ops.DepthSweep(P, DEV, overlap=overlap)(*args, want_cost=True)
         for k in ("cost", "depth", "conf"):
