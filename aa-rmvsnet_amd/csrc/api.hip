@@ -796,19 +796,20 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
     // cost stage: its slots were last read by group gi - 2's regulariser steps
     if (aux && gi >= 2 && (e = hipStreamWaitEvent(aux, ev_used[gi & 1], 0)) != hipSuccess)
       return sweep_fail(e, "sweep: event wait");
-    if ((e = launch_omega_group(ca, g, ws, g0, n, cs, rec != nullptr)) != hipSuccess)
+    // training: the group's omega conv output and statistics go straight to the record (the
+    // backward reads them instead of recomputing the omega conv; the record's per-plane layout
+    // is the workspace slots')
+    Workspace wsg = ws;
+    if (rec) {
+      wsg.t1 = rec->t1 + (size_t)g0 * ws.t1_plane * 4;
+      wsg.omega_stats = rec->ostats + (size_t)g0 * (ws.omega_stats_bytes / 8);
+    }
+    if ((e = launch_omega_group(ca, g, wsg, g0, n, cs, rec != nullptr)) != hipSuccess)
       return sweep_fail(e, "sweep: omega stage");
     const int ok = d_last < g0 + n ? d_last - g0 : -1;
-    if ((e = launch_cost_x_group(ca, g, ws, g0, n, xs, ok >= 0 ? a->omega_out : nullptr, ok, cs)) !=
+    if ((e = launch_cost_x_group(ca, g, wsg, g0, n, xs, ok >= 0 ? a->omega_out : nullptr, ok, cs)) !=
         hipSuccess)
       return sweep_fail(e, "sweep: cost slices");
-    // training: the group's omega conv output and statistics into the record (the backward
-    // reads them instead of recomputing the omega conv), before the next group reuses the slots
-    if (rec && ((e = hipMemcpyAsync(rec->t1 + (size_t)g0 * ws.t1_plane * 4, ws.t1, (size_t)n * ws.t1_plane * 16,
-                                    hipMemcpyDeviceToDevice, cs)) != hipSuccess ||
-                (e = hipMemcpyAsync(rec->ostats + (size_t)g0 * (ws.omega_stats_bytes / 8), ws.omega_stats,
-                                    (size_t)n * ws.omega_stats_bytes, hipMemcpyDeviceToDevice, cs)) != hipSuccess))
-      return sweep_fail(e, "sweep: record omega");
     if (aux && ((e = hipEventRecord(ev_cost[gi & 1], aux)) != hipSuccess ||
                 (e = hipStreamWaitEvent(stream, ev_cost[gi & 1], 0)) != hipSuccess))
       return sweep_fail(e, "sweep: event");

@@ -2307,18 +2307,16 @@ hipError_t cost_bwd_group(void* ctx, int g0, int n, const float* gx, hipStream_t
   const SweepGeom g{a->B, a->H, a->W, a->nsrc, a->D, cu_count()};
   const CostArgs ca = cost_args_of(a);
   hipError_t e;
-  // the forward's omega conv output and GroupNorm statistics of the group's planes, as the
-  // recorded forward kept them
-  if ((e = hipMemcpyAsync(c.ws.t1, a->record->t1 + (size_t)g0 * c.ws.t1_plane * 4, (size_t)n * c.ws.t1_plane * 16,
-                          hipMemcpyDeviceToDevice, s)) != hipSuccess ||
-      (e = hipMemcpyAsync(c.ws.omega_stats, a->record->ostats + (size_t)g0 * (c.ws.omega_stats_bytes / 8),
-                          (size_t)n * c.ws.omega_stats_bytes, hipMemcpyDeviceToDevice, s)) != hipSuccess)
-    return e;
+  // the forward's omega conv output and GroupNorm statistics of the group's planes, read where
+  // the recorded forward wrote them (the record's per-plane layout is the workspace slots')
+  Workspace ws = c.ws;
+  ws.t1 = a->record->t1 + (size_t)g0 * c.ws.t1_plane * 4;
+  ws.omega_stats = a->record->ostats + (size_t)g0 * (c.ws.omega_stats_bytes / 8);
   CbwArgs ba{};
-  ba.p = pipe_args_c8(ca, g, c.ws);
-  group_strides(ba.p, c.ws, n);
-  ba.p.t1_prev = reinterpret_cast<const float4*>(c.ws.t1);
-  ba.p.st_prev = c.ws.omega_stats;
+  ba.p = pipe_args_c8(ca, g, ws);
+  group_strides(ba.p, ws, n);
+  ba.p.t1_prev = reinterpret_cast<const float4*>(ws.t1);
+  ba.p.st_prev = ws.omega_stats;
   ba.gx = gx;
   ba.go = L.go;
   ba.wo = L.wo;
