@@ -341,7 +341,7 @@ def ceiling_limits():
     latency-bound) and the texture-unit (TA, TD) busy fractions and L1 hit rate for cost_x
     (bound by its gathers through the vector L1)."""
     here = os.path.dirname(os.path.abspath(__file__))
-    for name in ("r05_ceiling_pmc.json", "r04_ceiling_pmc.json", "r03_ceiling_pmc.json"):
+    for name in ("r06_ceiling_pmc.json", "r05_ceiling_pmc.json", "r04_ceiling_pmc.json", "r03_ceiling_pmc.json"):
         path = os.path.join(here, "profiles", name)
         if not os.path.exists(path):
             continue
