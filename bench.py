@@ -351,15 +351,25 @@ def ceiling_limits():
             continue
         out = {"source": "profiles/" + name}
         om, cx = d.get("omega_conv") or {}, d.get("cost_x") or {}
+
+        def valu_pipe(k):
+            # share of the launch's GPU-active cycles a SIMD's VALU is busy: 4 cycles per wave64
+            # VALU instruction, the waves spread over 256 CUs x 4 SIMDs (MI355X)
+            if not (k.get("per_wave_valu") and k.get("waves") and k.get("gui_active_cycles")):
+                return None
+            return round(k["per_wave_valu"] * 4.0 * k["waves"] / 1024.0 / k["gui_active_cycles"], 4)
+
         if om:
             out["omega_conv"] = {k: om[k] for k in ("issue_frac", "dep_stall_frac", "parked_frac", "per_wave_valu")
                                  if k in om}
-            out["omega_conv"]["bound"] = "issue/latency"
+            out["omega_conv"]["valu_pipe_frac"] = valu_pipe(om)
+            out["omega_conv"]["bound"] = "VALU issue" if (valu_pipe(om) or 0) > 0.75 else "issue/latency"
         if cx:
             l1 = 1.0 - cx["tcp_to_l2_read_req"] / cx["tcp_accesses"] if cx.get("tcp_accesses") else None
             out["cost_x"] = {k: cx[k] for k in ("ta_busy_frac", "td_busy_frac", "issue_frac", "parked_frac")
                              if k in cx}
             out["cost_x"]["l1_hit_frac"] = round(l1, 4) if l1 is not None else None
+            out["cost_x"]["valu_pipe_frac"] = valu_pipe(cx)
             out["cost_x"]["bound"] = "L1 gather (TD)"
         return out
     return None
@@ -753,7 +763,7 @@ def main():
         if lim:
             roofline["limits"] = lim
             # what binds the dominant kernel by its counters (the HBM ratio stays in frac):
-            # omega_conv issue/latency, cost_x the vector-L1 gather path
+            # omega_conv the VALU pipe (87% busy), cost_x the vector-L1 gather path
             if dom in lim and lim[dom].get("bound"):
                 roofline["roofline_model"] = r["bound"]
                 roofline["bound"] = lim[dom]["bound"]
