@@ -32,7 +32,7 @@ static void carve(int B, int H, int W, int nsrc) {
   CHECK(bytes > 0);
   std::vector<unsigned char> ws(bytes);
   const int hid[5] = {16, 16, 16, 16, 8}, sc[5] = {1, 2, 4, 2, 1};
-  for (int par = 0; par < 3; ++par)
+  for (int par = 0; par < 8; ++par)   // planes processed: every slot of the rings (up to 6)
     for (int k = 0; k < 5; ++k)
       for (int which = 0; which < 2; ++which) {
         float* p = aarmvs_state_ptr(ws.data(), B, H, W, nsrc, par, k, which);
@@ -74,6 +74,7 @@ int main() {
   float dummy[64] = {};
   const float* srcs[AARMVS_MAX_SRC] = {dummy};
   CHECK(aarmvs_pack_params(nullptr, dummy, nullptr) == AARMVS_ERR_INVALID && has_error());
+  CHECK(aarmvs_aux_stream(nullptr) == AARMVS_ERR_INVALID && has_error());
   CHECK(aarmvs_homo_warp(nullptr, dummy, dummy, 1, 32, 8, 8, dummy, nullptr) == AARMVS_ERR_INVALID);
   CHECK(aarmvs_homo_warp(dummy, dummy, dummy, 1, 32, 1, 8, dummy, nullptr) == AARMVS_ERR_INVALID);
   CHECK(aarmvs_homo_warp_backward(dummy, dummy, dummy, 0, 32, 8, 8, dummy, dummy, nullptr) ==
