@@ -52,6 +52,8 @@ const ParamLayout& param_layout() {
     pk += 64;
     l.owm_off = pk;
     pk += 4 * 3 * 64 * 8 / 2;   // halves -> floats
+    l.owmc_off = pk;
+    pk += 4 * 3 * 64 * 8 / 2;
     for (int k = 0; k < 2; ++k) {
       l.dct_off[k] = pk;
       pk += 16 * 9 * 16;
@@ -339,6 +341,20 @@ __global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __r
     const _Float16 xl2 = (_Float16)(r1 - (float)xl);
     const bool top = (lane >> 5) == 0;   // K rows 0-7: against sq hi
     bm[i] = k == 0 ? xh : k == 1 ? (top ? xl : (_Float16)0.0f) : (top ? xl2 : xl);
+  }
+  // the centre tap (tap 4) in the same fragment form, columns n = co < 4, the others zero
+  // (omega_mfma ABL bit 1024: its own accumulator pair)
+  _Float16* bmc = reinterpret_cast<_Float16*>(pk + L.owmc_off);
+  for (int i = threadIdx.x; i < 4 * 3 * 64 * 8; i += blockDim.x) {
+    const int j = i & 7, lane = (i >> 3) & 63, k = (i >> 9) % 3, c = (i >> 9) / 3;
+    const int n = lane & 31, co = n & 3;
+    const float x = n < 4 ? w[(co * 32 + 8 * c + j) * 9 + 4] * sc : 0.0f;
+    const _Float16 xh = (_Float16)x;
+    const float r1 = x - (float)xh;
+    const _Float16 xl = (_Float16)r1;
+    const _Float16 xl2 = (_Float16)(r1 - (float)xl);
+    const bool top = (lane >> 5) == 0;
+    bmc[i] = k == 0 ? xh : k == 1 ? (top ? xl : (_Float16)0.0f) : (top ? xl2 : xl);
   }
 }
 

@@ -267,6 +267,7 @@ struct PipeArgs {
   const float* params;
   size_t off_owc, off_owb_scale;   // omega conv centre-tap 4x4x4 B operands, the fragments' scale
   size_t off_owm, off_owm_scale;   // omega_mfma's 32x32x16 B fragments, their scale
+  size_t off_owmc;                 // the centre tap's 32x32x16 B fragments (ABL 1024)
   size_t off_ow0t, off_ow0, off_ob0, off_og0w, off_og0b, off_ow1, off_ob1, off_og1w, off_og1b, off_ow2,
       off_ob2, off_og2w, off_og2b, off_owo, off_obo;
   int B, H, W, nsrc;
@@ -909,7 +910,13 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   // parity green): ten dependent 4x4x4 MFMAs per chunk on one accumulator stall the wave more
   // than the 32 FMAs they replace cost (the layout: tools/microbench/mfma4_layout.cpp)
   constexpr bool CMF = (ABL & 512) != 0 && !BAL;
+  // CM32 (ABL bit 1024, diagnostic): the centre tap on the 32x32x16 MFMAs of the off-centre taps'
+  // A operands, with B fragments holding only columns 0-3, into an accumulator pair of its own
+  // (32 more VGPRs: three waves per SIMD instead of four)
+  constexpr bool CM32 = (ABL & 1024) != 0 && !BAL;
   const half8* __restrict__ owc = reinterpret_cast<const half8*>(P + a.off_owc) + 3 * (lane & 3);
+  const half8* __restrict__ owmc = reinterpret_cast<const half8*>(P + a.off_owmc);
+  floatx16 acc2, acc3;
   floatx16 acc0, acc1;   // first written by chunk 0's MFMAs (ABL 1: zero here)
   if constexpr ((ABL & 1) != 0) {
 #pragma unroll
@@ -948,16 +955,21 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     // this chunk's B fragments, issued before the barrier: their L1/L2 latency is hidden
     // behind it and the centre-tap chain (2.5% of the kernel against loading them after;
     // DMA'ing all 12 to LDS once per item instead was 1.8%)
-    half8 Bd, Bl, Bl2;
+    half8 Bd, Bl, Bl2, Cd, Cl, Cl2;
     if constexpr ((ABL & 128) == 0) {
       Bd = owm[(c * 3 + 0) * 64 + lane];
       Bl = owm[(c * 3 + 1) * 64 + lane];
       Bl2 = owm[(c * 3 + 2) * 64 + lane];
     }
+    if constexpr (CM32) {
+      Cd = owmc[(c * 3 + 0) * 64 + lane];
+      Cl = owmc[(c * 3 + 1) * 64 + lane];
+      Cl2 = owmc[(c * 3 + 2) * 64 + lane];
+    }
     __syncthreads();   // every lane's box and reference reads of chunk c are done
     if (c < 3) stage(c + 1);
     // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel, fp32 (BAL)
-    if constexpr (!CMF) {
+    if constexpr (!CMF && !CM32) {
       const float* wt = w0t + (4 * kC + 8 * c) * 4;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -1040,6 +1052,20 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl, acc1, 0, 0, 0);
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl2, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl2, acc1, 0, 0, 0);
+      if constexpr (CM32) {
+        if (c == 0) {
+          const floatx16 z = {};
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Cd, z, 0, 0, 0);
+          acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Cd, z, 0, 0, 0);
+        } else {
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Cd, acc2, 0, 0, 0);
+          acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Cd, acc3, 0, 0, 0);
+        }
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Cl, acc2, 0, 0, 0);
+        acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Cl, acc3, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Cl2, acc2, 0, 0, 0);
+        acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Cl2, acc3, 0, 0, 0);
+      }
     } else {
       acc0[0] += (float)A0[0] + (float)Bd[1];
       acc1[0] += (float)A1[0] + (float)Bl[1];
@@ -1058,6 +1084,17 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       const int px = (r & 3) + 8 * (r >> 2) + rb;
       yimg[(64 * wave + px) * kMYStride + col] = BAL ? -acc0[r] : acc0[r];   // (BAL: chunk 3 left -sum)
       yimg[(64 * wave + 32 + px) * kMYStride + col] = BAL ? -acc1[r] : acc1[r];
+    }
+    // CM32: the centre tap's columns 0-3 into columns 32..35 of the pixel's Y row
+    if constexpr (CM32) {
+      if (col < 4) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int px = (r & 3) + 8 * (r >> 2) + rb;
+          yimg[(64 * wave + px) * kMYStride + 32 + col] = acc2[r];
+          yimg[(64 * wave + 32 + px) * kMYStride + 32 + col] = acc3[r];
+        }
+      }
     }
     // CMF: the centre tap in columns 32..35 of the pixel's Y row
     if constexpr (CMF) {
@@ -1090,7 +1127,7 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       g4[2] = u ? g4[2] + yv.z : yv.z;
       g4[3] = u ? g4[3] + yv.w : yv.w;
     }
-    if constexpr (CMF) {
+    if constexpr (CMF || CM32) {
       const float4 yv = *reinterpret_cast<const float4*>(yb + 32);
       g4[0] += yv.x;
       g4[1] += yv.y;
@@ -1119,8 +1156,13 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
 // The kernel: a block takes a.omega_ipb consecutive items (default 1).  A tile's (view, plane)
 // items are consecutive on one XCD (xcd_tile): the reference tile, and a view's source box
 // across the npl neighbouring planes, come from its L2.
+// the eval sweep's omega_mfma variant (A/B builds only: -DAARMVS_OMEGA_EVAL_ABL=1024 puts the
+// centre tap on the matrix cores; the library is built with 0)
+#ifndef AARMVS_OMEGA_EVAL_ABL
+#define AARMVS_OMEGA_EVAL_ABL 0
+#endif
 template <int ABL = 0, int TW = kOmegaTW, bool BAL = false>
-__global__ void __launch_bounds__(OmegaTile<TW>::NT) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ void __launch_bounds__(OmegaTile<TW>::NT) __attribute__((amdgpu_waves_per_eu((ABL & 1024) ? 3 : 4)))
 omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restrict__ Rel,
                   const unsigned* __restrict__ xbound) {
   if (blockDim.x != OmegaTile<TW>::NT) return;   // LDS images are sized for exactly this block
@@ -1281,6 +1323,7 @@ static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspac
   a.off_owc = L.owc_off;
   a.off_owb_scale = L.owb_scale_off;
   a.off_owm = L.owm_off;
+  a.off_owmc = L.owmc_off;
   a.off_owm_scale = L.owb_scale_off;
   a.off_ob0 = L.pk_off[P_OB0];
   a.off_og0w = L.pk_off[P_OG0W];
@@ -1377,7 +1420,7 @@ hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Work
       hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW, true>), dim3(nblk, 1, g.B),
                          dim3(OmegaTile<kOmegaTW>::NT), 0, s, a, a.params, a.rel, ws.xbound);
     else
-      hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW>), dim3(nblk, 1, g.B),
+      hipLaunchKernelGGL((omega_mfma_kernel<AARMVS_OMEGA_EVAL_ABL, kOmegaTW>), dim3(nblk, 1, g.B),
                          dim3(OmegaTile<kOmegaTW>::NT), 0, s, a, a.params, a.rel, ws.xbound);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

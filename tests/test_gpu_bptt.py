@@ -112,16 +112,22 @@ def test_recorded_forward_matches_eval_sweep_and_holds_the_tensors():
     np.testing.assert_allclose(z0.cpu().numpy(), zref, atol=2e-5 * np.abs(zref).max(), rtol=0)
 
 
-@pytest.mark.parametrize("nreg", ["2", "3", "5"])
-def test_recorded_forward_streams_are_bit_identical(monkeypatch, nreg):
+@pytest.mark.parametrize("nreg,shape", [("2", (1, 3, 64, 96, 20)), ("3", (1, 3, 64, 96, 20)),
+                                        ("5", (1, 3, 64, 96, 20)), ("default", (1, 3, 256, 320, 18))])
+def test_recorded_forward_streams_are_bit_identical(monkeypatch, nreg, shape):
     """The training forward's regulariser units on 2, 3 or 5 streams (AARMVS_REG_STREAMS_REC,
     api.hip reg_unit_streams) against one stream: the cost volume and every record tensor bit
-    for bit, over two plane groups."""
-    B, N, H, W, D = 1, 3, 64, 96, 20
+    for bit, over two plane groups.  64x96 takes the small-frame schedule (cost stage on the
+    caller's stream); "default" at 256x320 (> 65536 px) the large-frame one (cost stage on the
+    aux stream, units over three streams)."""
+    B, N, H, W, D = shape
     sc, P, feats, proj, dv, sw, args = _setup(B, N, H, W, D, 8, 4)
     monkeypatch.setenv("AARMVS_REG_STREAMS_REC", "1")
     cost1, rec1, _ = _record_forward(sw, args, B, H, W, D, zero=True)
-    monkeypatch.setenv("AARMVS_REG_STREAMS_REC", nreg)
+    if nreg == "default":
+        monkeypatch.delenv("AARMVS_REG_STREAMS_REC")
+    else:
+        monkeypatch.setenv("AARMVS_REG_STREAMS_REC", nreg)
     cost2, rec2, _ = _record_forward(sw, args, B, H, W, D, zero=True)
     torch.cuda.synchronize()
     assert torch.equal(cost1, cost2)

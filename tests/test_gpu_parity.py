@@ -262,7 +262,7 @@ def test_two_stream_schedule_is_bit_identical():
 
 
 @pytest.mark.parametrize("nreg", ["default", "2", "3", "4", "5", "5:02121"])
-@pytest.mark.parametrize("B,N,H,W,D", [(1, 3, 128, 160, 37), (2, 4, 64, 96, 5)])
+@pytest.mark.parametrize("B,N,H,W,D", [(1, 3, 128, 160, 37), (2, 4, 64, 96, 5), (1, 3, 256, 320, 20)])
 def test_multi_stream_regulariser_is_bit_identical(monkeypatch, B, N, H, W, D, nreg):
     """The U-Net step's five units (cell 0 | cell 1 | cell 2 | deconv_0, cell 3 | deconv_1,
     cell 4, head) of neighbouring planes on the library's streams (AARMVS_REG_STREAMS=2: cells
@@ -271,8 +271,9 @@ def test_multi_stream_regulariser_is_bit_identical(monkeypatch, B, N, H, W, D, n
     AARMVS_REG_MAP) against the one-stream order: bit-identical cost volume, depth and
     confidence, also over continued d_ranges whose boundaries fall inside and at the end of
     plane groups, with and without the cost-stage stream (config 1's 160x128 at D=37 crosses
-    three plane groups).  "default": the library's choice, which for these small frames (B*H*W
-    <= 65536) is the cost stage on the caller's stream and the units over four streams."""
+    three plane groups).  "default": the library's choice: for the small frames (B*H*W <= 65536)
+    the cost stage on the caller's stream and the units over four streams, at 256x320 the cost
+    stage on the aux stream and the units over three."""
     nreg, _, umap = nreg.partition(":")
     if umap:
         monkeypatch.setenv("AARMVS_REG_MAP", umap)
