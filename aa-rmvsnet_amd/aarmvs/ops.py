@@ -392,9 +392,11 @@ class DepthSweep:
     """
 
     def __init__(self, params: dict, device, overlap: bool = True):
-        """``overlap``: run the next plane group's cost stage on a second stream beside the
-        current group's regulariser steps, and (eval sweeps) the back of each plane's U-Net step
-        on a library stream beside the front of the next plane's (same results, bit for bit)."""
+        """``overlap``: run the next plane group's cost stage on a second stream (the library's
+        aux stream, aux_stream()) beside the current group's regulariser steps, and spread each
+        plane's U-Net step over the library's streams so that the steps of neighbouring planes
+        overlap (four streams in all; small frames move the cost stage to the current stream;
+        same results, bit for bit)."""
         self.device = torch.device(device)
         self.packed = pack_params(params, self.device)
         self._ws = {}
