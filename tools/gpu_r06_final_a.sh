@@ -12,5 +12,5 @@ tail -1 gpurun_out/${T}_smoke.log
 bash tools/gpu_head_prof.sh ${T}_head || exit 1
 CEIL_DIR=gpurun_out/ceil_$T bash tools/gpu_ceiling.sh > gpurun_out/ceil_$T.log 2>&1 || { tail -5 gpurun_out/ceil_$T.log; exit 1; }
 python tools/ceiling_summary.py gpurun_out/ceil_$T --out gpurun_out/${T}_ceiling_pmc.json > /dev/null 2>&1
-python tools/pmc_summarize.py gpurun_out/ceil_$T/fetch gpurun_out/ceil_$T/write --workload dtu_eval_1600x1184_n7_d512 --out gpurun_out/${T}_pmc_traffic.json > gpurun_out/${T}_pmc_traffic.txt 2>&1
+python tools/pmc_summarize.py gpurun_out/ceil_$T/fetch gpurun_out/ceil_$T/write --workload dtu_eval_1600x1184_n7_d512 --source "round 6 final tree ($T): tools/gpu_ceiling.sh fetch/write passes over one 16-plane group at the headline" --out gpurun_out/${T}_pmc_traffic.json > gpurun_out/${T}_pmc_traffic.txt 2>&1
 ls gpurun_out/${T}_head
