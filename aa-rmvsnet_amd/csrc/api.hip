@@ -711,9 +711,16 @@ int aarmvs_sweep(const aarmvs_sweep_args* a, hipStream_t stream) {
   hipStream_t aux = (a->aux_stream && a->aux_stream != stream) ? a->aux_stream : nullptr;
   // (a training forward, with its record: AARMVS_REG_STREAMS_REC; 3 streams by default too,
   // config-4 training step 251.4 -> 243.3 ms, profiles/r06m_train_streams.txt)
+  // under stream capture (a caller recording the sweep into a graph) everything stays on
+  // `stream`: the captured graph is the one-stream order, bit-identical to every schedule
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if ((e = hipStreamIsCapturing(stream, &cap)) != hipSuccess) return hip_fail(e, "sweep: capture status");
+  if (cap != hipStreamCaptureStatusNone) aux = nullptr;
   const bool small = aux && small_frame((long)a->B * a->H * a->W);
   int ustream[kUnetUnits];
-  const int nreg = reg_unit_streams(reg_streams(aux != nullptr, rec != nullptr, small), ustream);
+  const int nreg = cap != hipStreamCaptureStatusNone
+                       ? reg_unit_streams(1, ustream)
+                       : reg_unit_streams(reg_streams(aux != nullptr, rec != nullptr, small), ustream);
   // small frames: the cost stage on the caller's stream, the aux stream one of the units' streams
   hipStream_t unit_aux = nullptr;
   if (small && nreg > 3) {

@@ -1527,7 +1527,10 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
     const char* v = getenv("AARMVS_BWD_PIPE");
     return v ? atoi(v) : 1;
   }();
-  const bool pipe_on = pipe_mode != 0;
+  // (under stream capture the backward stays on the caller's stream, as the sweep does)
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  CK(hipStreamIsCapturing(s, &cap));
+  const bool pipe_on = pipe_mode != 0 && cap == hipStreamCaptureStatusNone;
   int dev = 0;
   CK(current_device(dev));
   PipeSet& ps = ps_dev[dev];

@@ -362,3 +362,41 @@ def test_sweep_with_points_behind_a_source_camera_matches_oracle():
              torch.from_numpy(sc["depth_values"]), want_cost=True)
     np.testing.assert_allclose(out["cost"].cpu().numpy(), ref["cost"].numpy(), atol=1e-4, rtol=1e-4)
     assert rel_l1(out["depth"].cpu().numpy(), ref["depth"].numpy()) <= 1e-3
+
+
+@pytest.mark.parametrize("B,N,H,W,D", [(1, 3, 128, 160, 20), (1, 3, 256, 320, 20)])
+def test_sweep_graph_capture_replays_bit_identical(B, N, H, W, D):
+    """A caller may record the sweep into a HIP graph (torch.cuda.CUDAGraph): under stream
+    capture the library keeps everything on the capturing stream (api.hip: the multi-stream
+    schedules are not captured), and the replay's cost volume and depth equal the eager sweep's
+    bit for bit, for a small-frame and a large-frame schedule."""
+    from aarmvs import ops
+    sc = syn.scene(B, N, H, W, D, seed=5)
+    P = P_of(6)
+    sw = ops.DepthSweep(P, DEV, overlap=True)
+    f = torch.from_numpy(sc["features"]).to(DEV)
+    proj = torch.from_numpy(sc["proj_matrices"])
+    dv = torch.from_numpy(sc["depth_values"]).to(DEV).float().contiguous()
+    ref, srcs = f[0].contiguous(), [f[v].contiguous() for v in range(1, N)]
+    rel = sw.relative(proj[:, 0], [proj[:, v] for v in range(1, N)], B)
+    cost = torch.empty(B, D, H, W, device=DEV)
+
+    def run():
+        return sw(ref, srcs, None, [None] * (N - 1), dv, want_depth=True, cost_out=cost, rel=rel)
+
+    out = run()
+    torch.cuda.synchronize()
+    eager_cost, eager_depth = cost.clone(), out["depth"].clone()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    cost.zero_()
+    with torch.cuda.graph(g):
+        gout = run()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(cost, eager_cost) and torch.equal(gout["depth"], eager_depth)

@@ -1,7 +1,7 @@
 """Launch overhead of small sweeps (round 6): one eval sweep at a BASELINE
 config (default config 1, 160x128, N=3, D=48) timed as ordinary stream launches and as a
 replayed HIP graph of the same call (torch.cuda.CUDAGraph capture), with the outputs compared.
-usage: python tools/graph_probe.py [N H W D]"""
+usage: [PROBE_OVERLAP=0] python tools/graph_probe.py [N H W D]"""
 import os
 import sys
 import time
@@ -16,7 +16,7 @@ N, H, W, D = (int(x) for x in sys.argv[1:5]) if len(sys.argv) >= 5 else (3, 128,
 B = 1
 sc = syn.scene(B, N, H, W, D, seed=0)
 P = {k: torch.from_numpy(v).cuda() for k, v in syn.sweep_weights(1).items()}
-sw = ops.DepthSweep(P, "cuda")
+sw = ops.DepthSweep(P, "cuda", overlap=os.environ.get("PROBE_OVERLAP", "1") == "1")
 f = torch.from_numpy(sc["features"]).cuda()
 proj = torch.from_numpy(sc["proj_matrices"])
 dv = torch.from_numpy(sc["depth_values"]).cuda().float().contiguous()
@@ -31,6 +31,7 @@ def run():
 
 out = run()
 torch.cuda.synchronize()
+print("eager sweep done", flush=True)
 eager_depth = out["depth"].clone()
 eager_cost = cost.clone()
 K = 30
@@ -50,9 +51,11 @@ with torch.cuda.stream(s):
     run()   # warm-up on the capture stream
 torch.cuda.current_stream().wait_stream(s)
 torch.cuda.synchronize()
+print("capturing", flush=True)
 with torch.cuda.graph(g):
     gout = run()
 torch.cuda.synchronize()
+print("captured", flush=True)
 for _ in range(3):
     g.replay()
 torch.cuda.synchronize()
