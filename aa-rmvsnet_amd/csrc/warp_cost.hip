@@ -703,9 +703,22 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 // LDS-DMA, 16 B per lane: lane l of the wave lands at wave_dst + 16 l (wave_dst uniform);
-// an offset past the buffer's range loads zeros
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float* wave_dst, uint32_t off) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)wave_dst, 16, off, 0, 0, 0);
+// an offset past the buffer's range loads zeros.  soff: a wave-uniform byte offset (the chunk's
+// plane) in the instruction's scalar offset, so the per-lane offset stays loop-invariant
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float* wave_dst, uint32_t off,
+                                      uint32_t soff = 0) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)wave_dst, 16, off, soff, 0, 0);
+}
+// hi = fp16(x) for a pair, lo = fp16(x - hi): the difference on v_fma_mix_f32 straight from
+// the packed fp16 hi (x - hi is exact in fp32, so this is the same value as the convert-back
+// and subtract it replaces: 4 instructions per pair instead of 6)
+__device__ __forceinline__ uint32_t split_pair(float a, float b, uint32_t& lo_bits) {
+  const uint32_t hb = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){a, b}, half2_t));
+  float la, lb;
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(la) : "v"(hb), "v"(a));
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(lb) : "v"(hb), "v"(b));
+  lo_bits = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){la, lb}, half2_t));
+  return hb;
 }
 __device__ __forceinline__ void dma_wait() {
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
@@ -867,7 +880,7 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   }
   const bool lds = bx.nx * bx.ny <= min(kMBoxPx, a.box_cap);
   const uint32_t zp = lds ? (uint32_t)kMBoxPx : fbytes / 32u;
-  const TapP tp = tap_p4(tf, in_img, H, W, lds, bx, zp);
+  TapP tp = tap_p4(tf, in_img, H, W, lds, bx, zp);
   const int items = lds ? bx.nx * bx.ny * 2 : 0;
   const uint32_t mg = box_magic(bx.nx);
   uint32_t boff[NB];
@@ -878,31 +891,39 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
                         ((uint32_t)p - __umul24((uint32_t)r, (uint32_t)bx.nx));
     boff[j] = gp * 32u + 16u * (uint32_t)img_half((uint32_t)p, i & 1);
   }
-  const uint32_t rpix = in_img ? (uint32_t)(gy * W + gx) : fbytes / 32u;
+  const uint32_t rpix = in_img ? (uint32_t)(gy * W + gx) * 32u : fbytes;
+  // the wave's LDS destinations in scalar registers (m0 without a readfirstlane per DMA)
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
   auto stage = [&](int c) {
     const uint32_t cb = (uint32_t)c * cbytes;
 #pragma unroll
     for (int j = 0; j < NB; ++j)
       if (!(ABL & 2) && tid + j * kMThreads < items)
-        dma16(rsrc, box + (j * kMThreads + wave * 64) * 4, boff[j] + cb);
+        dma16(rsrc, box + (j * kMThreads + wave_s * 64) * 4, boff[j], cb);
     // this lane's reference pixel in the c8 image (past the buffer: zeros)
     if (!(ABL & 8)) {
-      const uint32_t ro = cb + rpix * 32u;
-      dma16(rref, rimg + (wave * 64) * 4, ro);
-      dma16(rref, rimg + (kMThreads + wave * 64) * 4, ro + 16u);
+      dma16(rref, rimg + (wave_s * 64) * 4, rpix, cb);
+      dma16(rref, rimg + (kMThreads + wave_s * 64) * 4, rpix + 16u, cb);
     }
   };
-  // sq staging scale: bound 2^-e in [2^14, 2^15) (sq <= 4 max|f|^2 <= bound), e of either
-  // sign, so that fp16 cannot overflow and the lo parts of small sq stay normal numbers
+  // sq staging scale: bound 2^-e in [2^13, 2^15) (sq <= 4 max|f|^2 <= bound), e even and of
+  // either sign, so that fp16 cannot overflow and the lo parts of small sq stay normal numbers.
+  // The scale is applied as 2^(-e/2) to the difference: the bilinear weights carry it (the
+  // sample is 2^(-e/2) g exactly) and the reference is subtracted by one fma with -2^(-e/2),
+  // so sq arrives scaled with no multiply of its own; the centre tap accumulates the scaled sq
+  // and is scaled back by 2^e at the end (all exact power-of-two scalings)
   int e = 0;
   {
     const float bound = __uint_as_float(*xbound);
     if (bound > 0.0f) {
       const int k = ilogbf(bound);
       e = k >= 134 ? 120 : (k < -100 ? -114 : k - 14);
+      e += e & 1;
     }
   }
-  const float sqs = ldexpf(1.0f, -e);
+  const float dsc = ldexpf(1.0f, -(e / 2));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) tp.wt[k] = __fmul_rn(tp.wt[k], dsc);
   const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]: centre tap = tap 4
   const half8* __restrict__ owm = reinterpret_cast<const half8*>(P + a.off_owm);
   // CMF (ABL bit 512, diagnostic): the centre tap on v_mfma_f32_4x4x4f16 instead of the fp32
@@ -950,8 +971,13 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     // the chunk loop cost 16 register copies per chunk)
     const float4 rf0 = *reinterpret_cast<const float4*>(rimg + tid * 4);
     const float4 rf1 = *reinterpret_cast<const float4*>(rimg + (kMThreads + tid) * 4);
-    const float4 s0 = sqdiff4(g0, rf0), s1 = sqdiff4(g1, rf1);
-    const float sq[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    // sq 2^-e: (2^(-e/2) g - 2^(-e/2) r)^2, the difference rounded once as in sqdiff4
+    auto dsq = [&](float g, float r) {
+      const float dd = __fmaf_rn(r, -dsc, g);
+      return __fmul_rn(dd, dd);
+    };
+    const float sq[8] = {dsq(g0.x, rf0.x), dsq(g0.y, rf0.y), dsq(g0.z, rf0.z), dsq(g0.w, rf0.w),
+                         dsq(g1.x, rf1.x), dsq(g1.y, rf1.y), dsq(g1.z, rf1.z), dsq(g1.w, rf1.w)};
     // this chunk's B fragments, issued before the barrier: their L1/L2 latency is hidden
     // behind it and the centre-tap chain (2.5% of the kernel against loading them after;
     // DMA'ing all 12 to LDS once per item instead was 1.8%)
@@ -981,14 +1007,7 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     // reference read past the buffer.  Two values per v_cvt_pk_f16_f32.
     uint32_t hw[4], lw[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float2 pp = make_float2(sq[2 * i] * sqs, sq[2 * i + 1] * sqs);
-      const half2_t hv = __builtin_convertvector((float2_t){pp.x, pp.y}, half2_t);
-      const float2_t hb = __builtin_convertvector(hv, float2_t);
-      const half2_t lv = __builtin_convertvector((float2_t){pp.x - hb[0], pp.y - hb[1]}, half2_t);
-      hw[i] = __builtin_bit_cast(uint32_t, hv);
-      lw[i] = __builtin_bit_cast(uint32_t, lv);
-    }
+    for (int i = 0; i < 4; ++i) hw[i] = split_pair(sq[2 * i], sq[2 * i + 1], lw[i]);
     // CMF: the centre tap of the own pixel as sixteen 4x4 blocks (block = 4 lanes = 4 pixels,
     // K = 4 channels), before the swaps: A = this lane's sq hi / lo of channels 4 s .. 4 s + 3,
     // B = the tap's weights in three fp16 terms (hi sq x (W_hi + W_lo + W_lo2) + lo sq x (W_hi
@@ -1135,13 +1154,14 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       g4[3] += yv.w;
     }
     }
-    const float isc = P[a.off_owm_scale] * ldexpf(1.0f, e);
+    const float pe = ldexpf(1.0f, e);
+    const float isc = P[a.off_owm_scale] * pe;
     const float* __restrict__ b0 = P + a.off_ob0;
     float4 out;
-    out.x = fmaf(g4[0], isc, o4[0]) + b0[0];
-    out.y = fmaf(g4[1], isc, o4[1]) + b0[1];
-    out.z = fmaf(g4[2], isc, o4[2]) + b0[2];
-    out.w = fmaf(g4[3], isc, o4[3]) + b0[3];
+    out.x = fmaf(g4[0], isc, o4[0] * pe) + b0[0];
+    out.y = fmaf(g4[1], isc, o4[1] * pe) + b0[1];
+    out.z = fmaf(g4[2], isc, o4[2] * pe) + b0[2];
+    out.w = fmaf(g4[3], isc, o4[3] * pe) + b0[3];
     a.t1_next[kp * a.t1_kstride + ((size_t)b * nsrc + v) * HW + gy * W + gx] = out;
     ps = ((double)out.x + (double)out.y) + ((double)out.z + (double)out.w);
     pss = ((double)out.x * out.x + (double)out.y * out.y) + ((double)out.z * out.z + (double)out.w * out.w);
