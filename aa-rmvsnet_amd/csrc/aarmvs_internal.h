@@ -63,10 +63,7 @@ struct ParamLayout {
   size_t h3p_off[5];        // the same, every tap positive (the inference cells)
   size_t h3_scale_off;      // 5 floats: 1 / (power-of-two weight scale) per cell
   size_t ow0t_off;          // omega conv3x3 weights as [tap][ci][co] (1,152 floats)
-  size_t owc_off;           // omega conv3x3 centre tap as split-fp16 v_mfma_f32_4x4x4f16 B operands
-                            // [chunk][co][hi, lo, lo2][K-step][4 halves] (omega_mfma; owm's scale)
   size_t owb_scale_off;     // 1 float: 1 / (power-of-two scale of the omega conv fragments)
-  size_t owmc_off;          // omega conv3x3 centre tap as 32x32x16 B fragments (columns 0-3; ABL 1024)
   size_t owm_off;           // omega conv3x3 off-centre taps as split-fp16 v_mfma_f32_32x32x16_f16
                             // B fragments [chunk][2][64 lanes][8] (omega_mfma; same scale)
   size_t dct_off[2];        // deconv_0/1 weights as [ci][tap][co] (2,304 floats each)

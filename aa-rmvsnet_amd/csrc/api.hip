@@ -46,14 +46,10 @@ const ParamLayout& param_layout() {
     pk += 64;
     l.ow0t_off = pk;
     pk += 4 * 32 * 9;
-    l.owc_off = pk;
-    pk += 4 * 4 * 6 * 4 / 2;    // halves -> floats (192: 64-float aligned)
     l.owb_scale_off = pk;
     pk += 64;
     l.owm_off = pk;
     pk += 4 * 3 * 64 * 8 / 2;   // halves -> floats
-    l.owmc_off = pk;
-    pk += 4 * 3 * 64 * 8 / 2;
     for (int k = 0; k < 2; ++k) {
       l.dct_off[k] = pk;
       pk += 16 * 9 * 16;
@@ -311,29 +307,20 @@ __global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __r
   }
   const float sc = ldexpf(1.0f, e);
   if (threadIdx.x == 0) pk[L.owb_scale_off] = ldexpf(1.0f, -e);
-  // the centre tap (tap 4) as v_mfma_f32_4x4x4f16 B operands, in the same three fp16 terms as
-  // the 32x32x16 fragments below: [chunk c][co j][term t (hi, lo, lo2)][K-step s][4 halves],
-  // element kk of step s against input channel 8 c + 4 s + kk (lane l of a 4x4 block holds
-  // column j = l & 3: 48 contiguous bytes per lane and chunk)
-  _Float16* bc = reinterpret_cast<_Float16*>(pk + L.owc_off);
-  for (int i = threadIdx.x; i < 4 * 4 * 6 * 4; i += blockDim.x) {
-    const int kk = i & 3, s = (i >> 2) & 1, t = (i >> 3) % 3, j = (i / 24) & 3, c = i / 96;
-    const float x = w[(j * 32 + 8 * c + 4 * s + kk) * 9 + 4] * sc;
-    const _Float16 xh = (_Float16)x;
-    const float r1 = x - (float)xh;
-    const _Float16 xl = (_Float16)r1;
-    bc[i] = t == 0 ? xh : t == 1 ? xl : (_Float16)(r1 - (float)xl);
-  }
   // omega_mfma's v_mfma_f32_32x32x16_f16 B fragments: per chunk c and kind k against
   // A = [sq hi | sq lo]: 0: [W_hi; W_hi], 1: [W_lo; 0], 2: [W_lo2; W_lo] with W = W_hi + W_lo +
   // W_lo2 (three fp16 terms: the weights exact to ~2^-33, so the conv carries no systematic
   // per-weight error; the dropped terms are sq_lo W_lo2 and sq_lo's own rounding, ~2^-22 random
-  // per product); lane l holds B[8 (l >> 5) + j][n = l & 31] with column n = 4 u + co (tap slot
-  // u: taps 0..3, 5..8)
+  // per product); lane l holds B[8 (l >> 5) + j][n = l & 31] with column n = 4 u + co.  The
+  // kernel passes them as the A operand (the product transposed: rows n, columns pixels), so
+  // that slot u of row group g = u >> 1 lands in accumulator registers 4 g .. 4 g + 3 of lanes
+  // 0-31 (u even) or 32-63 (u odd); tap slots u -> taps 0, 6, 1, 7, 2, 8, 3, 5 pair the taps of
+  // one dx in one register group (omega_item's row sums)
   _Float16* bm = reinterpret_cast<_Float16*>(pk + L.owm_off);
   for (int i = threadIdx.x; i < 4 * 3 * 64 * 8; i += blockDim.x) {
     const int j = i & 7, lane = (i >> 3) & 63, k = (i >> 9) % 3, c = (i >> 9) / 3;
-    const int n = lane & 31, u = n >> 2, tap = u < 4 ? u : u + 1, co = n & 3;
+    const int n = lane & 31, u = n >> 2, g = u >> 1, co = n & 3;
+    const int tap = (u & 1) ? (g < 3 ? 6 + g : 5) : g;
     const float x = w[(co * 32 + 8 * c + j) * 9 + tap] * sc;
     const _Float16 xh = (_Float16)x;
     const float r1 = x - (float)xh;
@@ -341,20 +328,6 @@ __global__ void pack_omega_conv_kernel(const float* __restrict__ raw, float* __r
     const _Float16 xl2 = (_Float16)(r1 - (float)xl);
     const bool top = (lane >> 5) == 0;   // K rows 0-7: against sq hi
     bm[i] = k == 0 ? xh : k == 1 ? (top ? xl : (_Float16)0.0f) : (top ? xl2 : xl);
-  }
-  // the centre tap (tap 4) in the same fragment form, columns n = co < 4, the others zero
-  // (omega_mfma ABL bit 1024: its own accumulator pair)
-  _Float16* bmc = reinterpret_cast<_Float16*>(pk + L.owmc_off);
-  for (int i = threadIdx.x; i < 4 * 3 * 64 * 8; i += blockDim.x) {
-    const int j = i & 7, lane = (i >> 3) & 63, k = (i >> 9) % 3, c = (i >> 9) / 3;
-    const int n = lane & 31, co = n & 3;
-    const float x = n < 4 ? w[(co * 32 + 8 * c + j) * 9 + 4] * sc : 0.0f;
-    const _Float16 xh = (_Float16)x;
-    const float r1 = x - (float)xh;
-    const _Float16 xl = (_Float16)r1;
-    const _Float16 xl2 = (_Float16)(r1 - (float)xl);
-    const bool top = (lane >> 5) == 0;
-    bmc[i] = k == 0 ? xh : k == 1 ? (top ? xl : (_Float16)0.0f) : (top ? xl2 : xl);
   }
 }
 

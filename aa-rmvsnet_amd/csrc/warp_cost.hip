@@ -265,9 +265,8 @@ struct PipeArgs {
   float* x;                   // [B,H,W,32] (NHWC)
   float* omega_out;           // [nsrc,B,H,W] (prev plane) or null
   const float* params;
-  size_t off_owc, off_owb_scale;   // omega conv centre-tap 4x4x4 B operands, the fragments' scale
-  size_t off_owm, off_owm_scale;   // omega_mfma's 32x32x16 B fragments, their scale
-  size_t off_owmc;                 // the centre tap's 32x32x16 B fragments (ABL 1024)
+  size_t off_owb_scale;            // the omega conv fragments' scale
+  size_t off_owm, off_owm_scale;   // omega_mfma's 32x32x16 fragments, their scale
   size_t off_ow0t, off_ow0, off_ob0, off_og0w, off_og0b, off_ow1, off_ob1, off_og1w, off_og1b, off_ow2,
       off_ob2, off_og2w, off_og2b, off_owo, off_obo;
   int B, H, W, nsrc;
@@ -750,7 +749,6 @@ __device__ __forceinline__ void dma_wait() {
 // Lane l of wave w holds haloed pixel 64 w + l = (hy, hx) = ((64 w + l) / TW, (64 w + l) % TW);
 // MFMA row group 0 / 1 of the wave is its lanes 0-31 / 32-63.
 constexpr int kMTileH = 16;
-constexpr int kMYStride = 36;   // floats per pixel in Y
 template <int TW>
 struct OmegaTile {
   static constexpr int NT = kMTileH * TW;   // threads = haloed pixels
@@ -764,8 +762,8 @@ constexpr int kOmegaTW = 16;   // the library's tile width
 // ABL: ablation bits for the diagnostic harness only (tools/microbench/pipe_bench.cpp; the
 // library instantiates ABL = 0): 1 no MFMAs, 2 no box DMA, 4 no box sampling, 8 no reference
 // loads, 16 sampling positions without the homography divisions (the own pixel), 32 no Y
-// image / gather (t1 from the accumulators), 64 no statistics atomics, 128 no B-fragment loads,
-// 512 the centre tap on 4x4x4 MFMAs (CMF below)
+// image / gather (t1 from the row sums of the own lanes), 64 no statistics atomics, 128 no
+// fragment loads
 // BAL: sign-balanced accumulation, for the training sweep only: +9% time
 // wave_sum_d (device_common.h) of two values at once, in the same order and so with the same
 // result, on DPP moves with an undefined `old` operand: only lane 63's value is used, and every
@@ -828,11 +826,16 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   using T = OmegaTile<TW>;
   constexpr int kMThreads = T::NT, kMBoxPx = T::BOXPX, kMOutH = T::OUTH, kMOutW = T::OUTW;
   constexpr int NB = (2 * kMBoxPx + kMThreads - 1) / kMThreads;   // box pieces per thread
-  constexpr int YFL = kMThreads * kMYStride;                      // Y image floats
-  static_assert(YFL >= (kMBoxPx + 1) * 8, "the box fits in the Y image space");
+  static_assert(TW == 16, "the row sums shift along 16-lane DPP rows: one haloed row each");
+  // LDS: chunk c's source box and reference pixels, then (after the last chunk) the row-sum
+  // images zm, zp (16 B per haloed pixel each)
+  constexpr int kRefFl = (kMBoxPx + 1) * 8;
+  constexpr int YFL = kRefFl + 2 * kMThreads * 4;
+  static_assert(2 * kMThreads * 4 <= YFL, "the row-sum images fit in the box space");
   __shared__ __attribute__((aligned(16))) float smem[YFL];
-  float* const box = smem;   // chunk c's source box, then (after the last chunk) Y
-  float* const yimg = smem;
+  float* const box = smem;
+  float4* const zms = reinterpret_cast<float4*>(smem);
+  float4* const zps = zms + kMThreads;
   __shared__ int red[kMThreads / 64][4];
   int tid;
   asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));   // see omega_mfma_kernel
@@ -847,8 +850,6 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   const bool interior = in_img && hy >= 1 && hy <= kMOutH && hx >= 1 && hx <= kMOutW;
   // chunk c's reference pixels: one 16-B half per lane and DMA, half h of haloed pixel t at
   // rimg[(h NT + t) 4], after the box (conflict-free, lane-linear reads)
-  constexpr int kRefFl = (kMBoxPx + 1) * 8;
-  static_assert(kRefFl + 2 * kMThreads * 4 <= YFL, "the box and the reference fit in the Y space");
   float* const rimg = smem + kRefFl;
 
   const float dep = a.dvals[b * a.D + a.d_next + kp];
@@ -871,7 +872,7 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     box_extend(tf, H, W, lx, ly, bhx, bhy);
   }
   const Box bx = box_reduce<kMThreads / 64>(lx, ly, bhx, bhy, red);
-  // after box_reduce's barrier: every wave is past the previous item's Y gather and wave sums
+  // after box_reduce's barrier: every wave is past the previous item's row-sum reads and wave sums
   if (tid < 8) box[kMBoxPx * 8 + tid] = 0.f;   // the zero pixel
   if (has_prev && tid == 0) {
     double s0, s1;
@@ -926,25 +927,12 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   for (int k = 0; k < 4; ++k) tp.wt[k] = __fmul_rn(tp.wt[k], dsc);
   const float* __restrict__ w0t = P + a.off_ow0t;   // [9][32][4]: centre tap = tap 4
   const half8* __restrict__ owm = reinterpret_cast<const half8*>(P + a.off_owm);
-  // CMF (ABL bit 512, diagnostic): the centre tap on v_mfma_f32_4x4x4f16 instead of the fp32
-  // FMA chain.  Measured in round 6: 9.20 against 8.50 ms per headline launch (bit-different,
-  // parity green): ten dependent 4x4x4 MFMAs per chunk on one accumulator stall the wave more
-  // than the 32 FMAs they replace cost (the layout: tools/microbench/mfma4_layout.cpp)
-  constexpr bool CMF = (ABL & 512) != 0 && !BAL;
-  // CM32 (ABL bit 1024, diagnostic): the centre tap on the 32x32x16 MFMAs of the off-centre taps'
-  // A operands, with B fragments holding only columns 0-3, into an accumulator pair of its own
-  // (32 more VGPRs: three waves per SIMD instead of four)
-  constexpr bool CM32 = (ABL & 1024) != 0 && !BAL;
-  const half8* __restrict__ owc = reinterpret_cast<const half8*>(P + a.off_owc) + 3 * (lane & 3);
-  const half8* __restrict__ owmc = reinterpret_cast<const half8*>(P + a.off_owmc);
-  floatx16 acc2, acc3;
   floatx16 acc0, acc1;   // first written by chunk 0's MFMAs (ABL 1: zero here)
   if constexpr ((ABL & 1) != 0) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
   }
   float o4[4] = {0.f, 0.f, 0.f, 0.f};
-  floatx4 accc = {0.f, 0.f, 0.f, 0.f};
 
   stage(0);
   dma_wait();
@@ -981,21 +969,16 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     // this chunk's B fragments, issued before the barrier: their L1/L2 latency is hidden
     // behind it and the centre-tap chain (2.5% of the kernel against loading them after;
     // DMA'ing all 12 to LDS once per item instead was 1.8%)
-    half8 Bd, Bl, Bl2, Cd, Cl, Cl2;
+    half8 Bd, Bl, Bl2;
     if constexpr ((ABL & 128) == 0) {
       Bd = owm[(c * 3 + 0) * 64 + lane];
       Bl = owm[(c * 3 + 1) * 64 + lane];
       Bl2 = owm[(c * 3 + 2) * 64 + lane];
     }
-    if constexpr (CM32) {
-      Cd = owmc[(c * 3 + 0) * 64 + lane];
-      Cl = owmc[(c * 3 + 1) * 64 + lane];
-      Cl2 = owmc[(c * 3 + 2) * 64 + lane];
-    }
     __syncthreads();   // every lane's box and reference reads of chunk c are done
     if (c < 3) stage(c + 1);
     // centre tap (omega.reweight_network.0.0, tap 4) on the own pixel, fp32 (BAL)
-    if constexpr (!CMF && !CM32) {
+    {
       const float* wt = w0t + (4 * kC + 8 * c) * 4;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -1008,27 +991,8 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
     uint32_t hw[4], lw[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) hw[i] = split_pair(sq[2 * i], sq[2 * i + 1], lw[i]);
-    // CMF: the centre tap of the own pixel as sixteen 4x4 blocks (block = 4 lanes = 4 pixels,
-    // K = 4 channels), before the swaps: A = this lane's sq hi / lo of channels 4 s .. 4 s + 3,
-    // B = the tap's weights in three fp16 terms (hi sq x (W_hi + W_lo + W_lo2) + lo sq x (W_hi
-    // + W_lo), the off-centre taps' product set); D[pixel 4 b + r][co = lane & 3] in register
-    // r of lane 4 b + co
-    if constexpr (CMF) {
-      const half8 wh = owc[c * 12 + 0], wl = owc[c * 12 + 1], wl2 = owc[c * 12 + 2];
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const half4 ah = __builtin_bit_cast(half4, u32x2{hw[2 * st], hw[2 * st + 1]});
-        const half4 al = __builtin_bit_cast(half4, u32x2{lw[2 * st], lw[2 * st + 1]});
-        const half4 bh = st ? wh.hi : wh.lo, bl = st ? wl.hi : wl.lo, bl2 = st ? wl2.hi : wl2.lo;
-        accc = __builtin_amdgcn_mfma_f32_4x4x4f16(ah, bh, accc, 0, 0, 0);
-        accc = __builtin_amdgcn_mfma_f32_4x4x4f16(al, bh, accc, 0, 0, 0);
-        accc = __builtin_amdgcn_mfma_f32_4x4x4f16(ah, bl, accc, 0, 0, 0);
-        accc = __builtin_amdgcn_mfma_f32_4x4x4f16(ah, bl2, accc, 0, 0, 0);
-        accc = __builtin_amdgcn_mfma_f32_4x4x4f16(al, bl, accc, 0, 0, 0);
-      }
-    }
-    // lanes 0-31 / 32-63 hold rows 2w / 2w+1: after the swaps, (hw, lw) are the A operands
-    // of row 2w (lanes 0-31 hi, 32-63 lo of pixel lane & 31) and of row 2w+1
+    // after the swaps, (hw, lw) are the pixel operands of the wave's pixels 0-31 (lanes 0-31 hi,
+    // 32-63 lo of pixel lane & 31) and of its pixels 32-63
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const auto r = __builtin_amdgcn_permlane32_swap(hw[i], lw[i], false, false);
@@ -1058,33 +1022,22 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       Bl = A0;
       Bl2 = A1;
     }
+    // D^T = W x [sq hi | sq lo]^T: the weight fragments as the A operand, so that a lane holds
+    // its pixel's tap slots (rows) rather than a slot's pixels: row r of lane l is slot
+    // 2 (r >> 2) + (l >> 5), output channel r & 3 (the row sums below)
     if (!(ABL & 1)) {
       if (c == 0) {   // the accumulators start from the MFMA's inline-zero C operand (no zero fill)
         const floatx16 z = {};
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, z, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, z, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bd, A0, z, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bd, A1, z, 0, 0, 0);
       } else {
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bd, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bd, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bd, A0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bd, A1, acc1, 0, 0, 0);
       }
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl, acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bl2, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Bl2, acc1, 0, 0, 0);
-      if constexpr (CM32) {
-        if (c == 0) {
-          const floatx16 z = {};
-          acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Cd, z, 0, 0, 0);
-          acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Cd, z, 0, 0, 0);
-        } else {
-          acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Cd, acc2, 0, 0, 0);
-          acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Cd, acc3, 0, 0, 0);
-        }
-        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Cl, acc2, 0, 0, 0);
-        acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Cl, acc3, 0, 0, 0);
-        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Cl2, acc2, 0, 0, 0);
-        acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, Cl2, acc3, 0, 0, 0);
-      }
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bl, A0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bl, A1, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bl2, A0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bl2, A1, acc1, 0, 0, 0);
     } else {
       acc0[0] += (float)A0[0] + (float)Bd[1];
       acc1[0] += (float)A1[0] + (float)Bl[1];
@@ -1094,65 +1047,60 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
       __syncthreads();   // chunk c+1's box and reference visible
     }
   }
-  // Y image (over the box space: every lane passed chunk 3's box reads before the barrier
-  // above): D[row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)][col = lane & 31] of row group g
+  // The 3x3 conv's off-centre taps as row sums, in registers.  acc0 / acc1 hold the wave's
+  // pixels 0-31 / 32-63 (pixel lane & 31 in lanes l and l + 32); register group g (registers
+  // 4 g .. 4 g + 3, output channels 0-3) holds tap slot 2 g in lanes 0-31 and 2 g + 1 in lanes
+  // 32-63, slots -> taps 0, 6 | 1, 7 | 2, 8 | 3, 5 (pack_omega_conv_kernel): the groups 0-2 are
+  // the taps of dx = -1, 0, +1 of row dy = -1 (lanes 0-31) and dy = +1 (lanes 32-63).  A 16-lane
+  // DPP row is one haloed row (TW = 16), so the dx neighbours are one lane away:
+  //   Z_dy[q] = Y(dy,-1)[q - 1] + Y(dy,0)[q] + Y(dy,+1)[q + 1]          (row_shr / row_shl)
+  //   Z_0[q]  = Y(0,-1)[q - 1] + Y(0,+1)[q + 1]
+  //   t1[p]   = Z_-1[p - TW] + Z_0[p] + Z_+1[p + TW]                    (via LDS: other waves)
+  // (the edge lanes of a row get zeros from the DPP bound: they are halo pixels, never output)
+  auto shr1 = [](float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xF, 0xF, true));
+  };
+  auto shl1 = [](float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x101, 0xF, 0xF, true));
+  };
+  float zmr[4], zpr[4], z0[4];
+#pragma unroll
+  for (int co = 0; co < 4; ++co) {
+    const float r0 = (shr1(acc0[co]) + acc0[4 + co]) + shl1(acc0[8 + co]);
+    const float r1 = (shr1(acc1[co]) + acc1[4 + co]) + shl1(acc1[8 + co]);
+    // -> Z_-1 of the wave's pixel `lane` in zmr, Z_+1 in zpr
+    const auto zz = __builtin_amdgcn_permlane32_swap(__float_as_uint(r0), __float_as_uint(r1), false, false);
+    zmr[co] = __uint_as_float(zz[0]);
+    zpr[co] = __uint_as_float(zz[1]);
+    // -> tap 3 and tap 5 of pixel `lane`
+    const auto t35 = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc0[12 + co]),
+                                                      __float_as_uint(acc1[12 + co]), false, false);
+    z0[co] = shr1(__uint_as_float(t35[0])) + shl1(__uint_as_float(t35[1]));
+  }
+  // the row-sum images over the box space: every lane passed chunk 3's box reads before the
+  // barrier in the loop
   if constexpr ((ABL & 32) == 0) {
-    const int col = lane & 31, rb = 4 * (lane >> 5);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int px = (r & 3) + 8 * (r >> 2) + rb;
-      yimg[(64 * wave + px) * kMYStride + col] = BAL ? -acc0[r] : acc0[r];   // (BAL: chunk 3 left -sum)
-      yimg[(64 * wave + 32 + px) * kMYStride + col] = BAL ? -acc1[r] : acc1[r];
-    }
-    // CM32: the centre tap's columns 0-3 into columns 32..35 of the pixel's Y row
-    if constexpr (CM32) {
-      if (col < 4) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int px = (r & 3) + 8 * (r >> 2) + rb;
-          yimg[(64 * wave + px) * kMYStride + 32 + col] = acc2[r];
-          yimg[(64 * wave + 32 + px) * kMYStride + 32 + col] = acc3[r];
-        }
-      }
-    }
-    // CMF: the centre tap in columns 32..35 of the pixel's Y row
-    if constexpr (CMF) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) yimg[(64 * wave + 4 * (lane >> 2) + r) * kMYStride + 32 + (lane & 3)] = accc[r];
-    }
+    zms[tid] = make_float4(zmr[0], zmr[1], zmr[2], zmr[3]);
+    zps[tid] = make_float4(zpr[0], zpr[1], zpr[2], zpr[3]);
   }
   __syncthreads();
   // GroupNorm partials in fp64 from the first addition on (var = E[x^2] - E[x]^2 cancels)
   double ps = 0.0, pss = 0.0;
   if (interior) {
-    float g4[4] = {0.f, 0.f, 0.f, 0.f};
+    float g4[4];
     if constexpr ((ABL & 32) != 0) {
-      g4[0] = acc0[0] + acc1[1];
-      g4[1] = acc0[2] + acc1[3];
-      g4[2] = acc0[4] + acc1[5];
-      g4[3] = acc0[6] + acc1[7];
-    } else {
-    // neighbour q = tid + (dy TW + dx): one base address, constant offsets
-    // (the sum starts from tap 0's value rather than 0 + it: the same sum but for the sign
-    // of an exactly zero one)
-    const float* const yb = yimg + tid * kMYStride;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int tap = u < 4 ? u : u + 1;
-      const int dq = (tap / 3 - 1) * TW + tap % 3 - 1;
-      const float4 yv = *reinterpret_cast<const float4*>(yb + dq * kMYStride + 4 * u);
-      g4[0] = u ? g4[0] + yv.x : yv.x;
-      g4[1] = u ? g4[1] + yv.y : yv.y;
-      g4[2] = u ? g4[2] + yv.z : yv.z;
-      g4[3] = u ? g4[3] + yv.w : yv.w;
+      for (int co = 0; co < 4; ++co) g4[co] = (zmr[co] + z0[co]) + zpr[co];
+    } else {
+      const float4 up = zms[tid - TW], dn = zps[tid + TW];
+      g4[0] = (up.x + z0[0]) + dn.x;
+      g4[1] = (up.y + z0[1]) + dn.y;
+      g4[2] = (up.z + z0[2]) + dn.z;
+      g4[3] = (up.w + z0[3]) + dn.w;
     }
-    if constexpr (CMF || CM32) {
-      const float4 yv = *reinterpret_cast<const float4*>(yb + 32);
-      g4[0] += yv.x;
-      g4[1] += yv.y;
-      g4[2] += yv.z;
-      g4[3] += yv.w;
-    }
+    if (BAL) {   // chunk 3 left -sum in the accumulators
+#pragma unroll
+      for (int co = 0; co < 4; ++co) g4[co] = -g4[co];
     }
     const float pe = ldexpf(1.0f, e);
     const float isc = P[a.off_owm_scale] * pe;
@@ -1176,13 +1124,12 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
 // The kernel: a block takes a.omega_ipb consecutive items (default 1).  A tile's (view, plane)
 // items are consecutive on one XCD (xcd_tile): the reference tile, and a view's source box
 // across the npl neighbouring planes, come from its L2.
-// the eval sweep's omega_mfma variant (A/B builds only: -DAARMVS_OMEGA_EVAL_ABL=1024 puts the
-// centre tap on the matrix cores; the library is built with 0)
-#ifndef AARMVS_OMEGA_EVAL_ABL
-#define AARMVS_OMEGA_EVAL_ABL 0
+// (AARMVS_OMEGA_WAVES: the minimum waves per SIMD the compiler is held to; A/B builds only)
+#ifndef AARMVS_OMEGA_WAVES
+#define AARMVS_OMEGA_WAVES 4
 #endif
 template <int ABL = 0, int TW = kOmegaTW, bool BAL = false>
-__global__ void __launch_bounds__(OmegaTile<TW>::NT) __attribute__((amdgpu_waves_per_eu((ABL & 1024) ? 3 : 4)))
+__global__ void __launch_bounds__(OmegaTile<TW>::NT) __attribute__((amdgpu_waves_per_eu(AARMVS_OMEGA_WAVES)))
 omega_mfma_kernel(PipeArgs a, const float* __restrict__ P, const float* __restrict__ Rel,
                   const unsigned* __restrict__ xbound) {
   if (blockDim.x != OmegaTile<TW>::NT) return;   // LDS images are sized for exactly this block
@@ -1340,10 +1287,8 @@ static PipeArgs pipe_args(const CostArgs& ca, const SweepGeom& g, const Workspac
   a.omega_k = 0;
   a.off_ow0 = L.pk_off[P_OW0];
   a.off_ow0t = L.ow0t_off;
-  a.off_owc = L.owc_off;
   a.off_owb_scale = L.owb_scale_off;
   a.off_owm = L.owm_off;
-  a.off_owmc = L.owmc_off;
   a.off_owm_scale = L.owb_scale_off;
   a.off_ob0 = L.pk_off[P_OB0];
   a.off_og0w = L.pk_off[P_OG0W];
@@ -1440,7 +1385,7 @@ hipError_t launch_omega_group(const CostArgs& ca, const SweepGeom& g, const Work
       hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW, true>), dim3(nblk, 1, g.B),
                          dim3(OmegaTile<kOmegaTW>::NT), 0, s, a, a.params, a.rel, ws.xbound);
     else
-      hipLaunchKernelGGL((omega_mfma_kernel<AARMVS_OMEGA_EVAL_ABL, kOmegaTW>), dim3(nblk, 1, g.B),
+      hipLaunchKernelGGL((omega_mfma_kernel<0, kOmegaTW>), dim3(nblk, 1, g.B),
                          dim3(OmegaTile<kOmegaTW>::NT), 0, s, a, a.params, a.rel, ws.xbound);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

@@ -87,11 +87,11 @@ int main(int argc, char** argv) {
     PipeArgs a = a0;
     a.npl = 8; a.t1_kstride = (size_t)B * nsrc * HW; a.st_kstride = ws.omega_stats_bytes / 8;
     a.d_next = 1; a.t1_next = t1o; a.st_next = sto;
-    const int ntm = OmegaTile<32>::tiles(H, W);
-    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, dim3(ntm * nsrc * 8, 1, B), dim3(OmegaTile<32>::NT), 0, 0, a, dpar, drel, ws.xbound);
+    const int ntm = OmegaTile<16>::tiles(H, W);
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, dim3(ntm * nsrc * 8, 1, B), dim3(OmegaTile<16>::NT), 0, 0, a, dpar, drel, ws.xbound);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
-    for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(kern, dim3(ntm * nsrc * 8, 1, B), dim3(OmegaTile<32>::NT), 0, 0, a, dpar, drel, ws.xbound);
+    for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(kern, dim3(ntm * nsrc * 8, 1, B), dim3(OmegaTile<16>::NT), 0, 0, a, dpar, drel, ws.xbound);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     printf("omega_mfma npl=8 %-34s %8.3f ms/plane\n", name, ms / 5 / 8);
@@ -101,14 +101,14 @@ int main(int argc, char** argv) {
   float4* t1b; double* stb; float* xb;
   CK(hipMalloc(&t1b, 8 * t1k * 16)); CK(hipMalloc(&stb, 8 * stk * 8)); CK(hipMalloc(&xb, 8 * xk * 4));
   CK(hipMemset(stb, 0, 8 * stk * 8));
-  const int ntm = OmegaTile<32>::tiles(H, W);
+  const int ntm = OmegaTile<16>::tiles(H, W);
   const double bc = (128.0 * (nsrc + 1) + 16.0 * nsrc) * HW;
   const double bx = 128.0 * (nsrc + 2) * HW;
   for (int npl : {1, 2, 4, 8}) {
     PipeArgs a = a0;
     a.npl = npl; a.t1_kstride = t1k; a.st_kstride = stk; a.x_kstride = xk;
     a.d_next = 1; a.t1_next = t1b; a.st_next = stb;
-    auto om = [&] { hipLaunchKernelGGL((omega_mfma_kernel<0, 32>), dim3(ntm * nsrc * npl, 1, B), dim3(OmegaTile<32>::NT), 0, 0, a, dpar, drel, ws.xbound); };
+    auto om = [&] { hipLaunchKernelGGL((omega_mfma_kernel<0, 16>), dim3(ntm * nsrc * npl, 1, B), dim3(OmegaTile<16>::NT), 0, 0, a, dpar, drel, ws.xbound); };
     for (int i = 0; i < 2; ++i) om();
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
@@ -117,75 +117,28 @@ int main(int argc, char** argv) {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     printf("omega_mfma npl=%d  %8.3f ms/plane  %7.0f GB/s algorithmic\n", npl, ms / 10 / npl, bc * npl / (ms / 10) / 1e6);
     if (npl == 8) {
-      {
-        std::vector<float4> h0(8 * t1k), h1(8 * t1k);
-        CK(hipMemcpy(h0.data(), t1b, 8 * t1k * 16, hipMemcpyDeviceToHost));
-        ablate("double-buffered box (256)", omega_mfma_kernel<256, 32>, t1b, stb);
-        CK(hipMemcpy(h1.data(), t1b, 8 * t1k * 16, hipMemcpyDeviceToHost));
-        printf("  DB t1 vs default: %s\n", memcmp(h0.data(), h1.data(), 8 * t1k * 16) ? "DIFFERENT" : "identical");
-      }
-      {
-        // 256-thread blocks (16 x 16 haloed tiles): 4 blocks per CU
-        std::vector<float4> h0(8 * t1k), h1(8 * t1k);
-        ablate("default (0)", omega_mfma_kernel<0, 32>, t1b, stb);
-        CK(hipMemcpy(h0.data(), t1b, 8 * t1k * 16, hipMemcpyDeviceToHost));
-        PipeArgs a = a0;
-        a.npl = 8; a.t1_kstride = t1k; a.st_kstride = stk; a.d_next = 1; a.t1_next = t1b; a.st_next = stb;
-        const int nt16 = OmegaTile<16>::tiles(H, W);
-        a.part_n = nt16;
-        auto k16 = [&] { hipLaunchKernelGGL((omega_mfma_kernel<0, 16>), dim3(nt16 * nsrc * 8, 1, B), dim3(OmegaTile<16>::NT), 0, 0, a, dpar, drel, ws.xbound); };
-        for (int i = 0; i < 2; ++i) k16();
-        CK(hipDeviceSynchronize());
-        CK(hipEventRecord(e0));
-        for (int i = 0; i < 5; ++i) k16();
-        CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-        float ms2; CK(hipEventElapsedTime(&ms2, e0, e1));
-        CK(hipMemcpy(h1.data(), t1b, 8 * t1k * 16, hipMemcpyDeviceToHost));
-        size_t nd = 0; double mx = 0;
-        for (size_t i = 0; i < 8 * t1k; ++i) {
-          const float* x = &h0[i].x; const float* y = &h1[i].x;
-          for (int j = 0; j < 4; ++j) { double d = fabs((double)x[j] - y[j]); if (d > 0) { ++nd; mx = d > mx ? d : mx; } }
-        }
-        printf("omega_mfma npl=8 16x16 tiles, 256 threads           %8.3f ms/plane  (t1 vs 16x32: %zu differ, max %.3g)\n", ms2 / 5 / 8, nd, mx);
-        auto t16 = [&](const char* name, auto kern) {
-          for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, dim3(nt16 * nsrc * 8, 1, B), dim3(OmegaTile<16>::NT), 0, 0, a, dpar, drel, ws.xbound);
-          CK(hipDeviceSynchronize());
-          CK(hipEventRecord(e0));
-          for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(kern, dim3(nt16 * nsrc * 8, 1, B), dim3(OmegaTile<16>::NT), 0, 0, a, dpar, drel, ws.xbound);
-          CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-          float m3; CK(hipEventElapsedTime(&m3, e0, e1));
-          printf("omega_mfma npl=8 16x16 %-28s %8.3f ms/plane\n", name, m3 / 5 / 8);
-        };
-        t16("double-buffered box (256)", omega_mfma_kernel<256, 16>);
-        t16("no MFMA (1)", omega_mfma_kernel<1, 16>);
-        t16("no box DMA (2)", omega_mfma_kernel<2, 16>);
-        t16("no sampling (4)", omega_mfma_kernel<4, 16>);
-        t16("no Y image (32)", omega_mfma_kernel<32, 16>);
-        t16("skeleton (31)", omega_mfma_kernel<31, 16>);
-      }
-      ablate("no MFMA (1)", omega_mfma_kernel<1, 32>, t1b, stb);
-      ablate("no box DMA (2)", omega_mfma_kernel<2, 32>, t1b, stb);
-      ablate("no sampling (4)", omega_mfma_kernel<4, 32>, t1b, stb);
-      ablate("no ref loads (8)", omega_mfma_kernel<8, 32>, t1b, stb);
-      ablate("no divisions (16)", omega_mfma_kernel<16, 32>, t1b, stb);
-      ablate("double-buffered box (256)", omega_mfma_kernel<256, 32>, t1b, stb);
-      ablate("double-buffered box, no Y image (288)", omega_mfma_kernel<288, 32>, t1b, stb);
-      ablate("no DMA, no sampling (6)", omega_mfma_kernel<6, 32>, t1b, stb);
-      ablate("no DMA/sampling/MFMA/ref (15)", omega_mfma_kernel<15, 32>, t1b, stb);
-      ablate("skeleton (31)", omega_mfma_kernel<31, 32>, t1b, stb);
-      ablate("skeleton, no Y image (63)", omega_mfma_kernel<63, 32>, t1b, stb);
-      ablate("skeleton, no stats atomics (95)", omega_mfma_kernel<95, 32>, t1b, stb);
-      ablate("skeleton, no B loads (159)", omega_mfma_kernel<159, 32>, t1b, stb);
-      ablate("skeleton - Y/atomics/B (255)", omega_mfma_kernel<255, 32>, t1b, stb);
-      ablate("no Y image (32)", omega_mfma_kernel<32, 32>, t1b, stb);
-      ablate("no B loads (128)", omega_mfma_kernel<128, 32>, t1b, stb);
+      ablate("default (0)", omega_mfma_kernel<0, 16>, t1b, stb);
+      ablate("no MFMA (1)", omega_mfma_kernel<1, 16>, t1b, stb);
+      ablate("no box DMA (2)", omega_mfma_kernel<2, 16>, t1b, stb);
+      ablate("no sampling (4)", omega_mfma_kernel<4, 16>, t1b, stb);
+      ablate("no ref loads (8)", omega_mfma_kernel<8, 16>, t1b, stb);
+      ablate("no divisions (16)", omega_mfma_kernel<16, 16>, t1b, stb);
+      ablate("no DMA, no sampling (6)", omega_mfma_kernel<6, 16>, t1b, stb);
+      ablate("no DMA/sampling/MFMA/ref (15)", omega_mfma_kernel<15, 16>, t1b, stb);
+      ablate("skeleton (31)", omega_mfma_kernel<31, 16>, t1b, stb);
+      ablate("skeleton, no Y image (63)", omega_mfma_kernel<63, 16>, t1b, stb);
+      ablate("skeleton, no stats atomics (95)", omega_mfma_kernel<95, 16>, t1b, stb);
+      ablate("skeleton, no B loads (159)", omega_mfma_kernel<159, 16>, t1b, stb);
+      ablate("skeleton - Y/atomics/B (255)", omega_mfma_kernel<255, 16>, t1b, stb);
+      ablate("no Y image (32)", omega_mfma_kernel<32, 16>, t1b, stb);
+      ablate("no B loads (128)", omega_mfma_kernel<128, 16>, t1b, stb);
     }
     // plane npl-1 must equal a single-plane launch at d_next = npl
     if (npl > 1) {
       std::vector<float4> hb(t1k), hs(t1k);
       CK(hipMemcpy(hb.data(), t1b + (npl - 1) * t1k, t1k * 16, hipMemcpyDeviceToHost));
       PipeArgs a1 = a; a1.npl = 1; a1.d_next = npl;
-      hipLaunchKernelGGL((omega_mfma_kernel<0, 32>), dim3(ntm * nsrc, 1, B), dim3(OmegaTile<32>::NT), 0, 0, a1, dpar, drel, ws.xbound);
+      hipLaunchKernelGGL((omega_mfma_kernel<0, 16>), dim3(ntm * nsrc, 1, B), dim3(OmegaTile<16>::NT), 0, 0, a1, dpar, drel, ws.xbound);
       CK(hipDeviceSynchronize());
       CK(hipMemcpy(hs.data(), t1b, t1k * 16, hipMemcpyDeviceToHost));
       printf("  plane %d vs single launch: %s\n", npl - 1, memcmp(hb.data(), hs.data(), t1k * 16) ? "DIFFERENT" : "identical");
