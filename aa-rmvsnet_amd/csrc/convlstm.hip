@@ -153,7 +153,7 @@ struct CellDef<0> {   // [x, h0] @ H
   static constexpr int NP = 2, CH[kMaxParts] = {32, 16, 0};
   static constexpr int MODE[kMaxParts] = {SRC_PLAIN, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16;
-  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1, H3PIPE = 1;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1, H3PIPE = 1, H3MS = 1;
   static constexpr int MIN_WAVES = 1;   // amdgpu_waves_per_eu lower bound (register budget)
   static constexpr int SKEW = 3;        // CellArgs::skew of the double-buffered kernel
 };
@@ -162,7 +162,7 @@ struct CellDef<1> {   // [maxpool(h0'), h1] @ H/2
   static constexpr int NP = 2, CH[kMaxParts] = {16, 16, 0};
   static constexpr int MODE[kMaxParts] = {SRC_POOL, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16;
-  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1, H3PIPE = 1;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = 1, H3PIPE = 1, H3MS = 1;
   static constexpr int MIN_WAVES = 1;
   static constexpr int SKEW = 2;
 };
@@ -173,7 +173,7 @@ struct CellDef<3> {   // [gnrelu(u0), h1', h3] @ H/2
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 16};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 16;
-  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = AARMVS_C3DB, H3PIPE = 1;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = AARMVS_C3DB, H3PIPE = 1, H3MS = 1;
   static constexpr int MIN_WAVES = 1;
   static constexpr int SKEW = AARMVS_C3SKEW;
 };
@@ -182,7 +182,7 @@ struct CellDef<4> {   // [gnrelu(u1), h0', h4] @ H
   static constexpr int NP = 3, CH[kMaxParts] = {16, 16, 8};
   static constexpr int MODE[kMaxParts] = {SRC_GNRELU, SRC_PLAIN, SRC_PLAIN};
   static constexpr int HID = 8;
-  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = AARMVS_C4DB, H3PIPE = AARMVS_C4PIPE;
+  static constexpr int H3RW = 1, H3WAVES = 8, H3DB = AARMVS_C4DB, H3PIPE = AARMVS_C4PIPE, H3MS = 1;
   // <= 128 VGPRs: two 512-thread blocks per CU (the sign-balanced accumulator pair took the
   // compiler's choice to 130, one block per CU: 160 -> 202 us per plane at the headline)
   static constexpr int MIN_WAVES = 4;
@@ -210,14 +210,18 @@ typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
 // RW: rows (32-pixel n-tiles) per wave -- the A (weight) fragments of a tap are reused
 // RW times; WAVES: waves per block.  Defaults per cell in CellDef.
-template <int KIND, int RW_ = CellDef<KIND>::H3RW, int WAVES_ = CellDef<KIND>::H3WAVES>
+// MS: waves per tile row -- each of a row's MS waves takes MT / MS of the m-tiles (the gates of
+// 8 hidden channels per m-tile: the LSTM update of those channels is the wave's own), so a block
+// of WAVES waves covers WAVES / MS rows
+template <int KIND, int RW_ = CellDef<KIND>::H3RW, int WAVES_ = CellDef<KIND>::H3WAVES, int MS_ = 1>
 struct H3Cfg {
   using D = CellDef<KIND>;
   static constexpr int CIN = D::CH[0] + D::CH[1] + D::CH[2];
   static constexpr int NCHK = (CIN + 15) / 16;
   static constexpr int HID = D::HID, MT = HID / 8, COUT = 4 * HID;
-  static constexpr int RW = RW_, WAVES = WAVES_;
-  static constexpr int TH = RW * WAVES, THREADS = WAVES * 64, TW = 32, W2 = TW + 2, TROWS = TH + 2;
+  static constexpr int RW = RW_, WAVES = WAVES_, MS = MS_, MTL = MT / MS, RWAVES = WAVES / MS;
+  static_assert(MT % MS == 0 && WAVES % MS == 0, "whole m-tiles and rows per wave");
+  static constexpr int TH = RW * RWAVES, THREADS = WAVES * 64, TW = 32, W2 = TW + 2, TROWS = TH + 2;
   static constexpr int NPIX = TROWS * W2;
   static constexpr int A_HALVES = NCHK * 9 * MT * 64 * 8;   // per hi / lo
   static constexpr size_t LDS_BYTES = (size_t)A_HALVES * 2 * 2 + (size_t)NPIX * 32 * 2 + 32 * 4;
@@ -254,9 +258,9 @@ __device__ __forceinline__ uint32_t h3_split2(float a, float b, uint32_t& lo_bit
 // each LDS plane as ONE 16-B store (8 channels as fp16 pairs) at h3_pix(p, h): 2-way bank
 // conflicts at most.  Out-of-image pixels and channels past the chunk's valid count load
 // zeros through the buffer range check.  NTH: staging threads (default: the block).
-template <int KIND, int RW, int WAVES, int NTH = 0, bool PAIRSKIP = false>
+template <int KIND, int RW, int WAVES, int NTH = 0, bool PAIRSKIP = false, int MS = 1>
 struct H3PixStager {
-  using C = H3Cfg<KIND, RW, WAVES>;
+  using C = H3Cfg<KIND, RW, WAVES, MS>;
   using D = typename C::D;
   static constexpr int TH = NTH ? NTH : C::THREADS;   // staging threads
   static constexpr int NITEM = 2 * C::NPIX;
@@ -351,12 +355,12 @@ struct H3PixStager {
 // GroupNorm+ReLU part, staged x 2^-e) to the h parts' scale 2^kHScaleExp (CH is the first chunk
 // past part 0); the epilogue undoes 2^kHScaleExp with the weight scale.
 template <class C, int KIND, int CH, bool BAL>
-__device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], floatx16 (&accn)[C::MT][C::RW],
+__device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MTL][C::RW], floatx16 (&accn)[C::MTL][C::RW],
                                                float xr) {
   if constexpr ((KIND == 0 || C::D::MODE[0] == SRC_GNRELU) && CH > 0 && C::chunk_part(CH) != 0 &&
                 C::chunk_part(CH - 1) == 0) {
 #pragma unroll
-    for (int m = 0; m < C::MT; ++m)
+    for (int m = 0; m < C::MTL; ++m)
 #pragma unroll
       for (int r = 0; r < C::RW; ++r) {
         acc[m][r] *= xr;
@@ -384,10 +388,11 @@ __device__ __forceinline__ void xguard_rescale(floatx16 (&acc)[C::MT][C::RW], fl
 // pack_cell_h3_kernel), so the chunk costs 5 k-steps instead of 9 with a zero K half each;
 // tap 9 of step 4 is a zero weight against tap 8's pixels.
 template <class C, int CH, bool PIPE = false, bool BAL = true, int ONCE = 0>
-__device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], floatx16 (&accn)[C::MT][C::RW],
+__device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MTL][C::RW], floatx16 (&accn)[C::MTL][C::RW],
                                               const char* wl_hi, const char* wl_lo, const char* in_hi,
-                                              const char* in_lo, int wave, int lane) {
-  constexpr int MT = C::MT, RW = C::RW;
+                                              const char* in_lo, int wave, int lane, int m0 = 0) {
+  // wave: the wave's row group (its rows wave RW ..); m0: its first m-tile (H3Cfg::MS)
+  constexpr int MT = C::MT, MTL = C::MTL, RW = C::RW;
   const int col = lane & 31, h = lane >> 5;
   if constexpr (C::chunk_paired(CH)) {
     // (PIPE ignored: the plain fragment schedule.)  The lane's tap offsets are recomputed here
@@ -405,8 +410,8 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], flo
         bl[r] = *reinterpret_cast<const half8*>(in_lo + boff);
       }
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int aoff = ((((CH * 9 + s) * MT + m) * 64) + lane) * 16;
+      for (int m = 0; m < MTL; ++m) {
+        const int aoff = ((((CH * 9 + s) * MT + m0 + m) * 64) + lane) * 16;
         const half8 ah = *reinterpret_cast<const half8*>(wl_hi + aoff);
         const half8 al = *reinterpret_cast<const half8*>(wl_lo + aoff);
 #pragma unroll
@@ -419,7 +424,7 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], flo
       }
     }
   } else if constexpr (PIPE) {
-    half8 bh[2][RW], bl[2][RW], ah[2][MT], al[2][MT];
+    half8 bh[2][RW], bl[2][RW], ah[2][MTL], al[2][MTL];
     auto fetch = [&](int tap, int s) {
       if ((ONCE & 2) && tap > 0) {   // microbenchmark ablation: B fragments of tap 0 only
 #pragma unroll
@@ -433,12 +438,12 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], flo
       }
       if ((ONCE & 1) && tap > 0) {   // microbenchmark ablation: A fragments of tap 0 only
 #pragma unroll
-        for (int m = 0; m < MT; ++m) ah[s][m] = ah[s ^ 1][m], al[s][m] = al[s ^ 1][m];
+        for (int m = 0; m < MTL; ++m) ah[s][m] = ah[s ^ 1][m], al[s][m] = al[s ^ 1][m];
         return;
       }
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int aoff = ((((CH * 9 + tap) * MT + m) * 64) + lane) * 16;
+      for (int m = 0; m < MTL; ++m) {
+        const int aoff = ((((CH * 9 + tap) * MT + m0 + m) * 64) + lane) * 16;
         ah[s][m] = *reinterpret_cast<const half8*>(wl_hi + aoff);
         al[s][m] = *reinterpret_cast<const half8*>(wl_lo + aoff);
       }
@@ -450,7 +455,7 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], flo
       if (tap + 1 < 9) fetch(tap + 1, s ^ 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MTL; ++m)
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
           floatx16& d = (BAL && ((tap + CH) & 1)) ? accn[m][r] : acc[m][r];
@@ -472,8 +477,8 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], flo
         bl[r] = *reinterpret_cast<const half8*>(in_lo + boff);
       }
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int aoff = ((((CH * 9 + tap) * MT + m) * 64) + lane) * 16;
+      for (int m = 0; m < MTL; ++m) {
+        const int aoff = ((((CH * 9 + tap) * MT + m0 + m) * 64) + lane) * 16;
         const half8 ah = *reinterpret_cast<const half8*>(wl_hi + aoff);
         const half8 al = *reinterpret_cast<const half8*>(wl_lo + aoff);
 #pragma unroll
@@ -492,16 +497,16 @@ __device__ __forceinline__ void h3_mfma_chunk(floatx16 (&acc)[C::MT][C::RW], flo
 // m*8 + 4 hi .. +3 of pixel (y, x): one 16-B load / store per (m, row).
 template <class C>
 __device__ __forceinline__ void cell_c_load(const CellArgs& a, int b, int yw, int x, int hi,
-                                            float (&cst)[C::MT][C::RW][4]) {
+                                            float (&cst)[C::MTL][C::RW][4], int m0 = 0) {
 #pragma unroll
-  for (int m = 0; m < C::MT; ++m)
+  for (int m = 0; m < C::MTL; ++m)
 #pragma unroll
     for (int r = 0; r < C::RW; ++r) {
       const int y = yw + r;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (y < a.H && x < a.W)
         v = *reinterpret_cast<const float4*>(
-            a.c_in + (((size_t)b * a.H + y) * a.W + x) * C::HID + m * 8 + 4 * hi);
+            a.c_in + (((size_t)b * a.H + y) * a.W + x) * C::HID + (m0 + m) * 8 + 4 * hi);
       cst[m][r][0] = v.x;
       cst[m][r][1] = v.y;
       cst[m][r][2] = v.z;
@@ -511,9 +516,9 @@ __device__ __forceinline__ void cell_c_load(const CellArgs& a, int b, int yw, in
 
 // gate epilogue (module.py:83-90): undo the weight scale, add the bias, LSTM update
 template <class C, int ABL, bool PRECISE>
-__device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 (&acc)[C::MT][C::RW],
-                                              const float (&cst)[C::MT][C::RW][4], float inv_scale,
-                                              int b, int yw, int x, int hi) {
+__device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 (&acc)[C::MTL][C::RW],
+                                              const float (&cst)[C::MTL][C::RW][4], float inv_scale,
+                                              int b, int yw, int x, int hi, int m0 = 0) {
   constexpr int HID = C::HID;
 #pragma unroll
   for (int r = 0; r < C::RW; ++r) {
@@ -521,23 +526,24 @@ __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 
     if (y < a.H && x < a.W) {
       const size_t pix = ((size_t)b * a.H + y) * a.W + x;
 #pragma unroll
-      for (int m = 0; m < C::MT; ++m) {
+      for (int ml = 0; ml < C::MTL; ++ml) {
+        const int m = m0 + ml;
         float cn[4], hn[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int ch = m * 8 + 4 * hi + q;
-          const float gi = fmaf(acc[m][r][q], inv_scale, a.bias[ch]);
-          const float gf = fmaf(acc[m][r][4 + q], inv_scale, a.bias[HID + ch]);
-          const float go = fmaf(acc[m][r][8 + q], inv_scale, a.bias[2 * HID + ch]);
-          const float gg = fmaf(acc[m][r][12 + q], inv_scale, a.bias[3 * HID + ch]);
+          const float gi = fmaf(acc[ml][r][q], inv_scale, a.bias[ch]);
+          const float gf = fmaf(acc[ml][r][4 + q], inv_scale, a.bias[HID + ch]);
+          const float go = fmaf(acc[ml][r][8 + q], inv_scale, a.bias[2 * HID + ch]);
+          const float gg = fmaf(acc[ml][r][12 + q], inv_scale, a.bias[3 * HID + ch]);
           if (ABL & 4) {
             cn[q] = gi + gf;
-            hn[q] = go + gg + cst[m][r][q];
+            hn[q] = go + gg + cst[ml][r][q];
           } else if (PRECISE) {   // the training sweep: unbiased activations (device_common.h)
-            cn[q] = precise_sigmoid(gf) * cst[m][r][q] + precise_sigmoid(gi) * precise_tanh(gg);
+            cn[q] = precise_sigmoid(gf) * cst[ml][r][q] + precise_sigmoid(gi) * precise_tanh(gg);
             hn[q] = precise_sigmoid(go) * precise_tanh(cn[q]);
           } else {
-            cn[q] = fast_sigmoid(gf) * cst[m][r][q] + fast_sigmoid(gi) * fast_tanh(gg);
+            cn[q] = fast_sigmoid(gf) * cst[ml][r][q] + fast_sigmoid(gi) * fast_tanh(gg);
             hn[q] = fast_sigmoid(go) * fast_tanh(cn[q]);
           }
         }
@@ -555,7 +561,7 @@ __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int ch = m * 8 + 4 * hi + q;
-              zz[q] = fmaf(acc[m][r][4 * gt + q], inv_scale, a.bias[gt * HID + ch]);
+              zz[q] = fmaf(acc[ml][r][4 * gt + q], inv_scale, a.bias[gt * HID + ch]);
             }
             *reinterpret_cast<float4*>(zo + gt * P * 4) = make_float4(zz[0], zz[1], zz[2], zz[3]);
           }
@@ -569,12 +575,12 @@ __device__ __forceinline__ void cell_epilogue(const CellArgs& a, const floatx16 
 // ablation bits for the microbenchmark only (1 no MFMA, 2 no staging loads/stores, 4 no
 // gate math, 8 / 16 the A / B fragments read for tap 0 only)
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
-          int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false>
+          int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false, int MS = 1>
 __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(CellDef<KIND>::MIN_WAVES))) lstm_cell_h3_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
-  using C = H3Cfg<KIND, RW, WAVES>;
+  using C = H3Cfg<KIND, RW, WAVES, MS>;
   using D = typename C::D;
-  constexpr int MT = C::MT, NCHK = C::NCHK;
+  constexpr int MT = C::MTL, NCHK = C::NCHK;
   extern __shared__ __attribute__((aligned(16))) char lds_h3[];
   char* wl_hi = lds_h3;
   char* wl_lo = wl_hi + C::A_HALVES * 2;
@@ -607,7 +613,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
   };
   // the inference cells skip a paired chunk's unused half; the training cells (PRECISE) keep
   // the uniform staging loop (skipping it costs the 128-VGPR cell 4 spills there)
-  H3PixStager<KIND, RW, WAVES, 0, !PRECISE> st;
+  H3PixStager<KIND, RW, WAVES, 0, !PRECISE, MS> st;
   const int xe = KIND == 0 ? xguard_exp(a.xbound)
                  : D::MODE[0] == SRC_GNRELU ? gguard_exp(a.part[0].gamma, a.part[0].beta, H, W) : 0;
   st.xs = ldexpf(1.0f, -xe);
@@ -619,13 +625,14 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
     st.template load<0>(a, b, y0, x0, tid);
   }
   const int hi = lane >> 5, col = lane & 31;
+  const int rwave = wave % C::RWAVES, m0 = (wave / C::RWAVES) * C::MTL;   // row group, m-tiles
   for (; tile < ntiles; tile += gridDim.x) {
     int b, y0, x0;
     coords(tile, b, y0, x0);
     const int next = tile + (int)gridDim.x;
     int nb = 0, ny0 = 0, nx0 = 0;
     if (next < ntiles) coords(next, nb, ny0, nx0);
-    const int yw = y0 + wave * RW;   // this wave's first row
+    const int yw = y0 + rwave * RW;   // this wave's first row
     floatx16 acc[MT][RW], accn[MT][RW];   // sign-balanced pair (h3_mfma_chunk)
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -646,9 +653,9 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
       } else if (next < ntiles) {
         st.template load<0>(a, nb, ny0, nx0, tid);
       }
-      if (CH == 0) cell_c_load<C>(a, b, yw, x0 + col, hi, cst);
+      if (CH == 0) cell_c_load<C>(a, b, yw, x0 + col, hi, cst, m0);
       xguard_rescale<C, KIND, CH, PRECISE>(acc, accn, xr);
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE, (ABL >> 3) & 3>(acc, accn, wl_hi, wl_lo, in_hi, in_lo, wave, lane);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE, (ABL >> 3) & 3>(acc, accn, wl_hi, wl_lo, in_hi, in_lo, rwave, lane, m0);
     };
     chunk(std::integral_constant<int, 0>{});
     if constexpr (NCHK > 1) chunk(std::integral_constant<int, 1>{});
@@ -658,7 +665,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int r = 0; r < RW; ++r)
         if constexpr (PRECISE) acc[m][r] -= accn[m][r];
-    cell_epilogue<C, ABL, PRECISE>(a, acc, cst, inv_scale, b, yw, x0 + col, hi);
+    cell_epilogue<C, ABL, PRECISE>(a, acc, cst, inv_scale, b, yw, x0 + col, hi, m0);
   }
 }
 
@@ -669,12 +676,12 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
 // the chunk after that; at a tile's last chunk, the gate epilogue.  Across the two
 // waves of a SIMD one wave's staging VALU work fills the other's MFMA issue gaps.
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
-          int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false>
+          int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false, int MS = 1>
 __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(CellDef<KIND>::MIN_WAVES))) lstm_cell_h3db_kernel(
     CellArgs a, const float* __restrict__ inv_scale_ptr) {
-  using C = H3Cfg<KIND, RW, WAVES>;
+  using C = H3Cfg<KIND, RW, WAVES, MS>;
   using D = typename C::D;
-  constexpr int MT = C::MT, NCHK = C::NCHK;
+  constexpr int MT = C::MTL, NCHK = C::NCHK;
   constexpr int PB = C::NPIX * 32;   // one plane (hi or lo) of one input buffer
   static_assert(NCHK >= 2, "two or more input chunks");
   extern __shared__ __attribute__((aligned(16))) char lds_h3[];
@@ -706,7 +713,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
   };
   int tile = blockIdx.x;
   if (tile >= ntiles) return;   // whole block
-  H3PixStager<KIND, RW, WAVES> st;
+  H3PixStager<KIND, RW, WAVES, 0, false, MS> st;
   const int xe = KIND == 0 ? xguard_exp(a.xbound)
                  : D::MODE[0] == SRC_GNRELU ? gguard_exp(a.part[0].gamma, a.part[0].beta, H, W) : 0;
   st.xs = ldexpf(1.0f, -xe);
@@ -722,13 +729,14 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
   __syncthreads();
   int par = 0;
   const int hi = lane >> 5, col = lane & 31;
+  const int rwave = wave % C::RWAVES, m0 = (wave / C::RWAVES) * C::MTL;   // row group, m-tiles
   const bool early = a.skew > 0 && ((wave >> (a.skew - 1)) & 1) != 0;
   for (; tile < ntiles; tile += gridDim.x) {
     coords(tile, b, y0, x0);
     const int next = tile + (int)gridDim.x;
     int nb = 0, ny0 = 0, nx0 = 0;
     if (next < ntiles) coords(next, nb, ny0, nx0);
-    const int yw = y0 + wave * RW;   // this wave's first row
+    const int yw = y0 + rwave * RW;   // this wave's first row
     const int x = x0 + col;
     floatx16 acc[MT][RW], accn[MT][RW];   // sign-balanced pair (h3_mfma_chunk)
     float cst[MT][RW][4];
@@ -738,7 +746,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
       for (int r = 0; r < RW; ++r)
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[m][r][j] = accn[m][r][j] = 0.0f;
-    cell_c_load<C>(a, b, yw, x, hi, cst);
+    cell_c_load<C>(a, b, yw, x, hi, cst, m0);
     auto step = [&](auto CHc) {
       constexpr int CH = decltype(CHc)::value;
       constexpr bool F_NEXT = CH + 1 >= NCHK;   // following chunk: the next tile's first
@@ -765,7 +773,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
       // either order is safe and the results are the same.
       if (early) stage();
       xguard_rescale<C, KIND, CH, PRECISE>(acc, accn, xr);
-      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE, (ABL >> 3) & 3>(acc, accn, wl_hi, wl_lo, cur, cur + PB, wave, lane);
+      if (!(ABL & 1)) h3_mfma_chunk<C, CH, PIPE != 0, PRECISE, (ABL >> 3) & 3>(acc, accn, wl_hi, wl_lo, cur, cur + PB, rwave, lane, m0);
       if (!early) stage();
       if constexpr (CH == NCHK - 1) {
 #pragma unroll
@@ -773,7 +781,7 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
           for (int r = 0; r < RW; ++r)
             if constexpr (PRECISE) acc[m][r] -= accn[m][r];
-        cell_epilogue<C, ABL, PRECISE>(a, acc, cst, inv_scale, b, yw, x, hi);
+        cell_epilogue<C, ABL, PRECISE>(a, acc, cst, inv_scale, b, yw, x, hi, m0);
       }
       __syncthreads();   // buffer `oth` staged; buffer `cur` free for the step after next
       par ^= 1;
@@ -793,14 +801,15 @@ __global__ void __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu
 // with the double-buffered kernel's wave halves skewed (CellDef::SKEW) cell 3 is faster
 // double-buffered too (95.0 -> 90.8 us per plane in the sweep), cell 4 still is not (161 -> 200).
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
-          int DB = CellDef<KIND>::H3DB, int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false>
+          int DB = CellDef<KIND>::H3DB, int PIPE = CellDef<KIND>::H3PIPE, bool PRECISE = false,
+          int MS = CellDef<KIND>::H3MS>
 static hipError_t run_cell_h3_(const CellArgs& a, const float* inv_scale, int cu, int kid,
                                hipStream_t s) {
-  using C = H3Cfg<KIND, RW, WAVES>;
+  using C = H3Cfg<KIND, RW, WAVES, MS>;
   constexpr size_t lds = C::LDS_BYTES + (DB ? (size_t)C::NPIX * 32 * 2 : 0);
   static_assert(lds <= 160 * 1024, "h3 cell tile exceeds LDS");
-  const void* fn = DB ? (const void*)lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE>
-                      : (const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE>;
+  const void* fn = DB ? (const void*)lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE, MS>
+                      : (const void*)lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE, MS>;
   static bool attr_set[kMaxDevices] = {};
   if (hipError_t e = ensure_dyn_lds(fn, (int)lds, attr_set); e != hipSuccess) return e;
   const int ntiles = a.B * ((a.W + C::TW - 1) / C::TW) * ((a.H + C::TH - 1) / C::TH);
@@ -816,21 +825,49 @@ static hipError_t run_cell_h3_(const CellArgs& a, const float* inv_scale, int cu
   ak.skew = skew_env >= 0 ? skew_env : CellDef<KIND>::SKEW;
   ProfScope ps(s, kid);
   if (DB)
-    hipLaunchKernelGGL((lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE>), dim3(grid),
+    hipLaunchKernelGGL((lstm_cell_h3db_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE, MS>), dim3(grid),
                        dim3(C::THREADS), lds, s, ak, inv_scale);
   else
-    hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE>), dim3(grid),
+    hipLaunchKernelGGL((lstm_cell_h3_kernel<KIND, RW, WAVES, ABL, PIPE, PRECISE, MS>), dim3(grid),
                        dim3(C::THREADS), lds, s, ak, inv_scale);
   return hipGetLastError();
 }
 // The training sweep (a.z_out set: the record for the BPTT) runs the unbiased gate activations
 // (PRECISE, device_common.h); the inference sweep the fast ones.
 template <int KIND, int RW = CellDef<KIND>::H3RW, int WAVES = CellDef<KIND>::H3WAVES, int ABL = 0,
-          int DB = CellDef<KIND>::H3DB, int PIPE = CellDef<KIND>::H3PIPE>
+          int DB = CellDef<KIND>::H3DB, int PIPE = CellDef<KIND>::H3PIPE, int MS = CellDef<KIND>::H3MS>
 static hipError_t run_cell_h3(const CellArgs& a, const float* inv_scale, int cu, int kid,
                               hipStream_t s) {
-  return a.z_out ? run_cell_h3_<KIND, RW, WAVES, ABL, DB, PIPE, true>(a, inv_scale, cu, kid, s)
-                 : run_cell_h3_<KIND, RW, WAVES, ABL, DB, PIPE, false>(a, inv_scale, cu, kid, s);
+  return a.z_out ? run_cell_h3_<KIND, RW, WAVES, ABL, DB, PIPE, true, MS>(a, inv_scale, cu, kid, s)
+                 : run_cell_h3_<KIND, RW, WAVES, ABL, DB, PIPE, false, MS>(a, inv_scale, cu, kid, s);
+}
+
+// Tile shape of the cells with two or more m-tiles (round 6, second session; every shape is
+// bit-identical, tests/test_gpu_parity.py::test_cell_tile_shapes_are_bit_identical):
+//   0: the CellDef configuration (8 waves, one per 32-pixel row, all m-tiles: 8-row tiles);
+//   1: 8 waves, two per row (H3Cfg MS = 2, each half the m-tiles): 4-row tiles, twice the blocks;
+//   2: 16 waves, two per row: 8-row tiles at four waves per SIMD instead of two.
+// In isolation (tools/microbench/cell_bench.cpp CB_SMALL, profiles/r06s6_cell_shapes.txt) shapes
+// 1 and 2 beat 0 on small grids and on cell 0 at the headline (128x160 cell 0 12 -> 9 us, 1600x1184
+// cell 0 384 -> 314 us).  In the multi-stream sweep they do not (profiles/r06s7_cell_shapes_ab.txt:
+// headline cell 0 300 -> 296 us, cells 1 and 2 1 us slower, config 1 0.353 -> 0.341 G hyp/s --
+// twice the LDS-bound blocks crowd out the units of the other streams, config 2 +1.5%, the
+// training step unchanged), so shape 0 stays the default.  AARMVS_CELL_MS (read per launch)
+// selects a shape for every such cell.
+template <int KIND>
+static int cell_shape(const CellArgs&, int) {
+  const char* e = std::getenv("AARMVS_CELL_MS");
+  return (e && *e) ? std::max(0, std::min(2, std::atoi(e))) : 0;
+}
+template <int KIND>
+static hipError_t run_cell(const CellArgs& a, const float* inv_scale, int cu, int kid, hipStream_t s) {
+  using D = CellDef<KIND>;
+  if constexpr (D::HID >= 16) {
+    const int sh = cell_shape<KIND>(a, cu);
+    if (sh == 1) return run_cell_h3<KIND, 1, 8, 0, D::H3DB, D::H3PIPE, 2>(a, inv_scale, cu, kid, s);
+    if (sh == 2) return run_cell_h3<KIND, 1, 16, 0, D::H3DB, D::H3PIPE, 2>(a, inv_scale, cu, kid, s);
+  }
+  return run_cell_h3<KIND>(a, inv_scale, cu, kid, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1384,19 +1421,19 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
   CellArgs a0 = cell(0, {{x, 32, SRC_PLAIN, nullptr, nullptr, nullptr},
                          {io.h_prev[0], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 1);
   a0.xbound = ws.xbound;
-  if ((e = run_cell_h3<0>(a0, params + L.h3_scale_off + 0, cu, K_CELL0, s)) != hipSuccess) return e;
+  if ((e = run_cell<0>(a0, params + L.h3_scale_off + 0, cu, K_CELL0, s)) != hipSuccess) return e;
   }
   if (stages & 2) {
   // cell 1: [maxpool(h0'), h1] @ H/2
   CellArgs a1 = cell(1, {{io.h_new[0], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {io.h_prev[1], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 2);
-  if ((e = run_cell_h3<1>(a1, params + L.h3_scale_off + 1, cu, K_CELL1, s)) != hipSuccess) return e;
+  if ((e = run_cell<1>(a1, params + L.h3_scale_off + 1, cu, K_CELL1, s)) != hipSuccess) return e;
   }
   if (stages & 4) {
   // cell 2: [maxpool(h1'), h2] @ H/4
   CellArgs a2 = cell(2, {{io.h_new[1], 16, SRC_POOL, nullptr, nullptr, nullptr},
                          {io.h_prev[2], 16, SRC_PLAIN, nullptr, nullptr, nullptr}}, 4);
-  if ((e = run_cell_h3<2>(a2, params + L.h3_scale_off + 2, cu, K_CELL2, s)) != hipSuccess) return e;
+  if ((e = run_cell<2>(a2, params + L.h3_scale_off + 2, cu, K_CELL2, s)) != hipSuccess) return e;
   }
   // GroupNorm statistics are per batch element, so the two cells that consume the deconvs'
   // normalised outputs are launched per batch element; each reduces its element's deconv
@@ -1426,7 +1463,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
                            {io.h_prev[3] + b * 16 * hq, 16, SRC_PLAIN, nullptr, nullptr, nullptr}},
                        2);
     per_b(a3, b, hq, 16);
-    if ((e = run_cell_h3<3>(a3, params + L.h3_scale_off + 3, cu, K_CELL3, s)) != hipSuccess) return e;
+    if ((e = run_cell<3>(a3, params + L.h3_scale_off + 3, cu, K_CELL3, s)) != hipSuccess) return e;
   }
   }
   if (!(stages & 16)) return hipSuccess;
@@ -1454,7 +1491,7 @@ hipError_t launch_unet_step(const float* x, const float* params, const SweepGeom
                            {io.h_prev[4] + b * 8 * hw, 8, SRC_PLAIN, nullptr, nullptr, nullptr}},
                        1);
     per_b(a4, b, hw, 8);
-    if ((e = run_cell_h3<4>(a4, params + L.h3_scale_off + 4, cu, K_CELL4, s)) != hipSuccess) return e;
+    if ((e = run_cell<4>(a4, params + L.h3_scale_off + 4, cu, K_CELL4, s)) != hipSuccess) return e;
   }
   return hipSuccess;
 }

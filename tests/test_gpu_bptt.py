@@ -135,6 +135,22 @@ def test_recorded_forward_streams_are_bit_identical(monkeypatch, nreg, shape):
         assert torch.equal(rec1[k], rec2[k]), k
 
 
+@pytest.mark.parametrize("ms", ["0", "1", "2"])
+def test_recorded_forward_cell_shapes_are_bit_identical(monkeypatch, ms):
+    """The training forward's cells (unbiased gates, sign-balanced accumulators, the gate
+    record) in each tile shape (AARMVS_CELL_MS, convlstm.hip cell_shape) against the default:
+    the cost volume and every record tensor bit for bit."""
+    B, N, H, W, D = 1, 3, 72, 96, 3
+    sc, P, feats, proj, dv, sw, args = _setup(B, N, H, W, D, 8, 4)
+    cost1, rec1, _ = _record_forward(sw, args, B, H, W, D, zero=True)
+    monkeypatch.setenv("AARMVS_CELL_MS", ms)
+    cost2, rec2, _ = _record_forward(sw, args, B, H, W, D, zero=True)
+    torch.cuda.synchronize()
+    assert torch.equal(cost1, cost2)
+    for k in rec1:
+        assert torch.equal(rec1[k], rec2[k]), k
+
+
 # float32 CPU autograd's error depends on its reduction order, which ATen picks by thread count:
 # e.g. omega.reweight_network.2.bias of shape (2, 4, 24, 40, 5), a sum with heavy cancellation,
 # is 5.0e-7 off float64 with 1 thread and 2.0e-5 with 2-8 (DESIGN.md §6).  The float32 reference

@@ -4,6 +4,7 @@
 #include "../../aa-rmvsnet_amd/csrc/convlstm.hip"
 
 #include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -21,7 +22,10 @@ static float* rnd_buf(size_t n, float scale) {
 }
 
 int main() {
-  const int H = 1184, W = 1600, B = 1;
+  // CB_H / CB_W: another geometry (e.g. config 1's 128 x 160), CB_SMALL=1: the library configs
+  // and the cell-0 ablations only
+  const int H = getenv("CB_H") ? atoi(getenv("CB_H")) : 1184, W = getenv("CB_W") ? atoi(getenv("CB_W")) : 1600, B = 1;
+  const bool small = getenv("CB_SMALL") && atoi(getenv("CB_SMALL"));
   const size_t HW = (size_t)H * W;
   float* x32 = rnd_buf(32 * HW, 4.f);
   float* f16a = rnd_buf(16 * HW, 2.f);
@@ -73,6 +77,50 @@ int main() {
   const double fl0 = 2.0 * 9 * 48 * 64 * HW, fl1 = 2.0 * 9 * 32 * 64 * HW / 4, fl3 = 2.0 * 9 * 48 * 64 * HW / 4,
                fl4 = 2.0 * 9 * 40 * 32 * HW;
   auto h3 = [&](CellArgs a) { a.wpk = reinterpret_cast<const float*>(wh); return a; };
+  if (small) {
+    {   // MS=2 against the library config: h and c bit-identical (fresh c for each)
+      std::vector<float> c0(16 * HW), h1(16 * HW), h2(16 * HW), c1(16 * HW), c2(16 * HW);
+      CK(hipMemcpy(c0.data(), cst, 16 * HW * 4, hipMemcpyDeviceToHost));
+      auto once = [&](auto fn, std::vector<float>& ho, std::vector<float>& co) {
+        CK(hipMemcpy(cst, c0.data(), 16 * HW * 4, hipMemcpyHostToDevice));
+        CK(fn()); CK(hipDeviceSynchronize());
+        CK(hipMemcpy(ho.data(), hout, 16 * HW * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(co.data(), cst, 16 * HW * 4, hipMemcpyDeviceToHost));
+      };
+      auto cmp = [&](const char* name, auto f1, auto f2, size_t n) {
+        once(f1, h1, c1); once(f2, h2, c2);
+        const bool same = !memcmp(h1.data(), h2.data(), n * 4) && !memcmp(c1.data(), c2.data(), n * 4);
+        printf("  %s: MS2 vs library %s\n", name, same ? "bit-identical" : "DIFFERENT");
+      };
+      cmp("cell0", [&] { return run_cell_h3<0, 1, 8, 0, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); },
+          [&] { return run_cell_h3<0, 1, 16, 0, 1, 1, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, 16 * HW);
+      cmp("cell1", [&] { return run_cell_h3<1, 1, 8, 0, 1, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); },
+          [&] { return run_cell_h3<1, 1, 16, 0, 1, 1, 2>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, 16 * HW / 4);
+      cmp("cell3", [&] { return run_cell_h3<3, 1, 8, 0, 1, 1>(h3(args(3, 2)), invs, 256, K_CELL3, 0); },
+          [&] { return run_cell_h3<3, 1, 16, 0, 1, 1, 2>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, 16 * HW / 4);
+      CK(hipMemcpy(cst, c0.data(), 16 * HW * 4, hipMemcpyHostToDevice));
+    }
+    run("cell0 h3 DB1 PIPE1 (library)", [&] { return run_cell_h3<0, 1, 8, 0, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+    run("cell0 DB1 no MFMA (1)", [&] { return run_cell_h3<0, 1, 8, 1, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+    run("cell0 DB1 no staging (2)", [&] { return run_cell_h3<0, 1, 8, 2, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+    run("cell0 DB1 no gates (4)", [&] { return run_cell_h3<0, 1, 8, 4, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+    run("cell0 DB1 skeleton (7)", [&] { return run_cell_h3<0, 1, 8, 7, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+    run("cell0 RW1 W4 DB1", [&] { return run_cell_h3<0, 1, 4, 0, 1, 1>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+    run("cell0 W16 MS2 DB1 PIPE1", [&] { return run_cell_h3<0, 1, 16, 0, 1, 1, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+    run("cell0 W16 MS2 DB1 PIPE0", [&] { return run_cell_h3<0, 1, 16, 0, 1, 0, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+    run("cell0 W16 MS2 DB0 PIPE1", [&] { return run_cell_h3<0, 1, 16, 0, 0, 1, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+    run("cell0 W8 MS2 DB1 PIPE1", [&] { return run_cell_h3<0, 1, 8, 0, 1, 1, 2>(h3(args(0, 1)), invs, 256, K_CELL0, 0); }, fl0);
+    run("cell1 W16 MS2 DB1 PIPE1", [&] { return run_cell_h3<1, 1, 16, 0, 1, 1, 2>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+    run("cell1 W8 MS2 DB1 PIPE1", [&] { return run_cell_h3<1, 1, 8, 0, 1, 1, 2>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+    run("cell3 W16 MS2 DB1 PIPE1", [&] { return run_cell_h3<3, 1, 16, 0, 1, 1, 2>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+    run("cell3 W8 MS2 DB1 PIPE1", [&] { return run_cell_h3<3, 1, 8, 0, 1, 1, 2>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+    run("cell1 h3 DB1 PIPE1 (library)", [&] { return run_cell_h3<1, 1, 8, 0, 1, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+    run("cell1 DB1 skeleton (7)", [&] { return run_cell_h3<1, 1, 8, 7, 1, 1>(h3(args(1, 2)), invs, 256, K_CELL1, 0); }, fl1);
+    run("cell3 h3 DB1 PIPE1 (library)", [&] { return run_cell_h3<3, 1, 8, 0, 1, 1>(h3(args(3, 2)), invs, 256, K_CELL3, 0); }, fl3);
+    run("cell4 h3 DB0 PIPE0 (library)", [&] { return run_cell_h3<4, 1, 8, 0, 0, 0>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+    run("cell4 DB0 skeleton (7)", [&] { return run_cell_h3<4, 1, 8, 7, 0, 0>(h3(args(4, 1)), invs, 256, K_CELL4, 0); }, fl4);
+    return 0;
+  }
   {
     const int Hi = H / 2, Wi = W / 2;
     const dim3 grid((Wi + kDpTW - 1) / kDpTW, (Hi + kDpTH - 1) / kDpTH, B);
