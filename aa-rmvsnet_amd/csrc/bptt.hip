@@ -528,6 +528,18 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(GnbArgs a) {
     }
   }
   __syncthreads();
+  // the 36 block-uniform coefficients in scalar registers (read from LDS into VGPRs they held
+  // 36 more VGPRs through the loop: 176, two waves per SIMD)
+  float ca[16], cb[16], mrs[2][2];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    ca[c] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(coef[0][c])));
+    cb[c] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(coef[1][c])));
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) mrs[g][k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(mr[g][k])));
   double s[36];   // fp64: cancelling sums
 #pragma unroll
   for (int i = 0; i < 36; ++i) s[i] = 0.0;
@@ -542,9 +554,9 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(GnbArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c = 4 * q + i, grp = c >> 3;
-        const float yv = fmaf(U[i], coef[0][c], coef[1][c]);
+        const float yv = fmaf(U[i], ca[c], cb[c]);
         const float gn = yv > 0.f ? G[i] : 0.f;
-        const float xh = (U[i] - mr[grp][0]) * mr[grp][1];
+        const float xh = (U[i] - mrs[grp][0]) * mrs[grp][1];
         const float gxh = gn * a.gamma[c];
         s[2 * grp] += gxh;
         s[2 * grp + 1] += gxh * xh;
@@ -1212,11 +1224,14 @@ __global__ void __launch_bounds__(256) deconv_wgrad_kernel(DcwArgs a) {
 }
 
 // conv_0 (head) weight / bias gradient over a group: gW[ci][tap] = sum gcost[p] h4[p + off][ci],
-// gb = sum gcost.  Thread per pixel (32-bit index arithmetic: the caller checks the group's
-// pixel count), 73 sums, block reduce, one partial of kHwPart floats per block.  (Round 6: the
-// transposed form -- each h4 pixel read once, the nine gcost neighbours from L1 -- measured
-// 454 against 432 us per 16-plane group at 640x512: the 73 accumulators and the block reduce,
-// not the h4 reads, bound it.)
+// gb = sum gcost.  A lane pair per (sample, pixel) walks the group's planes, lane h taking input
+// channels 4 h .. 4 h + 3 (one 16-B load per tap, 36 sums): the tap offsets and their in-image
+// tests are formed once, and every plane's 9 loads are unconditional (a tap outside the image
+// reads its clamped neighbour with a zero weight), so they issue together.  Block reduce of the
+// 73 sums through LDS, one partial of kHwPart floats per block.  (Round 6, second session: the thread-per-
+// (plane, pixel) form -- three runtime divisions per pixel and a branch around every tap's loads
+// -- took 432 us per 16-plane group at 640x512, latency-bound on the loads one tap at a time; the
+// transposed form 454 us.)
 constexpr int kHwBlocks = 1024, kHwPart = 80;
 static_assert((size_t)kHwBlocks * kHwPart <= (size_t)kWgBlocks * kWgPartMax, "head partials fit wpart");
 struct HwArgs {
@@ -1228,36 +1243,59 @@ struct HwArgs {
 };
 
 __global__ void __launch_bounds__(256) head_wgrad_kernel(HwArgs a) {
-  __shared__ float red[73 * 4];
-  float s[73];
+  __shared__ float part[256][37];   // the threads' sums (odd row stride: conflict-free)
+  float s[37];   // [c][tap] for channels 4 h + c, then (h = 0) the bias sum
 #pragma unroll
-  for (int i = 0; i < 73; ++i) s[i] = 0.f;
+  for (int i = 0; i < 37; ++i) s[i] = 0.f;
   const uint32_t HW = (uint32_t)a.H * (uint32_t)a.W, W = (uint32_t)a.W;
-  const uint32_t n = (uint32_t)a.nplanes * (uint32_t)a.B * HW;
+  const uint32_t n = 2u * (uint32_t)a.B * HW;
+  const uint32_t h = threadIdx.x & 1u;
   for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < n; t += gridDim.x * 256u) {
-    const uint32_t kb = t / HW, p = t - kb * HW;
-    const int b = (int)(kb % (uint32_t)a.B), k = (int)(kb / (uint32_t)a.B);
+    const uint32_t bp = t >> 1, b = bp / HW, p = bp - b * HW;
     const int y = (int)(p / W), x = (int)(p - (uint32_t)y * W);
-    const float g = a.gcost[((size_t)b * a.D + a.d0 + k) * HW + p];
-    const float* hb = a.h4 + (size_t)k * a.hstride + (size_t)b * HW * 8;
+    uint32_t off[9];
+    unsigned ok = 0u;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int qy = y + tap / 3 - 1, qx = x + tap % 3 - 1;
-      if (qy >= 0 && qy < a.H && qx >= 0 && qx < a.W) {
-        const float4* hv = reinterpret_cast<const float4*>(hb + ((size_t)qy * a.W + qx) * 8);
-        const float4 q0 = hv[0], q1 = hv[1];
-        const float hh[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-#pragma unroll
-        for (int ci = 0; ci < 8; ++ci) s[ci * 9 + tap] = fmaf(g, hh[ci], s[ci * 9 + tap]);
-      }
+      if (qy >= 0 && qy < a.H && qx >= 0 && qx < a.W) ok |= 1u << tap;
+      const int cy = min(max(qy, 0), a.H - 1), cx = min(max(qx, 0), a.W - 1);
+      off[tap] = ((uint32_t)cy * W + (uint32_t)cx) * 8u + 4u * h;
     }
-    s[72] += g;
-  }
-  block_sum<73>(s, red);
-  if (threadIdx.x == 0) {
-    float* wp = a.wpart + (size_t)blockIdx.x * kHwPart;
+    const float* gp = a.gcost + ((size_t)b * a.D + a.d0) * HW + p;
+    const float* hb = a.h4 + (size_t)b * HW * 8;
+#pragma unroll 1
+    for (int k = 0; k < a.nplanes; ++k) {
+      const float g = gp[(size_t)k * HW];
+      const float* hk = hb + (size_t)k * a.hstride;
 #pragma unroll
-    for (int i = 0; i < 73; ++i) wp[i] = s[i];
+      for (int tap = 0; tap < 9; ++tap) {
+        const float4 q = *reinterpret_cast<const float4*>(hk + off[tap]);
+        const float gt = (ok >> tap) & 1u ? g : 0.f;
+        s[0 * 9 + tap] = fmaf(gt, q.x, s[0 * 9 + tap]);
+        s[1 * 9 + tap] = fmaf(gt, q.y, s[1 * 9 + tap]);
+        s[2 * 9 + tap] = fmaf(gt, q.z, s[2 * 9 + tap]);
+        s[3 * 9 + tap] = fmaf(gt, q.w, s[3 * 9 + tap]);
+      }
+      s[36] += h ? 0.f : g;
+    }
+  }
+  // block reduce in LDS, in a fixed order: sum t of this block's threads of parity hh for sum i
+  // (a register butterfly over 73 values took the kernel to 256 VGPRs, one wave per SIMD)
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 37; ++i) part[threadIdx.x][i] = s[i];
+  __syncthreads();
+  if (threadIdx.x < 74) {
+    const int hh = threadIdx.x / 37, i = threadIdx.x - 37 * hh;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int t = hh; t < 256; t += 2) acc += part[t][i];
+    float* wp = a.wpart + (size_t)blockIdx.x * kHwPart;
+    if (i < 36)
+      wp[36 * hh + i] = acc;   // [ci = 4 hh + i / 9][tap = i % 9]
+    else if (hh == 0)
+      wp[72] = acc;            // the bias sum (lanes of parity 0 hold it)
   }
 }
 
@@ -1785,7 +1823,7 @@ hipError_t bptt_regulariser(const BpttRun& r, hipStream_t s) {
       a.wpart = L.wpart;
       {
         ProfScope ps(s, K_HEAD_WGRAD);
-        if ((size_t)n * B * H * W >= (1ull << 31)) return hipErrorInvalidValue;   // 32-bit indices
+        if ((size_t)2 * B * H * W >= (1ull << 31)) return hipErrorInvalidValue;   // 32-bit indices
         hipLaunchKernelGGL(head_wgrad_kernel, dim3(kHwBlocks), dim3(256), 0, s, a);
       }
       CK(hipGetLastError());
