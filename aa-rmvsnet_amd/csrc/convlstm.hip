@@ -1182,6 +1182,19 @@ __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__
   const int tiles_x = (W + kHeadTW - 1) / kHeadTW;
   const int y0 = (blockIdx.x / tiles_x) * kHeadTH, x0 = (blockIdx.x % tiles_x) * kHeadTW;
   const float* hb = h4 + (size_t)b * 8 * HW;
+  // this thread's pixel and its WTA state, loaded with the tile (one memory round trip, not a
+  // second one after the conv)
+  const int ty = threadIdx.x / kHeadTW, tx = threadIdx.x % kHeadTW;
+  const int y = y0 + ty, x = x0 + tx;
+  const bool own = y < H && x < W;
+  const int p = own ? y * W + x : 0;
+  const size_t q = (size_t)b * HW + p;
+  float mp = 0.f, dp = 0.f, es = 0.f;
+  if (wta && own) {
+    mp = max_prob[q];
+    dp = depth[q];
+    es = exp_sum[q];
+  }
   for (int rem = threadIdx.x; rem < NPX; rem += 256) {
     const int yy = y0 - 1 + rem / TW2, xx = x0 - 1 + rem % TW2;
     float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
@@ -1194,15 +1207,12 @@ __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__
     t[rem][1] = q1;
   }
   __syncthreads();
-  const int ty = threadIdx.x / kHeadTW, tx = threadIdx.x % kHeadTW;
-  const int y = y0 + ty, x = x0 + tx;
-  if (y >= H || x >= W) return;
-  const int p = y * W + x;
+  if (!own) return;
   float v[9][8];
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
-    const int q = (ty + tap / 3) * TW2 + tx + tap % 3;
-    const float4 a0 = t[q][0], a1 = t[q][1];
+    const int qt = (ty + tap / 3) * TW2 + tx + tap % 3;
+    const float4 a0 = t[qt][0], a1 = t[qt][1];
     v[tap][0] = a0.x; v[tap][1] = a0.y; v[tap][2] = a0.z; v[tap][3] = a0.w;
     v[tap][4] = a1.x; v[tap][5] = a1.y; v[tap][6] = a1.z; v[tap][7] = a1.w;
   }
@@ -1214,8 +1224,6 @@ __global__ void __launch_bounds__(256) head_wta_kernel(const float* __restrict__
   const float cost = acc + bias[0];
   if (cost_out) cost_out[((size_t)b * D + d) * HW + p] = cost;
   if (wta) {
-    const size_t q = (size_t)b * HW + p;
-    float mp = max_prob[q], dp = depth[q], es = exp_sum[q];
     wta_select(cost, dvals[b * D + d], mp, dp, es);
     max_prob[q] = mp;
     depth[q] = dp;
