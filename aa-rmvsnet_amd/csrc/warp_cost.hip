@@ -757,7 +757,11 @@ struct OmegaTile {
   static int tiles(int H, int W) { return ((W + OUTW - 1) / OUTW) * ((H + OUTH - 1) / OUTH); }
   __device__ static int tiles_d(int H, int W) { return ((W + OUTW - 1) / OUTW) * ((H + OUTH - 1) / OUTH); }
 };
-constexpr int kOmegaTW = 16;   // the library's tile width
+// the library's tile width (AARMVS_OMEGA_TW = 32: 16 x 32 haloed tiles, 512 threads; A/B builds)
+#ifndef AARMVS_OMEGA_TW
+#define AARMVS_OMEGA_TW 16
+#endif
+constexpr int kOmegaTW = AARMVS_OMEGA_TW;
 
 // ABL: ablation bits for the diagnostic harness only (tools/microbench/pipe_bench.cpp; the
 // library instantiates ABL = 0): 1 no MFMAs, 2 no box DMA, 4 no box sampling, 8 no reference
@@ -826,7 +830,7 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   using T = OmegaTile<TW>;
   constexpr int kMThreads = T::NT, kMBoxPx = T::BOXPX, kMOutH = T::OUTH, kMOutW = T::OUTW;
   constexpr int NB = (2 * kMBoxPx + kMThreads - 1) / kMThreads;   // box pieces per thread
-  static_assert(TW == 16, "the row sums shift along 16-lane DPP rows: one haloed row each");
+  static_assert(TW == 16 || TW == 32, "the row sums shift by DPP along one haloed row");
   // LDS: chunk c's source box and reference pixels, then (after the last chunk) the row-sum
   // images zm, zp (16 B per haloed pixel each)
   constexpr int kRefFl = (kMBoxPx + 1) * 8;
@@ -1056,12 +1060,15 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   //   Z_dy[q] = Y(dy,-1)[q - 1] + Y(dy,0)[q] + Y(dy,+1)[q + 1]          (row_shr / row_shl)
   //   Z_0[q]  = Y(0,-1)[q - 1] + Y(0,+1)[q + 1]
   //   t1[p]   = Z_-1[p - TW] + Z_0[p] + Z_+1[p + TW]                    (via LDS: other waves)
-  // (the edge lanes of a row get zeros from the DPP bound: they are halo pixels, never output)
+  // (the edge lanes of a row get zeros from the DPP bound: they are halo pixels, never output).
+  // TW = 32: a haloed row is a lane half, two DPP rows; wave_shr / wave_shl shift across them,
+  // and the lanes a shift carries across a half or the wave's end are halo columns too.
+  static constexpr int kShr = TW == 16 ? 0x111 : 0x138, kShl = TW == 16 ? 0x101 : 0x130;
   auto shr1 = [](float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xF, 0xF, true));
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), kShr, 0xF, 0xF, true));
   };
   auto shl1 = [](float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x101, 0xF, 0xF, true));
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), kShl, 0xF, 0xF, true));
   };
   float zmr[4], zpr[4], z0[4];
 #pragma unroll
