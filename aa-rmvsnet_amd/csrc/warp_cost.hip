@@ -1128,7 +1128,7 @@ __device__ __forceinline__ void omega_item(PA& a, const float* __restrict__ P,
   }
 }
 
-// The kernel: a block takes a.omega_ipb consecutive items (default 1).  A tile's (view, plane)
+// The kernel: a block takes a.omega_ipb consecutive items (omega_ipb()).  A tile's (view, plane)
 // items are consecutive on one XCD (xcd_tile): the reference tile, and a view's source box
 // across the npl neighbouring planes, come from its L2.
 // (AARMVS_OMEGA_WAVES: the minimum waves per SIMD the compiler is held to; A/B builds only)
@@ -1329,7 +1329,9 @@ static int pipe_box_cap() {
 static int omega_ipb(int items, int cu_count) {
   const char* s = std::getenv("AARMVS_OMEGA_IPB");
   if (s && *s) return std::max(1, std::min(8, std::atoi(s)));
-  int ipb = 4;
+  // 8 items per block where the grid stays >= 8 blocks per CU (round 6, second session: 7.58-7.61
+  // against 7.65-7.67 ms per headline launch at 4, profiles/r06s14_omega_ipb.txt)
+  int ipb = 8;
   while (ipb > 1 && (items + ipb - 1) / ipb < 8 * std::max(1, cu_count)) ipb >>= 1;
   return ipb;
 }

@@ -202,7 +202,7 @@ def test_pipeline_box_fallbacks_are_bit_identical(monkeypatch, cap):
 @pytest.mark.parametrize("ipb", ["1", "3", "8"])
 def test_omega_items_per_block_are_bit_identical(monkeypatch, ipb):
     """AARMVS_OMEGA_IPB sets how many consecutive (plane) items of one (tile, view) an
-    omega_conv block walks (default: 4, fewer on small grids).  The items' arithmetic is
+    omega_conv block walks (default: 8, fewer on small grids).  The items' arithmetic is
     unchanged, so the sweep must be bit-identical; D = 6 leaves a ragged last block."""
     B, N, H, W, D = 2, 3, 64, 96, 6
     sc = syn.scene(B, N, H, W, D, seed=11)
